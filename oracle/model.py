@@ -1,0 +1,228 @@
+"""CPU restatement of the reference GPT forward / generate — TEST INFRASTRUCTURE ONLY (oracle/__init__.py).
+
+A functional (no nn.Module) restatement over a state dict carrying the reference's parameter names.
+Every function cites the reference code it follows. ``dtype`` selects the activation/parameter dtype
+the reference would run in (fp32 for the CPU config; bf16 to mirror ``--precision bf16-true``): the
+op-by-op promotions (fp32 RMSNorm, fp32 RoPE products, dtype casts) are those of the reference.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional
+
+import numpy as np
+import torch
+import torch.nn.functional as F
+
+
+def find_multiple(n: int, k: int) -> int:  # lit_gpt/utils.py:74-78
+    assert k > 0
+    return n if n % k == 0 else n + k - n % k
+
+
+def build_rope_cache(seq_len: int, n_elem: int, base: int = 10000, condense_ratio: int = 1,
+                     pos_dtype: torch.dtype = torch.float32):
+    """lit_gpt/model.py:746-764. ``pos_dtype`` is the default dtype the reference runs
+    ``torch.arange(seq_len) / condense_ratio`` in (fp32 on CPU; bf16 under ``fabric.init_tensor()``
+    with bf16-true — the "bf16 RoPE position quirk" of SURVEY §7)."""
+    theta = 1.0 / (base ** (torch.arange(0, n_elem, 2, dtype=torch.float32) / n_elem))
+    seq_idx = torch.arange(seq_len, dtype=pos_dtype) / condense_ratio
+    idx_theta = torch.outer(seq_idx, theta).repeat(1, 2)
+    return torch.cos(idx_theta), torch.sin(idx_theta)
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """rotate-half RoPE in promoted precision, cast back (lit_gpt/model.py:767-773)."""
+    half = x.size(-1) // 2
+    rotated = torch.cat((-x[..., half:], x[..., :half]), dim=-1)
+    return ((x * cos) + (rotated * sin)).to(x.dtype)
+
+
+def rms_norm(x: torch.Tensor, w: torch.Tensor, eps: float) -> torch.Tensor:
+    """fp32 math, weight multiply in promoted dtype, one cast back (lit_gpt/rmsnorm.py:19-25)."""
+    xf = x.float()
+    normed = xf * torch.rsqrt(torch.mean(xf * xf, dim=-1, keepdim=True) + eps)
+    return (w * normed).to(x.dtype)
+
+
+def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) -> torch.Tensor:
+    """torch.nn.LayerNorm (lit_gpt/config.py:137-144 norm_class for GPT-NeoX)."""
+    return F.layer_norm(x, (x.size(-1),), w, b, eps)
+
+
+def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    return F.linear(x, w, b)
+
+
+@dataclass
+class Cache:
+    """Per-layer K/V for positions written so far (lit_gpt/model.py:776-799); stored un-expanded (G heads)."""
+    k: List[torch.Tensor] = field(default_factory=list)  # (G, S, hs) per layer
+    v: List[torch.Tensor] = field(default_factory=list)
+
+
+class OracleGPT:
+    """Functional restatement of GPT/Block/CausalSelfAttention/MLPs (lit_gpt/model.py:445-743)."""
+
+    def __init__(self, cfg, sd: Dict[str, np.ndarray], dtype: torch.dtype = torch.float32,
+                 weight_override: Optional[Callable[[str, np.ndarray], np.ndarray]] = None,
+                 rope_pos_dtype: torch.dtype = torch.float32):
+        self.cfg = cfg
+        self.dtype = dtype
+        self.p: Dict[str, torch.Tensor] = {}
+        for k, v in sd.items():
+            if weight_override is not None:
+                v = weight_override(k, v)
+            self.p[k] = torch.from_numpy(np.ascontiguousarray(v)).to(dtype)
+        self.rope_pos_dtype = rope_pos_dtype
+        self.max_seq_length = cfg.block_size
+        self.cache: Optional[Cache] = None
+
+    # GPT.max_seq_length setter + rope cache (model.py:466-484, 525-532)
+    def set_kv_cache(self, max_seq_length: int) -> None:
+        if max_seq_length > self.cfg.block_size:
+            raise ValueError(f"Cannot attend to {max_seq_length}, block size is only {self.cfg.block_size}")
+        self.max_seq_length = max_seq_length
+        self.cos, self.sin = build_rope_cache(max_seq_length, self.cfg.rope_n_elem, self.cfg.rope_base,
+                                              self.cfg.rope_condense_ratio, self.rope_pos_dtype)
+        c = self.cfg
+        S = max_seq_length
+        self.cache = Cache(
+            k=[torch.zeros(c.n_query_groups, S, c.head_size, dtype=self.dtype) for _ in range(c.n_layer)],
+            v=[torch.zeros(c.n_query_groups, S, c.head_size, dtype=self.dtype) for _ in range(c.n_layer)])
+
+    def _norm(self, prefix: str, x: torch.Tensor) -> torch.Tensor:
+        c = self.cfg
+        if c._norm_class == "RMSNorm":
+            return rms_norm(x, self.p[f"{prefix}.weight"], c.norm_eps)
+        return layer_norm(x, self.p[f"{prefix}.weight"], self.p[f"{prefix}.bias"], c.norm_eps)
+
+    def _lin(self, prefix: str, x: torch.Tensor) -> torch.Tensor:
+        return linear(x, self.p[f"{prefix}.weight"], self.p.get(f"{prefix}.bias"))
+
+    def _attn(self, i: int, x: torch.Tensor, cos, sin, input_pos: Optional[torch.Tensor]) -> torch.Tensor:
+        """CausalSelfAttention.forward (model.py:609-656) + SDPA (:658-665)."""
+        c = self.cfg
+        T = x.size(0)
+        G, hs, H = c.n_query_groups, c.head_size, c.n_head
+        qpk = H // G
+        qkv = self._lin(f"transformer.h.{i}.attn.attn", x).view(T, G, qpk + 2, hs)
+        q = qkv[:, :, :qpk].reshape(T, H, hs).transpose(0, 1)  # (H, T, hs)
+        k = qkv[:, :, qpk].transpose(0, 1)  # (G, T, hs)
+        v = qkv[:, :, qpk + 1].transpose(0, 1)
+        n = c.rope_n_elem
+        q = torch.cat((apply_rope(q[..., :n], cos, sin), q[..., n:]), dim=-1)
+        k = torch.cat((apply_rope(k[..., :n], cos, sin), k[..., n:]), dim=-1)
+        if input_pos is not None:
+            if self.cache is None:
+                raise TypeError("You need to call `gpt.set_kv_cache()`")
+            self.cache.k[i][:, input_pos] = k
+            self.cache.v[i][:, input_pos] = v
+            L = int(input_pos.max()) + 1  # keys beyond the last written position are masked out
+            kk, vv = self.cache.k[i][:, :L], self.cache.v[i][:, :L]
+            allowed = torch.arange(L)[None, :] <= input_pos[:, None]  # (T, L) = mask_cache rows
+        else:
+            kk, vv = k, v
+            allowed = torch.ones(T, T, dtype=torch.bool).tril()
+        kk = kk.repeat_interleave(qpk, dim=0)  # expand groups to heads (model.py:633-635)
+        vv = vv.repeat_interleave(qpk, dim=0)
+        scale = 1.0 / math.sqrt(hs)
+        att = (q.float() @ kk.float().transpose(-1, -2)) * scale
+        att = att.masked_fill(~allowed, float("-inf"))
+        att = torch.softmax(att, dim=-1)
+        y = (att @ vv.float()).to(self.dtype)  # (H, T, hs)
+        y = y.transpose(0, 1).reshape(T, H * hs)
+        return self._lin(f"transformer.h.{i}.attn.proj", y)
+
+    def _mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:
+        c = self.cfg
+        p = f"transformer.h.{i}.mlp"
+        if c._mlp_class == "LLaMAMLP":  # model.py:712-716
+            return self._lin(f"{p}.proj", F.silu(self._lin(f"{p}.fc_1", x)) * self._lin(f"{p}.fc_2", x))
+        if c._mlp_class == "GptNeoxMLP":  # model.py:699-702
+            return self._lin(f"{p}.proj", F.gelu(self._lin(f"{p}.fc", x), approximate=c.gelu_approximate))
+        if c._mlp_class == "LLaMAMoE":  # model.py:727-743
+            router = self._lin(f"{p}.gate", x)
+            probs, idx = torch.topk(router, c.n_expert_per_token)
+            probs = probs.softmax(dim=1, dtype=torch.float).to(x.dtype)
+            y = torch.zeros_like(x)
+            for e in range(c.n_expert):
+                tok, slot = torch.where(idx == e)
+                if tok.numel() == 0:
+                    continue
+                xe = x[tok]
+                ye = self._lin(f"{p}.experts.{e}.proj",
+                               F.silu(self._lin(f"{p}.experts.{e}.fc_1", xe)) * self._lin(f"{p}.experts.{e}.fc_2", xe))
+                y[tok] += probs[tok, slot, None] * ye
+            return y
+        raise NotImplementedError(c._mlp_class)
+
+    def forward(self, idx: torch.Tensor, input_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """GPT.forward (model.py:499-519) for B=1: idx (T,) int -> logits (T, V) in ``dtype``."""
+        c = self.cfg
+        T = idx.numel()
+        if self.max_seq_length < T:
+            raise ValueError(f"Cannot forward sequence of length {T}, max seq length is only {self.max_seq_length}.")
+        if input_pos is not None:
+            if self.cache is None:
+                raise TypeError("You need to call `gpt.set_kv_cache()`")
+            cos, sin = self.cos[input_pos], self.sin[input_pos]
+        else:
+            cos, sin = build_rope_cache(T, c.rope_n_elem, c.rope_base, c.rope_condense_ratio, self.rope_pos_dtype)
+        x = self.p["transformer.wte.weight"][idx.long()]
+        for i in range(c.n_layer):
+            pre = f"transformer.h.{i}"
+            n1 = self._norm(f"{pre}.norm_1", x)
+            h = self._attn(i, n1, cos, sin, input_pos)
+            if c.parallel_residual:  # Block.forward model.py:580-593
+                n2 = n1 if c.shared_attention_norm else self._norm(f"{pre}.norm_2", x)
+                x = self._mlp(i, n2) + h + x
+            else:
+                if c.shared_attention_norm:
+                    raise NotImplementedError("non-parallel residual and shared attention norm")
+                x = h + x
+                x = self._mlp(i, self._norm(f"{pre}.norm_2", x)) + x
+        x = self._norm("transformer.ln_f", x)
+        return self._lin("lm_head", x)
+
+
+def sample(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] = None,
+           multinomial: Optional[Callable[[torch.Tensor], torch.Tensor]] = None) -> torch.Tensor:
+    """generate/base.py:30-41 on the last row of (T, V) logits; returns (1,) int64."""
+    logits = logits[-1]
+    if top_k is not None:
+        v, i = torch.topk(logits, min(top_k, logits.size(-1)))
+        logits = torch.full_like(logits, float("-inf")).scatter_(-1, i, v)
+    if temperature > 0.0:
+        probs = torch.softmax(logits / temperature, dim=-1)
+        return (multinomial or (lambda p: torch.multinomial(p, num_samples=1)))(probs)
+    return torch.argmax(logits, dim=-1, keepdim=True)
+
+
+def generate(model: OracleGPT, prompt: torch.Tensor, max_returned_tokens: int, *, temperature: float = 1.0,
+             top_k: Optional[int] = None, eos_id: Optional[int] = None,
+             multinomial=None, record_logits: Optional[list] = None) -> torch.Tensor:
+    """generate/base.py:50-93: prefill at arange(T), then single-token steps at input_pos = T, T+1, ..."""
+    T = prompt.numel()
+    assert max_returned_tokens > T
+    if model.max_seq_length < max_returned_tokens - 1:
+        raise NotImplementedError(f"max_seq_length {model.max_seq_length} needs to be >= {max_returned_tokens - 1}")
+    tokens = [prompt]
+    logits = model.forward(prompt, torch.arange(T))
+    if record_logits is not None:
+        record_logits.append(logits[-1].float().clone())
+    token = sample(logits, temperature, top_k, multinomial).to(prompt.dtype)
+    tokens.append(token)
+    pos = T
+    for _ in range(2, max_returned_tokens - T + 1):
+        logits = model.forward(token.view(-1), torch.tensor([pos]))
+        if record_logits is not None:
+            record_logits.append(logits[-1].float().clone())
+        token = sample(logits, temperature, top_k, multinomial).to(prompt.dtype)
+        tokens.append(token)
+        if eos_id is not None and int(token) == eos_id:
+            break
+        pos += 1
+    return torch.cat(tokens)
