@@ -1,0 +1,271 @@
+"""Decode benchmark: Llama-2-7B int4-g128, single-stream greedy decode at context 2048 (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+N > 1 is launched by the driver as ``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...``
+and runs tensor parallelism (generate/tp.py sharding, RCCL all-reduce): one stream, so ``value`` is that stream's
+tokens/s (whole job) and scaling is "strong".
+
+A "step" = one decode token: one replay of the captured HIP graph (32 blocks + lm_head + argmax) at positions
+2048 + W ... 2048 + W + K - 1 after a 2048-token synthetic prefill. Inputs (weights, KV cache, token, position)
+are resident in HBM before the timed region. Timed region: barrier + synchronize, K replays, synchronize +
+barrier; the max over ranks is reported.
+
+Extra objects in the JSON line:
+  roofline      the dominant kernel (fused RMSNorm + fc_1/fc_2 int4 GEMV + SwiGLU of one block, 46.5 MB of
+                algorithmic bytes per launch) timed with HIP events on the launch stream; peak 8 TB/s
+  step_roofline the whole decode step: algorithmic bytes per token (weights + KV read/write) x tok/s
+  cpu_baseline  the CPU oracle (restatement of the reference's bf16 math) timed on this host on a bounded sample
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+import torch
+
+REPO = Path(__file__).resolve().parent
+for _p in (str(REPO / "lit-gpt_amd"), str(REPO)):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+MODEL = "Llama-2-7b-hf"
+PROMPT_LEN = 2048
+
+
+def algorithmic_bytes_per_token(cfg, pos: float, group: int = 128, tp: int = 1) -> float:
+    """Weights (all Linears incl. lm_head, int4 + bf16 group scale) + norms + embedding row + KV read/write,
+    per rank (SURVEY §8d formula)."""
+    C, V, L = cfg.n_embd, cfg.padded_vocab_size, cfg.n_layer
+    qkv = (cfg.n_head + 2 * cfg.n_query_groups) * cfg.head_size
+    per_layer = qkv * C + C * C + 3 * cfg.intermediate_size * C
+    bw = 0.5 + 2.0 / group
+    weights = (L * per_layer / tp + V * C) * bw
+    norms = (2 * L + 1) * C * 2
+    kv = 2 * L * (cfg.n_query_groups / tp) * cfg.head_size * 2 * (pos + 1) + 2 * L * (cfg.n_query_groups / tp) * cfg.head_size * 2
+    return weights + norms + C * 2 + kv
+
+
+def time_dominant_kernel(model, reps: int = 50):
+    """Average duration of the fused RMSNorm + SwiGLU GEMV of block 0 with HIP events on its launch stream."""
+    from lit_gpt import ops
+
+    blk = model.transformer.h[0]
+    f1, f2 = blk.mlp.fc_1, blk.mlp.fc_2
+    C = f1.in_features
+    x = torch.randn(C, device="cuda").to(torch.bfloat16)
+    out = torch.empty(f1.out_features, dtype=torch.bfloat16, device="cuda")
+    stream = torch.cuda.current_stream()
+
+    def launch():
+        ops.q4_gemv_swiglu(x, f1.qweight, f1.scales, f2.qweight, f2.scales, f1.out_features, C, f1.group, f1.fmt,
+                           norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps, out=out)
+
+    for _ in range(5):
+        launch()
+    # flush caches between launches so each reads its weights from HBM as in the decode step
+    flush = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.float32, device="cuda")
+    times = []
+    for _ in range(reps):
+        flush.zero_()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record(stream)
+        launch()
+        e.record(stream)
+        e.synchronize()
+        times.append(s.elapsed_time(e))
+    times.sort()
+    avg_ms = sum(times) / len(times)
+    nbytes = 2 * f1.qweight.numel() + 2 * f1.scales.numel() * f1.scales.element_size() + 2 * C * 2 + f1.out_features * 2
+    return avg_ms, nbytes
+
+
+def cpu_baseline(cfg, threads: int, seconds: float = 15.0):
+    """The oracle (CPU restatement of the reference's bf16 decode math) on a bounded sample: 2 of the 32 blocks
+    at full Llama-2-7B width + lm_head, KV context 2048, repeated decode steps; per-token time extrapolated to
+    all 32 blocks."""
+    from oracle import model as om
+
+    torch.set_num_threads(threads)
+    small = type(cfg)(**{**{k: getattr(cfg, k) for k in cfg.__dataclass_fields__}, "n_layer": 2})
+    g = torch.Generator().manual_seed(0)
+    sd = {}
+    from oracle import synth
+
+    for name, shape, kind in synth.param_shapes(small):
+        if kind == "normal":
+            sd[name] = (torch.randn(shape, generator=g) * 0.02).numpy()
+        else:
+            sd[name] = torch.ones(shape).numpy() if kind == "ones" else torch.zeros(shape).numpy()
+    m = om.OracleGPT(small, sd, dtype=torch.bfloat16)
+    del sd
+    S = PROMPT_LEN + 64
+    m.set_kv_cache(S)
+    for i in range(2):  # fill a 2048-long context cheaply (random K/V; attention cost is what matters)
+        m.cache.k[i][:, :PROMPT_LEN] = torch.randn(small.n_query_groups, PROMPT_LEN, small.head_size).bfloat16()
+        m.cache.v[i][:, :PROMPT_LEN] = torch.randn(small.n_query_groups, PROMPT_LEN, small.head_size).bfloat16()
+    tok = torch.tensor([1])
+    with torch.inference_mode():
+        m.forward(tok, torch.tensor([PROMPT_LEN]))  # warm-up
+        t_layers, t_head, n = 0.0, 0.0, 0
+        t_start = time.perf_counter()
+        pos = PROMPT_LEN + 1
+        while time.perf_counter() - t_start < seconds and pos < S:
+            t0 = time.perf_counter()
+            m.forward(tok, torch.tensor([pos]))
+            t_layers += time.perf_counter() - t0
+            n += 1
+            pos += 1
+        # lm_head + final norm share of one forward (measured separately so the 2->32 block scaling is exact)
+        x = torch.randn(1, small.n_embd).bfloat16()
+        t0 = time.perf_counter()
+        for _ in range(n):
+            m._lin("lm_head", m._norm("transformer.ln_f", x))
+        t_head = (time.perf_counter() - t0) / n
+    per_fwd = t_layers / n
+    per_block = (per_fwd - t_head) / 2
+    per_token = per_block * cfg.n_layer + t_head
+    return {"value": round(1.0 / per_token, 3), "unit": "tokens/s", "cores": threads, "kind": "port",
+            "sample": f"oracle bf16 decode, {n} steps at context ~{PROMPT_LEN} over 2 of {cfg.n_layer} "
+                      f"Llama-2-7B blocks + lm_head, extrapolated to {cfg.n_layer} blocks "
+                      f"({per_token * 1e3:.1f} ms/token)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--quantize", default="int4-g128")
+    ap.add_argument("--prompt_len", type=int, default=PROMPT_LEN)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    import torch.distributed as dist
+
+    from generate import tp as gtp
+    from generate.base import build_model
+    from lit_gpt import Config
+    from lit_gpt.runtime import DecodeGraph
+
+    fabric = gtp.init_distributed()
+    world, rank = fabric.world_size, fabric.global_rank
+    dev = torch.device("cuda", torch.cuda.current_device())
+    cfg = Config.from_name(MODEL)
+    T = args.prompt_len
+    max_seq = T + args.warmup + args.steps + 2
+    t0 = time.perf_counter()
+    from functools import partial
+
+    model = build_model(cfg, quantize=args.quantize, device=dev, max_seq_length=max_seq,
+                        tp=partial(gtp.tensor_parallel, fabric) if world > 1 else None)
+    load_s = time.perf_counter() - t0
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    prompt = torch.randint(0, cfg.vocab_size, (T,), generator=g, dtype=torch.int32).to(dev)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    with torch.inference_mode():
+        # prefill (reference-style tok/s includes it; reported separately)
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        logits = model(prompt.view(1, -1), torch.arange(T, device=dev), last_token_only=True)
+        from lit_gpt import ops
+
+        first = ops.argmax(logits.reshape(-1)).to(torch.int32)
+        torch.cuda.synchronize()
+        prefill_s = time.perf_counter() - t0
+        if args.no_graph:
+            from generate.base import next_token
+
+            tok = first.view(1, 1)
+            pos = torch.tensor([T], device=dev)
+
+            def step():
+                nonlocal tok
+                tok = next_token(model, pos, tok.view(1, 1), temperature=0.0)
+                pos.add_(1)
+        else:
+            dg = DecodeGraph(model, first, T)  # first decode step runs eagerly, then the step is captured
+
+            def step():
+                dg.step()
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        tok_s = args.steps / elapsed
+        ms_step = elapsed / args.steps * 1e3
+        avg_ms, kbytes = time_dominant_kernel(model)
+
+    cfg_full = Config.from_name(MODEL)
+    mean_pos = T + args.warmup + 1 + (args.steps - 1) / 2
+    step_bytes = algorithmic_bytes_per_token(cfg_full, mean_pos, tp=world)
+    step_gbs = step_bytes * tok_s / 1e9
+    kern_gbs = kbytes / (avg_ms * 1e-3) / 1e9
+    result = {
+        "metric": "decode tokens/s/GPU (Llama-2-7B int4, seq=2048) + % HBM roofline",
+        "value": round(tok_s, 2),
+        "unit": "tokens/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (random-init N(0,0.02) weights, uniform random prompt ids)",
+        "config": {"workload": "Llama-2-7B single-stream greedy decode after a 2048-token prefill",
+                   "weights": args.quantize, "prompt_len": T, "decode_positions": [T + args.warmup + 1,
+                                                                                   T + args.warmup + args.steps],
+                   "global_batch": 1, "seq_len": T, "parallelism": f"tp{world}",
+                   "graph": not args.no_graph},
+        "roofline": {"bound": "hbm", "kernel": "gemv_q4_kernel<.., DUAL> (RMSNorm+fc_1/fc_2+SwiGLU, block 0)",
+                     "achieved": round(kern_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(kern_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                     "bytes_per_launch": int(kbytes), "avg_launch_us": round(avg_ms * 1e3, 2)},
+        "step_roofline": {"bytes_per_token": int(step_bytes), "achieved": round(step_gbs, 1),
+                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(step_gbs / HBM_PEAK_GBS, 4),
+                          "roofline_tokens_per_s": round(HBM_PEAK_GBS * 1e9 / step_bytes, 1)},
+        "prefill_s": round(prefill_s, 4),
+        "reference_style_tokens_per_s": round((args.steps + args.warmup + 1) / (prefill_s + elapsed * (
+            args.steps + args.warmup + 1) / args.steps), 2),
+        "load_s": round(load_s, 2),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        try:
+            result["cpu_baseline"] = cpu_baseline(cfg_full, threads, args.cpu_seconds)
+        except Exception as e:  # the baseline is reported, never the target: do not lose the GPU number
+            result["cpu_baseline"] = {"error": repr(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

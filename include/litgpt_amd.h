@@ -1,0 +1,95 @@
+/*
+ * litgpt_amd.h — C ABI of liblitgpt_amd.so, the MI355X (gfx950) hot path of lit_gpt's quantized decode.
+ *
+ * Conventions: plain device pointers + sizes, no torch types; every buffer is caller-owned
+ * (kernels never allocate; scratch is passed in); all launches are asynchronous on `stream` (a hipStream_t;
+ * graph-capturable); return 0 on success, otherwise a hipError_t value with a message available from
+ * lga_last_error_string() (thread-local). bf16 tensors are raw uint16 bit patterns, row-major, contiguous.
+ *
+ * Reference interfaces replaced (file:line in /root/reference unless marked upstream):
+ *   - bitsandbytes 0.41.0 (requirements-all.txt:3; upstream, not in the reference tree) reached via Lightning's
+ *     BitsandbytesPrecision (generate/base.py:128-136, generate/tp.py:126-134,171,190): the ctypes C functions
+ *     cquantize_blockwise_bf16_nf4 / cdequantize_blockwise_bf16_nf4 / cgemm_4bit_inference_naive_bf16
+ *     (upstream names) behind Linear4bit.forward -> lga_quantize, lga_q4_gemv(_swiglu), lga_q4_gemm;
+ *   - the ATen kernels lit_gpt/model.py issues on the hot path -> the remaining entry points.
+ */
+#ifndef LITGPT_AMD_H
+#define LITGPT_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* lga_stream_t; /* == hipStream_t */
+
+/* weight formats */
+#define LGA_FMT_Q4G 0 /* int4, symmetric, per-group bf16 scale = bf16(absmax/7), nibble = q + 8 */
+#define LGA_FMT_NF4 1 /* bitsandbytes NF4 codebook, per-block fp32 absmax */
+
+/* -- plumbing ---------------------------------------------------------------------------------------- */
+const char* lga_last_error_string(void);
+int lga_version(void);
+int lga_device_info(int device, int* n_cu, char* arch_name, int arch_len);
+
+/* -- quantize at load (Lightning BitsandbytesPrecision.convert_module + bnb quantize on .to(device);
+ *    generate/base.py:168, generate/tp.py:171-190) ------------------------------------------------------
+ * w: (N, K) fp32 (w_is_bf16 = 0) or bf16 (1). qweight: (N, K/2) bytes, byte j = k 2j (low) | 2j+1 (high).
+ * scales: (N, K/group) bf16 for Q4G, fp32 for NF4. Layout spec: oracle/quant.py. */
+int lga_quantize(const void* w, int w_is_bf16, uint8_t* qweight, void* scales, int N, int K, int group, int fmt,
+                 lga_stream_t stream);
+
+/* -- decode GEMV, M = 1 (bnb gemv_4bit for one-token inputs; every Linear of lit_gpt/model.py:519,619,656,
+ *    712-716) -----------------------------------------------------------------------------------------------
+ * y[N] = x[K] . dequant(W)^T (+bias[N]) (+residual[N]); norm_weight != NULL applies RMSNorm
+ * (lit_gpt/rmsnorm.py:19-25, eps = norm_eps) to x first. variant < 0 = heuristic tile choice. */
+int lga_q4_gemv(const void* x, const uint8_t* qweight, const void* scales, const void* bias, const void* residual,
+                const void* norm_weight, float norm_eps, void* y, int N, int K, int group, int fmt, int variant,
+                lga_stream_t stream);
+/* y[N] = bf16(silu(bf16(x.W1^T))) * bf16(x.W2^T) — LLaMAMLP fc_1/fc_2 + silu*mul (lit_gpt/model.py:712-715) */
+int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const void* scales1, const uint8_t* qweight2,
+                       const void* scales2, const void* norm_weight, float norm_eps, void* y, int N, int K,
+                       int group, int fmt, int variant, lga_stream_t stream);
+
+/* -- prefill GEMM, M > 1 (bnb dequantize_4bit + cuBLAS GEMM) -------------------------------------------- */
+int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const void* bias, const void* residual,
+                void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
+
+/* -- row / elementwise ops ---------------------------------------------------------------------------- */
+/* RMSNorm over rows of n (lit_gpt/rmsnorm.py:19-25) */
+int lga_rmsnorm(const void* x, const void* weight, void* y, int rows, int n, float eps, lga_stream_t stream);
+/* RoPE (lit_gpt/model.py:641-644, 767-773) on the q and k slots of qkv (T, (H+2G)*hs) [per group g: q_per_kv
+ * q heads, k, v — scripts/convert_hf_checkpoint.py:174-188 layout], cos/sin rows rope_pos[t] of (rope_rows,
+ * rope_n_elem) fp32 tables; q_out (T, H, hs); k (roped) and v written to k_cache/v_cache (G, max_seq, hs) at row
+ * cache_pos[t] (KVCache.forward index_copy_, lit_gpt/model.py:788-795). */
+int lga_rope_kv_append(const void* qkv, void* q_out, void* k_cache, void* v_cache, const int64_t* cache_pos,
+                       const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, int T, int n_head,
+                       int n_query_groups, int head_size, int rope_n_elem, int max_seq, lga_stream_t stream);
+/* out[t] = table[idx[t]] (nn.Embedding, lit_gpt/model.py:515) */
+int lga_embedding(const void* idx, int idx_is_int64, const void* table, void* out, int T, int C, int V,
+                  lga_stream_t stream);
+/* y = bf16(a + b) (Block residual, lit_gpt/model.py:591-592) */
+int lga_add(const void* a, const void* b, void* y, long n, lga_stream_t stream);
+/* y = bf16(bf16(silu(a)) * b) (lit_gpt/model.py:715) */
+int lga_swiglu(const void* a, const void* b, void* y, long n, lga_stream_t stream);
+
+/* -- attention over the KV cache (SDPA with the input_pos mask rows, lit_gpt/model.py:651,658-665) --------
+ * q (T, H, hs); caches (G, max_seq, hs); query t attends keys 0..input_pos[t]; y (T, H*hs).
+ * n_splits > 1 splits the sequence (flash-decoding) and needs `workspace` of
+ * lga_attention_workspace_bytes(T, H, hs, n_splits) bytes. head_size in {64, 128}; H/G in {1,2,4,8}. */
+int lga_attention(const void* q, const void* k_cache, const void* v_cache, const int64_t* input_pos, void* y,
+                  float* workspace, int T, int n_head, int n_query_groups, int head_size, int max_seq, int n_splits,
+                  float scale, lga_stream_t stream);
+size_t lga_attention_workspace_bytes(int T, int n_head, int head_size, int n_splits);
+
+/* -- greedy sampling (generate/base.py:30-47 at temperature 0): lowest index among the maxima; optionally
+ *    writes the token (int32) and advances *pos_inout by one (generate/base.py:92) -------------------------- */
+int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
+               lga_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LITGPT_AMD_H */

@@ -1,0 +1,72 @@
+// Shared device helpers for the lit-gpt MI355X (gfx950) decode path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lga {
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+// ---- bf16 <-> f32 (bf16 stored as raw uint16_t; RNE on the way down, NaN kept a NaN) ----
+__device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
+__device__ __forceinline__ float bflo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bfhi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7FFFFFFFu) > 0x7F800000u) return (uint16_t)((u >> 16) | 0x40u);  // quiet NaN
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+__device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+// ---- wave-level reductions (64 lanes) ----
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+// sum over aligned groups of `W` lanes (W power of two <= 64)
+template <int W>
+__device__ __forceinline__ float group_sum(float v) {
+#pragma unroll
+  for (int o = W / 2; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// exact-order (no FMA contraction) helpers used where the reference's CPU math does mul then add
+__device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }
+__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
+
+__device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
+
+}  // namespace lga
+
+// error plumbing shared by every C entry point
+extern "C" void lga_set_error(const char* msg);
+
+#define LGA_CHECK_ARG(cond, msg)    \
+  do {                              \
+    if (!(cond)) {                  \
+      lga_set_error(msg);           \
+      return (int)hipErrorInvalidValue; \
+    }                               \
+  } while (0)
+
+#define LGA_LAUNCH_RETURN()                          \
+  do {                                               \
+    hipError_t e_ = hipGetLastError();               \
+    if (e_ != hipSuccess) {                          \
+      lga_set_error(hipGetErrorString(e_));          \
+      return (int)e_;                                \
+    }                                                \
+    return 0;                                        \
+  } while (0)

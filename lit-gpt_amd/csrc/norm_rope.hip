@@ -1,0 +1,148 @@
+// Row-wise and elementwise kernels of the decode/prefill step:
+//   lga_rmsnorm        RMSNorm (lit_gpt/rmsnorm.py:19-25): fp32 math, weight multiply in fp32, one bf16 cast
+//   lga_rope_kv_append RoPE on q,k (lit_gpt/model.py:641-644, apply_rope :767-773) fused with the KV-cache
+//                      write (KVCache.forward :788-795, index_copy_ at input_pos) — cache kept un-expanded
+//                      (n_query_groups heads) instead of the reference's expanded copy (:633-635, :675)
+//   lga_embedding      token-embedding gather (model.py:515)
+//   lga_add            bf16 residual add (Block.forward :591-592) when the add cannot ride a GEMV epilogue (TP)
+//   lga_swiglu         silu(a) * b with the reference's rounding points (LLaMAMLP.forward :715)
+#include "common.h"
+
+namespace lga {
+
+__global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                      uint16_t* __restrict__ y, int n, float eps) {
+  const size_t row = blockIdx.x;
+  const uint16_t* xr = x + row * n;
+  uint16_t* yr = y + row * n;
+  __shared__ float red[4];
+  float ss = 0.0f;
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float v = bf2f(xr[i]);
+    ss = fmaf(v, v, ss);
+  }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float rs = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)n + eps);
+  for (int i = threadIdx.x; i < n; i += 256) yr[i] = f2bf(__fmul_rn(bf2f(w[i]), __fmul_rn(bf2f(xr[i]), rs)));
+}
+
+// grid (T, G): one workgroup per (token, query group); slots 0..qpk-1 = q heads, qpk = k, qpk+1 = v
+__global__ void __launch_bounds__(256) rope_kv_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ q_out,
+                                                      uint16_t* __restrict__ k_cache, uint16_t* __restrict__ v_cache,
+                                                      const int64_t* __restrict__ cache_pos,
+                                                      const int64_t* __restrict__ rope_pos,
+                                                      const float* __restrict__ cos, const float* __restrict__ sin,
+                                                      int n_head, int n_groups, int hs, int n_elem, int max_seq,
+                                                      int rope_rows) {
+  const int t = blockIdx.x, g = blockIdx.y;
+  const int qpk = n_head / n_groups;
+  const long p = cache_pos[t];
+  const long rp = rope_pos[t];
+  if (p < 0 || p >= max_seq || rp < 0 || rp >= rope_rows) return;  // host validates; never go out of bounds
+  const uint16_t* src = qkv + ((size_t)t * (n_head + 2 * n_groups) + (size_t)g * (qpk + 2)) * hs;
+  const float* cr = cos + (size_t)rp * n_elem;
+  const float* sr = sin + (size_t)rp * n_elem;
+  const int half = n_elem / 2;
+  const int items = (qpk + 2) * hs;
+  for (int it = threadIdx.x; it < items; it += blockDim.x) {
+    const int slot = it / hs, d = it % hs;
+    const uint16_t* xs = src + (size_t)slot * hs;
+    uint16_t out = xs[d];
+    if (slot <= qpk && d < n_elem) {
+      const float x = bf2f(xs[d]);
+      const float r = d < half ? -bf2f(xs[d + half]) : bf2f(xs[d - half]);
+      out = f2bf(add_rn(mul_rn(x, cr[d]), mul_rn(r, sr[d])));
+    }
+    if (slot < qpk) {
+      q_out[((size_t)t * n_head + (size_t)g * qpk + slot) * hs + d] = out;
+    } else if (slot == qpk) {
+      k_cache[((size_t)g * max_seq + p) * hs + d] = out;
+    } else {
+      v_cache[((size_t)g * max_seq + p) * hs + d] = out;
+    }
+  }
+}
+
+template <typename IDX>
+__global__ void __launch_bounds__(256) embedding_kernel(const IDX* __restrict__ idx, const uint16_t* __restrict__ table,
+                                                        uint16_t* __restrict__ out, int C, int V) {
+  const int t = blockIdx.x;
+  long id = (long)idx[t];
+  id = id < 0 ? 0 : (id >= V ? V - 1 : id);  // host validates ids; clamp keeps the gather in bounds
+  const uint4* src = (const uint4*)(table + (size_t)id * C);
+  uint4* dst = (uint4*)(out + (size_t)t * C);
+  for (int i = threadIdx.x; i < C / 8; i += 256) dst[i] = src[i];
+}
+
+__global__ void __launch_bounds__(256) add_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ b,
+                                                  uint16_t* __restrict__ y, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+    y[i] = f2bf(bf2f(a[i]) + bf2f(b[i]));
+}
+
+__global__ void __launch_bounds__(256) swiglu_kernel(const uint16_t* __restrict__ a, const uint16_t* __restrict__ b,
+                                                     uint16_t* __restrict__ y, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const float g = round_bf(silu_f(bf2f(a[i])));
+    y[i] = f2bf(__fmul_rn(g, bf2f(b[i])));
+  }
+}
+
+static unsigned elementwise_grid(size_t n) {
+  size_t g = (n + 255) / 256;
+  return (unsigned)(g > 4096 ? 4096 : (g == 0 ? 1 : g));
+}
+
+}  // namespace lga
+
+extern "C" int lga_rmsnorm(const void* x, const void* weight, void* y, int rows, int n, float eps,
+                           hipStream_t stream) {
+  LGA_CHECK_ARG(x && weight && y && rows > 0 && n > 0, "lga_rmsnorm: bad arguments");
+  lga::rmsnorm_kernel<<<rows, 256, 0, stream>>>((const uint16_t*)x, (const uint16_t*)weight, (uint16_t*)y, n, eps);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_rope_kv_append(const void* qkv, void* q_out, void* k_cache, void* v_cache,
+                                  const int64_t* cache_pos, const int64_t* rope_pos, const float* cos,
+                                  const float* sin, int rope_rows, int T, int n_head, int n_query_groups,
+                                  int head_size, int rope_n_elem, int max_seq, hipStream_t stream) {
+  LGA_CHECK_ARG(qkv && q_out && k_cache && v_cache && cache_pos && rope_pos && (rope_n_elem == 0 || (cos && sin)),
+                "lga_rope_kv_append: null pointer");
+  LGA_CHECK_ARG(T > 0 && n_query_groups > 0 && n_head % n_query_groups == 0 && head_size > 0,
+                "lga_rope_kv_append: bad head geometry");
+  LGA_CHECK_ARG(rope_n_elem >= 0 && rope_n_elem <= head_size && rope_n_elem % 2 == 0,
+                "lga_rope_kv_append: rope_n_elem must be even and <= head_size");
+  const dim3 grid(T, n_query_groups);
+  lga::rope_kv_kernel<<<grid, 256, 0, stream>>>((const uint16_t*)qkv, (uint16_t*)q_out, (uint16_t*)k_cache,
+                                                (uint16_t*)v_cache, cache_pos, rope_pos, cos, sin, n_head,
+                                                n_query_groups, head_size, rope_n_elem, max_seq, rope_rows);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_embedding(const void* idx, int idx_is_int64, const void* table, void* out, int T, int C, int V,
+                             hipStream_t stream) {
+  LGA_CHECK_ARG(idx && table && out && T > 0 && C > 0 && C % 8 == 0 && V > 0, "lga_embedding: bad arguments");
+  if (idx_is_int64)
+    lga::embedding_kernel<int64_t><<<T, 256, 0, stream>>>((const int64_t*)idx, (const uint16_t*)table,
+                                                          (uint16_t*)out, C, V);
+  else
+    lga::embedding_kernel<int32_t><<<T, 256, 0, stream>>>((const int32_t*)idx, (const uint16_t*)table,
+                                                          (uint16_t*)out, C, V);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_add(const void* a, const void* b, void* y, long n, hipStream_t stream) {
+  LGA_CHECK_ARG(a && b && y && n > 0, "lga_add: bad arguments");
+  lga::add_kernel<<<lga::elementwise_grid(n), 256, 0, stream>>>((const uint16_t*)a, (const uint16_t*)b,
+                                                                 (uint16_t*)y, (size_t)n);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_swiglu(const void* a, const void* b, void* y, long n, hipStream_t stream) {
+  LGA_CHECK_ARG(a && b && y && n > 0, "lga_swiglu: bad arguments");
+  lga::swiglu_kernel<<<lga::elementwise_grid(n), 256, 0, stream>>>((const uint16_t*)a, (const uint16_t*)b,
+                                                                    (uint16_t*)y, (size_t)n);
+  LGA_LAUNCH_RETURN();
+}

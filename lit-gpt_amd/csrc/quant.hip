@@ -1,0 +1,88 @@
+// Load-time weight quantizer: (N, K) fp32/bf16 Linear weight -> packed int4 + per-group scale.
+//
+// Replaces the bitsandbytes quantize-on-device step that Lightning's BitsandbytesPrecision triggers on
+// `fabric.setup_module` / `fabric.to_device` (reference generate/base.py:168, generate/tp.py:190; bnb
+// `cquantize_blockwise_*_nf4`, upstream). Formats are specified byte-for-byte in oracle/quant.py:
+//   LGA_FMT_Q4G (0): symmetric int4, group G along K, scale = bf16(absmax / 7), nibble = q + 8
+//   LGA_FMT_NF4 (1): bnb NF4 codebook, block G along K, fp32 absmax
+// Packed byte j of a row holds k = 2j (low nibble) and k = 2j + 1 (high nibble).
+#include "common.h"
+
+namespace lga {
+
+__constant__ float kNF4[16] = {
+    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
+    -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
+    0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+    0.7229568362236023f, 1.0f};
+
+template <bool IN_BF16>
+__device__ __forceinline__ float load_w(const void* w, size_t i) {
+  if (IN_BF16) return bf2f(((const uint16_t*)w)[i]);
+  return ((const float*)w)[i];
+}
+
+// one thread per (row, group)
+template <bool IN_BF16, int FMT>
+__global__ void __launch_bounds__(256) quantize_kernel(const void* __restrict__ w, uint8_t* __restrict__ qw,
+                                                      void* __restrict__ scales, int N, int K, int G) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int groups = K / G;
+  if (gid >= (long)N * groups) return;
+  const int n = (int)(gid / groups), g = (int)(gid % groups);
+  const size_t base = (size_t)n * K + (size_t)g * G;
+  float amax = 0.0f;
+  for (int i = 0; i < G; ++i) amax = fmaxf(amax, fabsf(load_w<IN_BF16>(w, base + i)));
+  float inv;
+  if (FMT == 0) {
+    const uint16_t sb = f2bf(__fdiv_rn(amax, 7.0f));
+    ((uint16_t*)scales)[(size_t)n * groups + g] = sb;
+    const float s = bf2f(sb);
+    inv = s > 0.0f ? __fdiv_rn(1.0f, s) : 0.0f;
+  } else {
+    ((float*)scales)[(size_t)n * groups + g] = amax;
+    inv = amax > 0.0f ? __fdiv_rn(1.0f, amax) : 0.0f;
+  }
+  uint8_t* out = qw + ((size_t)n * K + (size_t)g * G) / 2;
+  for (int i = 0; i < G; i += 2) {
+    unsigned c[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const float v = __fmul_rn(load_w<IN_BF16>(w, base + i + h), inv);
+      if (FMT == 0) {
+        float q = rintf(v);
+        q = fminf(fmaxf(q, -8.0f), 7.0f);
+        c[h] = (unsigned)((int)q + 8);
+      } else {
+        unsigned code = 0;
+#pragma unroll
+        for (int j = 0; j < 15; ++j) {
+          const float mid = __fmul_rn(__fadd_rn(kNF4[j + 1], kNF4[j]), 0.5f);
+          code += (mid < v) ? 1u : 0u;
+        }
+        c[h] = code;
+      }
+    }
+    out[i / 2] = (uint8_t)(c[0] | (c[1] << 4));
+  }
+}
+
+}  // namespace lga
+
+extern "C" int lga_quantize(const void* w, int w_is_bf16, uint8_t* qweight, void* scales, int N, int K,
+                            int group, int fmt, hipStream_t stream) {
+  LGA_CHECK_ARG(w && qweight && scales, "lga_quantize: null pointer");
+  LGA_CHECK_ARG(N > 0 && K > 0 && group > 0 && group % 2 == 0 && K % group == 0,
+                "lga_quantize: K must be a positive multiple of an even group size");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_quantize: fmt must be 0 (int4-g) or 1 (nf4)");
+  const long total = (long)N * (K / group);
+  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  if (w_is_bf16) {
+    if (fmt == 0) lga::quantize_kernel<true, 0><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
+    else lga::quantize_kernel<true, 1><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
+  } else {
+    if (fmt == 0) lga::quantize_kernel<false, 0><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
+    else lga::quantize_kernel<false, 1><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
+  }
+  LGA_LAUNCH_RETURN();
+}

@@ -1,0 +1,70 @@
+// Greedy sampling on the device: argmax over the last row of logits (generate/base.py:30-41 with
+// temperature == 0; torch.argmax returns the first maximal index, so ties break to the LOWEST index).
+// Top-k masking never changes the arg-max (the maximal element is always inside the top-k set), so
+// `sample(..., top_k=k, temperature=0)` is this same kernel.
+//
+// The kernel also performs the decode loop's bookkeeping so the whole step stays on the GPU (and inside
+// one HIP graph): it writes the new token id (the `next.to(dtype=x.dtype)` of next_token, base.py:47) into
+// the token buffer the next step's embedding reads, and advances input_pos (`input_pos.add_(1)`, base.py:92).
+#include "common.h"
+
+namespace lga {
+
+// torch.argmax semantics: NaN compares greater than every number; among equals the lowest index wins
+__device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
+  const bool vn = v != v, bn = bv != bv;
+  if (vn || bn) return vn && (!bn || i < bi);
+  return (v > bv) || (v == bv && i < bi);
+}
+
+__global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict__ logits, int n,
+                                                      int64_t* __restrict__ out_idx, int32_t* __restrict__ token_out,
+                                                      int64_t* __restrict__ pos_inout) {
+  float bv = -INFINITY;
+  int bi = 0x7FFFFFFF;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const float v = bf2f(logits[i]);
+    if (better(v, i, bv, bi)) {
+      bv = v;
+      bi = i;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(bv, off);
+    const int oi = __shfl_xor(bi, off);
+    if (better(ov, oi, bv, bi)) {
+      bv = ov;
+      bi = oi;
+    }
+  }
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sv[wave] = bv;
+    si[wave] = bi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int nw = blockDim.x >> 6;
+    for (int w = 1; w < nw; ++w)
+      if (better(sv[w], si[w], bv, bi)) {
+        bv = sv[w];
+        bi = si[w];
+      }
+    if (bi >= n) bi = 0;
+    if (out_idx) *out_idx = bi;
+    if (token_out) *token_out = bi;
+    if (pos_inout) *pos_inout += 1;
+  }
+}
+
+}  // namespace lga
+
+extern "C" int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
+                          hipStream_t stream) {
+  LGA_CHECK_ARG(logits && n > 0, "lga_argmax: bad arguments");
+  lga::argmax_kernel<<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, out_idx, token_out, pos_inout);
+  LGA_LAUNCH_RETURN();
+}

@@ -1,0 +1,209 @@
+"""Single-device generation on the MI355X — drop-in for the reference's generate/base.py.
+
+Same functions and semantics as /root/reference/generate/base.py: ``multinomial_num_samples_1`` (:22-27),
+``sample`` (:30-41), ``next_token`` (:44-47), ``generate`` (:50-93: prefill at ``arange(T)``, then one-token
+steps at ``input_pos = T, T+1, ...``, stop on ``eos_id``, ``NotImplementedError`` when ``max_seq_length`` is too
+short) and ``main`` (:96-187) with the same flags and the same stderr timing line. Differences:
+  * greedy decoding (``temperature == 0``) runs each step as one HIP graph replay (lit_gpt/runtime.py) with the
+    argmax on the device — the role ``--compile`` (CUDA graphs) plays in the reference;
+  * ``--quantize`` takes this build's formats (int4-g128, nf4 / bnb.nf4 / bnb.nf4-dq);
+  * ``--synthetic NAME`` builds a random-init model of a registered config (no checkpoint, no tokenizer): the
+    prompt is ``--prompt_len`` synthetic token ids.
+"""
+
+from __future__ import annotations
+
+import argparse
+import sys
+import time
+from pathlib import Path
+from typing import Any, Optional
+
+import torch
+
+wd = Path(__file__).parent.parent.resolve()
+if str(wd) not in sys.path:
+    sys.path.append(str(wd))
+
+from lit_gpt import GPT, Config  # noqa: E402
+from lit_gpt import ops  # noqa: E402
+
+
+def multinomial_num_samples_1(probs: torch.Tensor) -> torch.Tensor:
+    return torch.multinomial(probs, num_samples=1)
+
+
+def sample(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] = None) -> torch.Tensor:
+    """logits (1, T, V) on the GPU -> (1,) token. Greedy runs the HIP argmax (lowest index on ties; top-k
+    cannot change the arg-max); temperature > 0 follows the reference's top-k + softmax + multinomial."""
+    logits = logits[0, -1]
+    if not logits.is_cuda:
+        raise RuntimeError("sample: logits must be on the GPU (this build has no CPU path)")
+    if temperature > 0.0:
+        if top_k is not None:
+            v, i = torch.topk(logits, min(top_k, logits.size(-1)))
+            logits = torch.full_like(logits, float("-inf")).scatter_(-1, i, v)
+        probs = torch.nn.functional.softmax(logits.float() / temperature, dim=-1)
+        return multinomial_num_samples_1(probs)
+    return ops.argmax(logits.to(torch.bfloat16).contiguous())
+
+
+def next_token(model: GPT, input_pos: torch.Tensor, x: torch.Tensor, **kwargs: Any) -> torch.Tensor:
+    logits = model(x, input_pos, last_token_only=True)
+    return sample(logits, **kwargs).to(dtype=x.dtype)
+
+
+@torch.inference_mode()
+def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temperature: float = 1.0,
+             top_k: Optional[int] = None, eos_id: Optional[int] = None, use_graph: bool = True) -> torch.Tensor:
+    """Takes a conditioning sequence (prompt, shape (T,)) and continues it; returns (T + new,) ids."""
+    T = prompt.size(0)
+    assert max_returned_tokens > T
+    if model.max_seq_length < max_returned_tokens - 1:
+        raise NotImplementedError(f"max_seq_length {model.max_seq_length} needs to be >= {max_returned_tokens - 1}")
+    device = prompt.device
+    tokens = [prompt]
+    token = next_token(model, torch.arange(0, T, device=device), prompt.view(1, -1), temperature=temperature,
+                       top_k=top_k).clone()
+    tokens.append(token)
+    n_steps = max_returned_tokens - T - 1
+    if n_steps <= 0:
+        return torch.cat(tokens)
+    if temperature == 0.0 and use_graph:
+        from lit_gpt.runtime import DecodeGraph
+
+        if eos_id is not None and int(token) == eos_id:
+            return torch.cat(tokens)
+        dg = DecodeGraph(model, token, T)  # runs the first decode step eagerly, then captures the step
+        out = torch.empty(n_steps, dtype=prompt.dtype, device=device)
+        out[0] = dg.token.view(-1)[0]
+        produced = 1
+        if not (eos_id is not None and int(out[0]) == eos_id):
+            for i in range(1, n_steps):
+                out[i] = dg.step().view(-1)[0]
+                produced = i + 1
+                if eos_id is not None and int(out[i]) == eos_id:
+                    break
+        tokens.append(out[:produced])
+        return torch.cat(tokens)
+    input_pos = torch.tensor([T], device=device)
+    for _ in range(n_steps):
+        token = next_token(model, input_pos, token.view(1, -1), temperature=temperature, top_k=top_k).clone()
+        tokens.append(token)
+        if eos_id is not None and int(token) == eos_id:
+            break
+        input_pos = input_pos.add_(1)
+    return torch.cat(tokens)
+
+
+def build_model(config: Config, *, quantize: Optional[str], device: torch.device, seed: int = 1234,
+                checkpoint_path: Optional[Path] = None, max_seq_length: Optional[int] = None,
+                tp=None) -> GPT:
+    """Instantiate on the meta device, load (or random-init, as GPT._init_weights) the float weights layer by
+    layer on the GPU, optionally shard them (``tp(model)``), quantize every Linear on the device, then build the
+    rope tables and the KV cache. Mirrors generate/base.py:151-171 / generate/tp.py:157-190."""
+    from lit_gpt.quantize import QuantizedPrecision
+
+    if quantize is None:
+        raise NotImplementedError("the MI355X path runs quantized weights: pass --quantize int4-g128 or nf4")
+    with torch.device("meta"):
+        model = GPT(config)
+    state = None
+    if checkpoint_path is not None:
+        state = torch.load(str(checkpoint_path), mmap=True, map_location="cpu", weights_only=True)
+        state = state.get("model", state)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    for name, p in list(model.named_parameters()):
+        mod_name, _, attr = name.rpartition(".")
+        mod = model.get_submodule(mod_name)
+        if state is not None:
+            t = state[name].to(device=device, dtype=torch.bfloat16)
+        elif attr == "weight" and (isinstance(mod, (torch.nn.Linear, torch.nn.Embedding))):
+            t = torch.empty(p.shape, dtype=torch.float32, device=device).normal_(0.0, 0.02, generator=gen)
+            t = t.to(torch.bfloat16)
+        elif attr == "bias":
+            t = torch.zeros(p.shape, dtype=torch.bfloat16, device=device)
+        else:  # norm weights
+            t = torch.ones(p.shape, dtype=torch.bfloat16, device=device)
+        setattr(mod, attr, torch.nn.Parameter(t, requires_grad=False))
+    if tp is not None:
+        tp(model)
+    QuantizedPrecision(quantize).convert_module(model, device)
+    torch.cuda.empty_cache()
+    model.max_seq_length = max_seq_length or config.block_size
+    model.cos, model.sin = model.rope_cache(device=device)
+    model.set_kv_cache(batch_size=1, device=device)
+    return model.eval()
+
+
+@torch.inference_mode()
+def main(prompt: str = "What food do llamas eat?", *, num_samples: int = 1, max_new_tokens: int = 50,
+         top_k: Optional[int] = 200, temperature: float = 0.8,
+         checkpoint_dir: Path = Path("checkpoints/stabilityai/stablelm-base-alpha-3b"),
+         quantize: Optional[str] = None, precision: Optional[str] = None, compile: bool = False,
+         synthetic: Optional[str] = None, prompt_len: int = 16) -> None:
+    precision = precision or "bf16-true"
+    if precision != "bf16-true":
+        raise NotImplementedError("the MI355X 4-bit path computes in bf16 (precision bf16-true)")
+    device = torch.device("cuda", torch.cuda.current_device())
+    tokenizer = None
+    if synthetic is not None:
+        config = Config.from_name(synthetic)
+        checkpoint_path = None
+        g = torch.Generator(device="cpu").manual_seed(1234)
+        encoded = torch.randint(0, config.vocab_size, (prompt_len,), generator=g, dtype=torch.int32).to(device)
+    else:
+        from lit_gpt.tokenizer import Tokenizer
+        from lit_gpt.utils import check_valid_checkpoint_dir
+
+        check_valid_checkpoint_dir(checkpoint_dir)
+        config = Config.from_json(checkpoint_dir / "lit_config.json")
+        checkpoint_path = checkpoint_dir / "lit_model.pth"
+        tokenizer = Tokenizer(checkpoint_dir)
+        encoded = tokenizer.encode(prompt, device=device)
+    prompt_length = encoded.size(0)
+    max_returned_tokens = prompt_length + max_new_tokens
+    print(f"Loading model {str(checkpoint_path or synthetic)!r} with {config.__dict__}", file=sys.stderr)
+    t0 = time.perf_counter()
+    model = build_model(config, quantize=quantize, device=device, checkpoint_path=checkpoint_path,
+                        max_seq_length=max_returned_tokens)
+    print(f"Time to load the model weights: {time.perf_counter() - t0:.02f} seconds.", file=sys.stderr)
+    torch.manual_seed(1234)
+    eos_id = tokenizer.eos_id if tokenizer is not None else None
+    for i in range(num_samples):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        y = generate(model, encoded, max_returned_tokens, temperature=temperature, top_k=top_k, eos_id=eos_id)
+        torch.cuda.synchronize()
+        t = time.perf_counter() - t0
+        for block in model.transformer.h:
+            block.attn.kv_cache.reset_parameters()
+        print(tokenizer.decode(y) if tokenizer is not None else y.tolist())
+        tokens_generated = y.size(0) - prompt_length
+        print(f"Time for inference {i + 1}: {t:.02f} sec total, {tokens_generated / t:.02f} tokens/sec",
+              file=sys.stderr)
+    print(f"Memory used: {torch.cuda.max_memory_allocated() / 1e9:.02f} GB", file=sys.stderr)
+
+
+def _cli(argv=None) -> None:
+    p = argparse.ArgumentParser(description="Generates text samples based on a pre-trained model and tokenizer.")
+    p.add_argument("--prompt", default="What food do llamas eat?")
+    p.add_argument("--num_samples", type=int, default=1)
+    p.add_argument("--max_new_tokens", type=int, default=50)
+    p.add_argument("--top_k", type=int, default=200)
+    p.add_argument("--temperature", type=float, default=0.8)
+    p.add_argument("--checkpoint_dir", type=Path, default=Path("checkpoints/stabilityai/stablelm-base-alpha-3b"))
+    p.add_argument("--quantize", default=None)
+    p.add_argument("--precision", default=None)
+    p.add_argument("--compile", action="store_true")
+    p.add_argument("--synthetic", default=None, help="random-init model of this registered config name")
+    p.add_argument("--prompt_len", type=int, default=16)
+    a = p.parse_args(argv)
+    main(a.prompt, num_samples=a.num_samples, max_new_tokens=a.max_new_tokens, top_k=a.top_k,
+         temperature=a.temperature, checkpoint_dir=a.checkpoint_dir, quantize=a.quantize, precision=a.precision,
+         compile=a.compile, synthetic=a.synthetic, prompt_len=a.prompt_len)
+
+
+if __name__ == "__main__":
+    _cli()

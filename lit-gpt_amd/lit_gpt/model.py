@@ -1,0 +1,341 @@
+"""GPT / Block / CausalSelfAttention / KVCache with the reference's module API and an MI355X HIP hot path.
+
+Public surface kept from /root/reference/lit_gpt/model.py: ``GPT(config)``; ``GPT.forward(idx,
+input_pos=None)`` (:499-519); ``max_seq_length`` property/setter (:462-484); ``rope_cache`` (:525-532);
+``set_kv_cache`` / ``clear_kv_cache`` (:534-559); ``from_name`` (:521-523); ``_init_weights`` (:490-497);
+attributes ``config, lm_head, transformer.{wte,h,ln_f}, cos, sin, mask_cache``. ``Block.forward(x, cos, sin,
+mask=None, input_pos=None)`` (:572-593) with ``norm_1, attn, norm_2, mlp``; ``CausalSelfAttention.forward``
+(:609-656) with ``attn`` (fused qkv Linear), ``proj``, ``kv_cache``, ``build_kv_cache``,
+``scaled_dot_product_attention``; ``KVCache`` (:776-799); ``LLaMAMLP`` / ``LLaMAMoE`` / ``GptNeoxMLP`` classes
+(``generate/tp.py`` isinstance-checks them); ``build_rope_cache`` / ``apply_rope`` / ``build_mask_cache``.
+
+What runs underneath (GPU, bf16 activations, Linears converted by ``QuantizedPrecision``): every op is a HIP
+kernel from ``liblitgpt_amd.so`` — embedding gather, RMSNorm fused into the qkv / fc GEMV prologue, RoPE fused
+with the KV-cache append, split-sequence decode attention, the out-projections with the residual add in their
+epilogue, SwiGLU fused into the dual fc_1/fc_2 GEMV, and greedy argmax. Differences from the reference that do
+not change results: the KV cache holds ``n_query_groups`` heads (un-expanded GQA), RoPE positions are exact
+fp32 (the reference's bf16 default-dtype rounding of positions > 256 is not reproduced), and the
+bool mask is never materialised on the hot path (the kernels read keys ``<= input_pos``).
+"""
+
+from __future__ import annotations
+
+import math
+from typing import Any, Optional, Tuple
+
+import torch
+import torch.nn as nn
+
+from lit_gpt import ops
+from lit_gpt.config import Config
+from lit_gpt.rmsnorm import RMSNorm
+
+_SPLIT_CHUNK = 64  # keys per decode-attention workgroup (flash-decoding split size)
+
+
+def _gpu_only(what: str) -> None:
+    raise RuntimeError(f"{what}: this build computes on the MI355X only (no CPU path); move the model to 'cuda'")
+
+
+def _lin(linear: nn.Module, x: torch.Tensor, **kw) -> torch.Tensor:
+    from lit_gpt.quantize import QuantLinear
+
+    if isinstance(linear, QuantLinear):
+        return linear(x, **kw)
+    raise NotImplementedError(
+        "unquantized nn.Linear on the MI355X path: convert the model with "
+        "lit_gpt.quantize.QuantizedPrecision('int4-g128' | 'nf4').convert_module(model) (the --quantize flag)")
+
+
+class GPT(nn.Module):
+    def __init__(self, config: Config) -> None:
+        super().__init__()
+        assert config.padded_vocab_size is not None
+        self.config = config
+        self.lm_head = nn.Linear(config.n_embd, config.padded_vocab_size, bias=config.lm_head_bias)
+        self.transformer = nn.ModuleDict(dict(
+            wte=nn.Embedding(config.padded_vocab_size, config.n_embd),
+            h=nn.ModuleList(Block(config) for _ in range(config.n_layer)),
+            ln_f=config.norm_class(config.n_embd, eps=config.norm_eps),
+        ))
+        self.max_seq_length = self.config.block_size
+        self.mask_cache: Optional[torch.Tensor] = None
+
+    @property
+    def max_seq_length(self) -> int:
+        return self._max_seq_length
+
+    @max_seq_length.setter
+    def max_seq_length(self, value: int) -> None:
+        if value > self.config.block_size:
+            raise ValueError(f"Cannot attend to {value}, block size is only {self.config.block_size}")
+        self._max_seq_length = value
+        if not hasattr(self, "cos"):
+            cos, sin = self.rope_cache()
+            self.register_buffer("cos", cos, persistent=False)
+            self.register_buffer("sin", sin, persistent=False)
+        elif value != self.cos.size(0):
+            self.cos, self.sin = self.rope_cache(device=self.cos.device)
+
+    def reset_parameters(self) -> None:
+        self.cos, self.sin = self.rope_cache()
+
+    def _init_weights(self, module: nn.Module) -> None:
+        if isinstance(module, nn.Linear):
+            torch.nn.init.normal_(module.weight, mean=0.0, std=0.02)
+            if module.bias is not None:
+                torch.nn.init.zeros_(module.bias)
+        elif isinstance(module, nn.Embedding):
+            torch.nn.init.normal_(module.weight, mean=0.0, std=0.02)
+
+    def _rope_tables(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        # model.to(bf16) would also cast the rope buffers; the kernels need the exact fp32 tables
+        if self.cos.dtype != torch.float32 or self.cos.size(0) != self.max_seq_length:
+            self.cos, self.sin = self.rope_cache(device=self.cos.device)
+        return self.cos, self.sin
+
+    def forward(self, idx: torch.Tensor, input_pos: Optional[torch.Tensor] = None, *,
+                last_token_only: bool = False) -> torch.Tensor:
+        """(B=1, T) ids -> (1, T, padded_vocab) logits; ``last_token_only`` computes only the last row (1, 1, V)
+        — all that ``generate`` samples from (generate/base.py:31)."""
+        B, T = idx.shape
+        if self.max_seq_length < T:
+            raise ValueError(f"Cannot forward sequence of length {T}, max seq length is only {self.max_seq_length}.")
+        if input_pos is not None and self.mask_cache is None:
+            raise TypeError("You need to call `gpt.set_kv_cache()`")
+        if not idx.is_cuda:
+            _gpu_only("GPT.forward")
+        if B != 1:
+            raise NotImplementedError("the MI355X decode path runs batch size 1 (as generate/base.py does)")
+        cos, sin = self._rope_tables()
+        if input_pos is not None:
+            input_pos = input_pos.to(device=idx.device, dtype=torch.int64).contiguous()
+        x = ops.embedding(idx.reshape(-1).contiguous(), self.transformer.wte.weight).view(1, T, -1)
+        for block in self.transformer.h:
+            x = block(x, cos, sin, None, input_pos)
+        if last_token_only:
+            x = x[:, -1:].contiguous()
+        ln = self.transformer.ln_f
+        if isinstance(ln, RMSNorm):
+            return _lin(self.lm_head, x, norm_weight=ln.weight, norm_eps=ln.eps)
+        return _lin(self.lm_head, ln(x))
+
+    @classmethod
+    def from_name(cls, name: str, **kwargs: Any) -> "GPT":
+        return cls(Config.from_name(name, **kwargs))
+
+    def rope_cache(self, device: Optional[torch.device] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+        return build_rope_cache(seq_len=self.max_seq_length, n_elem=self.config.rope_n_elem, device=device,
+                                condense_ratio=self.config.rope_condense_ratio, base=self.config.rope_base)
+
+    def set_kv_cache(self, batch_size: int, rope_cache_length: Optional[int] = None,
+                     device: Optional[torch.device] = None, dtype: Optional[torch.dtype] = None) -> None:
+        if rope_cache_length is None:
+            rope_cache_length = self.cos.size(-1)
+        for block in self.transformer.h:
+            block.attn.kv_cache = block.attn.build_kv_cache(batch_size, self.max_seq_length, rope_cache_length,
+                                                            device, dtype)
+        if self.mask_cache is None or self.mask_cache.size(3) != self.max_seq_length:
+            self.mask_cache = build_mask_cache(self.max_seq_length, device or self.transformer.wte.weight.device)
+
+    def clear_kv_cache(self) -> None:
+        self.mask_cache = None
+        for block in self.transformer.h:
+            block.attn.kv_cache = None
+
+
+class Block(nn.Module):
+    def __init__(self, config: Config) -> None:
+        super().__init__()
+        self.norm_1 = config.norm_class(config.n_embd, eps=config.norm_eps)
+        self.attn = CausalSelfAttention(config)
+        self.norm_2 = None if config.shared_attention_norm else config.norm_class(config.n_embd, eps=config.norm_eps)
+        self.mlp = config.mlp_class(config)
+        self.config = config
+
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
+                input_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
+        c = self.config
+        if c.parallel_residual or c.shared_attention_norm:
+            if c.shared_attention_norm and not c.parallel_residual:
+                raise NotImplementedError("No checkpoint amongst the ones we support uses this configuration"
+                                          " (non-parallel residual and shared attention norm).")
+            raise NotImplementedError("parallel-residual (GPT-NeoX) blocks have no MI355X kernels in this build; "
+                                      "config 1 (pythia) runs on the CPU oracle")
+        if not isinstance(self.norm_1, RMSNorm) or not isinstance(self.mlp, LLaMAMLP):
+            raise NotImplementedError(f"{type(self.mlp).__name__} / {type(self.norm_1).__name__} blocks have no "
+                                      "MI355X kernels in this build")
+        # residual adds ride the out-projection epilogues unless a hook (TP all-reduce) must see the bare output
+        if not self.attn._forward_hooks and not self.mlp._forward_hooks:
+            x = self.attn(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x)
+            return self.mlp(x, norm=self.norm_2, residual=x)
+        h = self.attn(self.norm_1(x), cos, sin, mask, input_pos)
+        x = ops.add(h.contiguous(), x.contiguous())
+        return ops.add(self.mlp(self.norm_2(x)).contiguous(), x)
+
+
+class CausalSelfAttention(nn.Module):
+    def __init__(self, config: Config) -> None:
+        super().__init__()
+        shape = (config.n_head + 2 * config.n_query_groups) * config.head_size
+        self.attn = nn.Linear(config.n_embd, shape, bias=config.bias)
+        self.proj = nn.Linear(config.n_embd, config.n_embd, bias=config.bias)
+        self.kv_cache: Optional[KVCache] = None
+        self.config = config
+
+    def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
+                input_pos: Optional[torch.Tensor] = None, *, norm: Optional["RMSNorm"] = None,
+                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``norm`` / ``residual`` are fusion hooks used by Block.forward: the RMSNorm runs in the qkv GEMV
+        prologue and the residual add in the proj epilogue. Without them this is the reference forward."""
+        B, T, C = x.size()
+        c = self.config
+        H, G, hs = c.n_head, c.n_query_groups, c.head_size
+        qkv = _lin(self.attn, x, norm_weight=None if norm is None else norm.weight,
+                   norm_eps=c.norm_eps if norm is None else norm.eps).view(T, -1)
+        dev = x.device
+        if input_pos is None:
+            # no cache (training-style causal forward, model.py:510-513): a private cache of T rows
+            pos = torch.arange(T, device=dev, dtype=torch.int64)
+            kc = torch.empty(G, T, hs, dtype=torch.bfloat16, device=dev)
+            vc = torch.empty_like(kc)
+            rope_pos = pos
+        else:
+            if not isinstance(self.kv_cache, KVCache):
+                raise TypeError("You need to call `gpt.set_kv_cache()`")
+            kv = self.kv_cache
+            if kv.k.dtype != torch.bfloat16:  # reference KVCache.forward casts to the activation dtype (:790-791)
+                kv.k, kv.v = kv.k.to(torch.bfloat16), kv.v.to(torch.bfloat16)
+            kc, vc = kv.k, kv.v
+            pos = input_pos
+            # callers may pass the full cos/sin tables (our GPT.forward) or rows pre-selected by input_pos (the
+            # reference's GPT.forward, model.py:505-506)
+            rope_pos = pos if (cos.size(0) != T or T == kc.size(-2)) else torch.arange(T, device=dev)
+        cos = cos.to(device=dev, dtype=torch.float32).contiguous()
+        sin = sin.to(device=dev, dtype=torch.float32).contiguous()
+        q = ops.rope_kv_append(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem)
+        S = kc.size(-2)
+        n_splits = max(1, math.ceil(S / _SPLIT_CHUNK)) if T == 1 else 1
+        y = ops.attention(q, kc, vc, pos, H, G, hs, 1.0 / math.sqrt(hs), n_splits)
+        out = _lin(self.proj, y.view(1, T, H * hs), residual=residual)
+        return out.view(B, T, -1)
+
+    def scaled_dot_product_attention(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
+                                     mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Reference-compatible helper (model.py:658-665); the fused path uses ``ops.attention`` instead."""
+        scale = 1.0 / math.sqrt(self.config.head_size)
+        y = torch.nn.functional.scaled_dot_product_attention(q, k, v, attn_mask=mask, dropout_p=0.0, scale=scale,
+                                                             is_causal=mask is None)
+        return y.transpose(1, 2)
+
+    def build_kv_cache(self, batch_size: int, max_seq_length: int, rope_cache_length: Optional[int] = None,
+                       device: Optional[torch.device] = None, dtype: Optional[torch.dtype] = None) -> "KVCache":
+        heads = self.config.n_query_groups  # un-expanded groups (the reference stores n_head, model.py:675)
+        v_shape = (batch_size, heads, max_seq_length, self.config.head_size)
+        if rope_cache_length is None:
+            if self.config.rotary_percentage != 1.0:
+                raise TypeError("Please pass the `rope_cache_length=gpt.cos.size(-1)` value")
+            k_shape = v_shape
+        else:
+            k_shape = (batch_size, heads, max_seq_length,
+                       rope_cache_length + self.config.head_size - self.config.rope_n_elem)
+        if device is None:
+            device = self.attn.weight.device
+        return KVCache(k_shape, v_shape, device=device, dtype=dtype or torch.bfloat16)
+
+
+class GptNeoxMLP(nn.Module):
+    """Kept for the API / TP isinstance checks (model.py:691-702); no MI355X kernels in this build."""
+
+    def __init__(self, config: Config) -> None:
+        super().__init__()
+        self.fc = nn.Linear(config.n_embd, config.intermediate_size, bias=config.bias)
+        self.proj = nn.Linear(config.intermediate_size, config.n_embd, bias=config.bias)
+        self.config = config
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError("GptNeoxMLP runs on the CPU oracle only in this build")
+
+
+class LLaMAMLP(nn.Module):
+    def __init__(self, config: Config) -> None:
+        super().__init__()
+        self.fc_1 = nn.Linear(config.n_embd, config.intermediate_size, bias=config.bias)
+        self.fc_2 = nn.Linear(config.n_embd, config.intermediate_size, bias=config.bias)
+        self.proj = nn.Linear(config.intermediate_size, config.n_embd, bias=config.bias)
+
+    def forward(self, x: torch.Tensor, *, norm: Optional["RMSNorm"] = None,
+                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """proj(silu(fc_1 x) * fc_2 x) (model.py:712-716); ``norm``/``residual`` are Block fusion hooks."""
+        from lit_gpt.quantize import QuantLinear
+
+        lead, C = x.shape[:-1], x.shape[-1]
+        x2 = x.reshape(-1, C).contiguous()
+        M = x2.shape[0]
+        f1, f2 = self.fc_1, self.fc_2
+        fusable = (M == 1 and isinstance(f1, QuantLinear) and isinstance(f2, QuantLinear) and f1.bias is None
+                   and f2.bias is None and (f1.fmt, f1.group) == (f2.fmt, f2.group))
+        if fusable:
+            g = ops.q4_gemv_swiglu(x2.view(-1), f1.qweight, f1.scales, f2.qweight, f2.scales, f1.out_features, C,
+                                   f1.group, f1.fmt, norm_weight=None if norm is None else norm.weight,
+                                   eps=1e-5 if norm is None else norm.eps).view(1, -1)
+        else:
+            n = x2 if norm is None else norm(x2)
+            g = ops.swiglu(_lin(f1, n).contiguous(), _lin(f2, n).contiguous())
+        out = _lin(self.proj, g, residual=residual)
+        return out.view(*lead, -1)
+
+
+class LLaMAMoE(nn.Module):
+    """Kept for the API / TP isinstance checks (model.py:719-743); the MoE kernels are a later milestone."""
+
+    def __init__(self, config: Config) -> None:
+        super().__init__()
+        self.gate = nn.Linear(config.n_embd, config.n_expert, bias=False)
+        self.experts = nn.ModuleList(LLaMAMLP(config) for _ in range(config.n_expert))
+        self.config = config
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        raise NotImplementedError("LLaMAMoE has no MI355X kernels in this build yet")
+
+
+LayerNorm = nn.LayerNorm  # config.norm_class for GPT-NeoX (reference config.py:137-144)
+
+
+class KVCache(nn.Module):
+    def __init__(self, k_shape: Tuple[int, int, int, int], v_shape: Tuple[int, int, int, int],
+                 device: Optional[torch.device] = None, dtype: Optional[torch.dtype] = None) -> None:
+        super().__init__()
+        self.register_buffer("k", torch.zeros(k_shape, device=device, dtype=dtype), persistent=False)
+        self.register_buffer("v", torch.zeros(v_shape, device=device, dtype=dtype), persistent=False)
+
+    def forward(self, input_pos: torch.Tensor, k: torch.Tensor, v: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Reference API (model.py:788-795); the fused path writes the cache inside ``lga_rope_kv_append``."""
+        self.k = self.k.to(k.dtype)
+        self.v = self.v.to(v.dtype)
+        return self.k.index_copy_(2, input_pos, k), self.v.index_copy_(2, input_pos, v)
+
+    def reset_parameters(self) -> None:
+        torch.nn.init.zeros_(self.k)
+        torch.nn.init.zeros_(self.v)
+
+
+def build_rope_cache(seq_len: int, n_elem: int, device: Optional[torch.device] = None, base: int = 10000,
+                     condense_ratio: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
+    """cos/sin tables (seq_len, n_elem) in fp32 (model.py:746-764) with exact fp32 positions."""
+    theta = 1.0 / (base ** (torch.arange(0, n_elem, 2, device=device, dtype=torch.float32) / n_elem))
+    seq_idx = torch.arange(seq_len, device=device, dtype=torch.float32) / condense_ratio
+    idx_theta = torch.outer(seq_idx, theta).repeat(1, 2)
+    return torch.cos(idx_theta), torch.sin(idx_theta)
+
+
+def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:
+    """Reference helper (model.py:767-773); the hot path applies RoPE inside ``lga_rope_kv_append``."""
+    half = x.size(-1) // 2
+    rotated = torch.cat((-x[..., half:], x[..., :half]), dim=-1)
+    return ((x * cos) + (rotated * sin)).to(dtype=x.dtype)
+
+
+def build_mask_cache(max_seq_length: int, device: Optional[torch.device] = None) -> torch.Tensor:
+    ones = torch.ones((max_seq_length, max_seq_length), device=device, dtype=torch.bool)
+    return torch.tril(ones).unsqueeze(0).unsqueeze(0)

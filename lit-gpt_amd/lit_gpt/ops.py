@@ -1,0 +1,226 @@
+"""Python view of the C-ABI library ``liblitgpt_amd.so`` (declared in ``include/litgpt_amd.h``).
+
+Every hot op of the decode path is a HIP kernel in ``lit-gpt_amd/csrc`` reached through these thin wrappers:
+they validate dtype / shape / contiguity / device, pass raw device pointers and sizes, launch on torch's
+current HIP stream (so the calls can be captured into a HIP graph), and turn a non-zero return code into a
+``RuntimeError`` carrying ``lga_last_error_string()``. There is no CPU fallback: without the library, or on a
+non-GPU tensor, every op raises.
+
+Reference boundary replaced: bitsandbytes' ctypes C functions behind ``Linear4bit`` and the ATen
+kernels that ``lit_gpt/model.py`` issues (RMSNorm, RoPE, index_copy_, SDPA, embedding, argmax).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from pathlib import Path
+from typing import Optional
+
+import torch
+
+LIB_PATH = Path(os.environ.get("LGA_LIB", Path(__file__).resolve().parent / "_lib" / "liblitgpt_amd.so"))
+
+FMT_Q4G = 0  # int4, symmetric, per-group bf16 scale
+FMT_NF4 = 1  # bitsandbytes NF4 codebook, per-block fp32 absmax
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+
+# symbol -> argtypes; the exported surface of include/litgpt_amd.h (tests check the .so exports each one)
+SIGNATURES = {
+    "lga_version": [],
+    "lga_last_error_string": [],
+    "lga_device_info": [_I, _P, _P, _I],
+    "lga_quantize": [_P, _I, _P, _P, _I, _I, _I, _I, _P],
+    "lga_q4_gemv": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
+    "lga_q4_gemv_swiglu": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
+    "lga_q4_gemm": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lga_rmsnorm": [_P, _P, _P, _I, _I, _F, _P],
+    "lga_rope_kv_append": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "lga_embedding": [_P, _I, _P, _P, _I, _I, _I, _P],
+    "lga_add": [_P, _P, _P, _L, _P],
+    "lga_swiglu": [_P, _P, _P, _L, _P],
+    "lga_attention": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
+    "lga_attention_workspace_bytes": [_I, _I, _I, _I],
+    "lga_argmax": [_P, _I, _P, _P, _P, _P],
+}
+_RESTYPES = {"lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class NativeLibraryError(RuntimeError):
+    pass
+
+
+def load_library(path: Optional[Path] = None) -> ctypes.CDLL:
+    """Load (once) and return the HIP library. Raises loudly when it is missing: there is no fallback."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = Path(path or LIB_PATH)
+    if not p.is_file():
+        raise NativeLibraryError(
+            f"HIP library not found at {p}. Build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C lit-gpt_amd/csrc` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
+    lib = ctypes.CDLL(str(p))
+    for name, argtypes in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = argtypes
+        fn.restype = _RESTYPES.get(name, ctypes.c_int)
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        msg = load_library().lga_last_error_string()
+        raise RuntimeError(f"liblitgpt_amd error {rc}: {msg.decode() if msg else ''}")
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _dev(t: torch.Tensor, name: str, dtype: Optional[torch.dtype] = None) -> int:
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: expected a GPU tensor (this build has no CPU path), got {t.device}")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def _opt(t: Optional[torch.Tensor], name: str, dtype=None) -> Optional[int]:
+    return None if t is None else _dev(t, name, dtype)
+
+
+# ------------------------------------------------------------------------------------------------ quantizer
+def quantize(weight: torch.Tensor, fmt: int, group: int):
+    """(N, K) fp32/bf16 device weight -> (packed uint8 (N, K/2), scales) on the same device."""
+    N, K = weight.shape
+    w = weight.contiguous()
+    if w.dtype not in (torch.float32, torch.bfloat16):
+        w = w.float()
+    qw = torch.empty(N, K // 2, dtype=torch.uint8, device=w.device)
+    sdt = torch.bfloat16 if fmt == FMT_Q4G else torch.float32
+    sc = torch.empty(N, K // group, dtype=sdt, device=w.device)
+    _check(load_library().lga_quantize(_dev(w, "weight"), int(w.dtype == torch.bfloat16), qw.data_ptr(),
+                                       sc.data_ptr(), N, K, group, fmt, _stream()))
+    return qw, sc
+
+
+# ------------------------------------------------------------------------------------------------ linear
+def q4_gemv(x, qweight, scales, N, K, group, fmt, *, bias=None, residual=None, norm_weight=None, eps=1e-5,
+            out=None, variant=-1):
+    """y (N,) = x (K,) . dequant(W)^T  [+bias] [+residual]; optional fused RMSNorm of x (norm_weight)."""
+    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_q4_gemv(_dev(x, "x", torch.bfloat16), _dev(qweight, "qweight", torch.uint8),
+                                      _dev(scales, "scales"), _opt(bias, "bias", torch.bfloat16),
+                                      _opt(residual, "residual", torch.bfloat16),
+                                      _opt(norm_weight, "norm_weight", torch.bfloat16), float(eps),
+                                      _dev(y, "y", torch.bfloat16), N, K, group, fmt, variant, _stream()))
+    return y
+
+
+def q4_gemv_swiglu(x, qw1, sc1, qw2, sc2, N, K, group, fmt, *, norm_weight=None, eps=1e-5, out=None, variant=-1):
+    """y (N,) = bf16(silu(bf16(x W1^T))) * bf16(x W2^T), optional fused RMSNorm of x."""
+    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_q4_gemv_swiglu(_dev(x, "x", torch.bfloat16), _dev(qw1, "qw1", torch.uint8),
+                                             _dev(sc1, "sc1"), _dev(qw2, "qw2", torch.uint8), _dev(sc2, "sc2"),
+                                             _opt(norm_weight, "norm_weight", torch.bfloat16), float(eps),
+                                             _dev(y, "y", torch.bfloat16), N, K, group, fmt, variant, _stream()))
+    return y
+
+
+def q4_gemm(x, qweight, scales, N, K, group, fmt, *, bias=None, residual=None, out=None):
+    """Y (M, N) = X (M, K) . dequant(W)^T [+bias] [+residual] with MFMA tiles."""
+    M = x.shape[0]
+    y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_q4_gemm(_dev(x, "x", torch.bfloat16), _dev(qweight, "qweight", torch.uint8),
+                                      _dev(scales, "scales"), _opt(bias, "bias", torch.bfloat16),
+                                      _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16),
+                                      M, N, K, group, fmt, _stream()))
+    return y
+
+
+# ------------------------------------------------------------------------------------------------ row ops
+def rmsnorm(x, weight, eps, out=None):
+    n = x.shape[-1]
+    rows = x.numel() // n
+    y = out if out is not None else torch.empty_like(x)
+    _check(load_library().lga_rmsnorm(_dev(x, "x", torch.bfloat16), _dev(weight, "weight", torch.bfloat16),
+                                      _dev(y, "y", torch.bfloat16), rows, n, float(eps), _stream()))
+    return y
+
+
+def rope_kv_append(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin, n_head, n_query_groups, head_size,
+                   rope_n_elem, q_out=None):
+    """qkv (T, (H+2G)*hs) -> q (T, H, hs) roped with cos/sin rows rope_pos; k (roped) and v written into the
+    (G, max_seq, hs) caches at rows cache_pos."""
+    T = qkv.shape[0]
+    max_seq = k_cache.shape[-2]
+    q = q_out if q_out is not None else torch.empty(T, n_head, head_size, dtype=torch.bfloat16, device=qkv.device)
+    _check(load_library().lga_rope_kv_append(
+        _dev(qkv, "qkv", torch.bfloat16), _dev(q, "q", torch.bfloat16), _dev(k_cache, "k_cache", torch.bfloat16),
+        _dev(v_cache, "v_cache", torch.bfloat16), _dev(cache_pos, "cache_pos", torch.int64),
+        _dev(rope_pos, "rope_pos", torch.int64), _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32),
+        cos.shape[0], T, n_head, n_query_groups, head_size, rope_n_elem, max_seq, _stream()))
+    return q
+
+
+def attention(q, k_cache, v_cache, input_pos, n_head, n_query_groups, head_size, scale, n_splits=1,
+              workspace=None, out=None):
+    T = q.shape[0]
+    max_seq = k_cache.shape[-2]
+    y = out if out is not None else torch.empty(T, n_head * head_size, dtype=torch.bfloat16, device=q.device)
+    if n_splits > 1 and workspace is None:
+        nbytes = load_library().lga_attention_workspace_bytes(T, n_head, head_size, n_splits)
+        workspace = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
+    _check(load_library().lga_attention(
+        _dev(q, "q", torch.bfloat16), _dev(k_cache, "k_cache", torch.bfloat16),
+        _dev(v_cache, "v_cache", torch.bfloat16), _dev(input_pos, "input_pos", torch.int64),
+        _dev(y, "y", torch.bfloat16), None if workspace is None else _dev(workspace, "workspace", torch.float32),
+        T, n_head, n_query_groups, head_size, max_seq, n_splits, float(scale), _stream()))
+    return y
+
+
+def embedding(idx, table, out=None):
+    T = idx.numel()
+    V, C = table.shape
+    y = out if out is not None else torch.empty(T, C, dtype=torch.bfloat16, device=table.device)
+    if idx.dtype not in (torch.int32, torch.int64):
+        raise TypeError(f"embedding: idx must be int32/int64, got {idx.dtype}")
+    _check(load_library().lga_embedding(_dev(idx, "idx"), int(idx.dtype == torch.int64),
+                                        _dev(table, "table", torch.bfloat16), _dev(y, "y", torch.bfloat16), T, C, V,
+                                        _stream()))
+    return y
+
+
+def add(a, b, out=None):
+    y = out if out is not None else torch.empty_like(a)
+    _check(load_library().lga_add(_dev(a, "a", torch.bfloat16), _dev(b, "b", torch.bfloat16),
+                                  _dev(y, "y", torch.bfloat16), a.numel(), _stream()))
+    return y
+
+
+def swiglu(a, b, out=None):
+    y = out if out is not None else torch.empty_like(a)
+    _check(load_library().lga_swiglu(_dev(a, "a", torch.bfloat16), _dev(b, "b", torch.bfloat16),
+                                     _dev(y, "y", torch.bfloat16), a.numel(), _stream()))
+    return y
+
+
+def argmax(logits, out_idx=None, token_out=None, pos_inout=None):
+    """Greedy token (lowest index on ties); optionally writes the token buffer and advances input_pos."""
+    n = logits.numel()
+    idx = out_idx if out_idx is not None else torch.empty(1, dtype=torch.int64, device=logits.device)
+    _check(load_library().lga_argmax(_dev(logits, "logits", torch.bfloat16), n, _dev(idx, "out_idx", torch.int64),
+                                     _opt(token_out, "token_out", torch.int32),
+                                     _opt(pos_inout, "pos_inout", torch.int64), _stream()))
+    return idx

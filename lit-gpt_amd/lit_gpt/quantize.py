@@ -1,0 +1,130 @@
+"""4-bit weight-only quantized Linear — the drop-in for bitsandbytes' ``Linear4bit``.
+
+Reference boundary ("Operator boundary being replaced"): any object used where ``nn.Linear`` is
+expected — ``forward(x[..., in_features]) -> y[..., out_features]`` with attributes ``weight``, ``bias``,
+``in_features``, ``out_features``. The reference gets it from Lightning's ``BitsandbytesPrecision(mode, dtype)``
+whose ``convert_module`` swaps every ``nn.Linear`` (lm_head included: ``ignore_modules`` is not passed,
+generate/base.py:133) and quantizes on the move to the GPU (generate/base.py:128-136, 168; generate/tp.py:171,
+190). ``QuantizedPrecision`` mirrors that: ``convert_module`` swaps the Linears of a (possibly TP-sharded,
+still float) model for ``QuantLinear`` modules that quantize their weight on the device with the HIP quantizer.
+
+Modes:
+  "int4-g128" (also "int4-g64", "int4-g32")  symmetric int4, per-group bf16 scale (BASELINE config 3)
+  "nf4"  / "bnb.nf4"                          NF4 codebook, fp32 absmax per 64 (bitsandbytes nf4 layout)
+  "bnb.nf4-dq"                                accepted; absmax kept fp32 (no double quantization)
+Group sizes must divide in_features; for a TP row-shard whose width is not a multiple of the requested group
+(e.g. Llama-2-7B mlp.proj at TP=8: 1376) the largest of {128, 64, 32} that divides it is used.
+"""
+
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+
+from lit_gpt import ops
+
+_MODES = {
+    "int4-g128": (ops.FMT_Q4G, 128),
+    "int4-g64": (ops.FMT_Q4G, 64),
+    "int4-g32": (ops.FMT_Q4G, 32),
+    "nf4": (ops.FMT_NF4, 64),
+    "bnb.nf4": (ops.FMT_NF4, 64),
+    "bnb.nf4-dq": (ops.FMT_NF4, 64),
+}
+
+
+def parse_mode(mode: str):
+    if mode not in _MODES:
+        raise NotImplementedError(
+            f"quantize mode {mode!r} is not supported on this build (supported: {sorted(_MODES)}); "
+            "bnb.fp4 / bnb.int8 have no MI355X kernel")
+    return _MODES[mode]
+
+
+def _fit_group(K: int, group: int) -> int:
+    for g in (group, 128, 64, 32):
+        if g <= group and K % g == 0:
+            return g
+    raise ValueError(f"in_features={K} is not a multiple of 32; no 4-bit group layout fits")
+
+
+class QuantLinear(nn.Module):
+    """Packed 4-bit weight ``qweight`` (N, K/2) uint8 + ``scales`` (N, K/group) on the GPU.
+
+    ``forward`` dispatches like bitsandbytes' ``matmul_4bit``: one token -> fused dequant-GEMV
+    (``lga_q4_gemv``), several -> MFMA GEMM (``lga_q4_gemm``). ``weight`` is kept as an alias of the packed
+    buffer so code that inspects ``linear.weight`` (e.g. ``.device``/``.dtype``) keeps working.
+    """
+
+    def __init__(self, in_features: int, out_features: int, fmt: int, group: int,
+                 bias: Optional[torch.Tensor] = None, device=None):
+        super().__init__()
+        self.in_features, self.out_features = in_features, out_features
+        self.fmt, self.group = fmt, group
+        self.register_buffer("qweight", torch.empty(out_features, in_features // 2, dtype=torch.uint8, device=device))
+        sdt = torch.bfloat16 if fmt == ops.FMT_Q4G else torch.float32
+        self.register_buffer("scales", torch.empty(out_features, in_features // group, dtype=sdt, device=device))
+        self.bias = None if bias is None else nn.Parameter(bias.to(torch.bfloat16), requires_grad=False)
+
+    @property
+    def weight(self) -> torch.Tensor:
+        return self.qweight
+
+    @classmethod
+    def from_float(cls, weight: torch.Tensor, bias: Optional[torch.Tensor], mode: str,
+                   device: Optional[torch.device] = None) -> "QuantLinear":
+        fmt, group = parse_mode(mode)
+        N, K = weight.shape
+        group = _fit_group(K, group)
+        device = device or (weight.device if weight.is_cuda else torch.device("cuda", torch.cuda.current_device()))
+        w = weight.detach().to(device)
+        m = cls(K, N, fmt, group, None if bias is None else bias.detach().to(device), device=device)
+        qw, sc = ops.quantize(w, fmt, group)
+        m.qweight.copy_(qw)
+        m.scales.copy_(sc)
+        return m
+
+    def forward(self, x: torch.Tensor, *, residual: Optional[torch.Tensor] = None,
+                norm_weight: Optional[torch.Tensor] = None, norm_eps: float = 1e-5) -> torch.Tensor:
+        lead = x.shape[:-1]
+        x2 = x.reshape(-1, self.in_features)
+        if x2.dtype != torch.bfloat16:
+            raise TypeError(f"QuantLinear expects bf16 activations (bf16-true), got {x2.dtype}")
+        x2 = x2.contiguous()
+        M = x2.shape[0]
+        res = None if residual is None else residual.reshape(M, self.out_features).contiguous()
+        if M == 1:
+            y = ops.q4_gemv(x2.view(-1), self.qweight, self.scales, self.out_features, self.in_features, self.group,
+                            self.fmt, bias=self.bias, residual=None if res is None else res.view(-1),
+                            norm_weight=norm_weight, eps=norm_eps)
+        else:
+            if norm_weight is not None:
+                x2 = ops.rmsnorm(x2, norm_weight, norm_eps)
+            y = ops.q4_gemm(x2, self.qweight, self.scales, self.out_features, self.in_features, self.group, self.fmt,
+                            bias=self.bias, residual=res)
+        return y.view(*lead, self.out_features)
+
+    def extra_repr(self) -> str:
+        kind = "int4" if self.fmt == ops.FMT_Q4G else "nf4"
+        return f"in_features={self.in_features}, out_features={self.out_features}, {kind}, group={self.group}"
+
+
+class QuantizedPrecision:
+    """Stand-in for Lightning's ``BitsandbytesPrecision(mode, dtype)`` (generate/base.py:128-134)."""
+
+    def __init__(self, mode: str, dtype: torch.dtype = torch.bfloat16) -> None:
+        parse_mode(mode)
+        if dtype != torch.bfloat16:
+            raise NotImplementedError("the MI355X 4-bit path computes in bf16 (precision bf16-true)")
+        self.mode, self.dtype = mode, dtype
+
+    def convert_module(self, module: nn.Module, device: Optional[torch.device] = None) -> nn.Module:
+        """Replace every ``nn.Linear`` (lm_head included) by a ``QuantLinear`` quantized on ``device``."""
+        for name, child in list(module.named_children()):
+            if isinstance(child, nn.Linear):
+                setattr(module, name, QuantLinear.from_float(child.weight, child.bias, self.mode, device))
+            else:
+                self.convert_module(child, device)
+        return module

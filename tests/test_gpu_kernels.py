@@ -1,0 +1,247 @@
+"""Per-kernel parity on the MI355X: every HIP op through the C-ABI against the CPU oracle.
+
+Integer / byte work (quantizer packing, KV append, argmax) must be bit-exact; fp kernels are checked against an
+fp64/fp32 reference of the same op on the same bf16 inputs with the tolerance written in each test.
+"""
+
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import model as om
+from oracle import quant, synth
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def bf16_np(x: np.ndarray) -> np.ndarray:
+    return quant.bf16_bits_to_f32(quant.f32_to_bf16_bits(x))
+
+
+def to_dev_bf16(x: np.ndarray) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(DEV).to(torch.bfloat16)
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from lit_gpt import ops as _ops
+
+    _ops.load_library()
+    return _ops
+
+
+_CACHE = {}
+
+
+def _weights(N, K, name, std=0.02):
+    key = ("w", N, K, name)
+    if key not in _CACHE:
+        seed = abs(hash((N, K, name))) % (2 ** 31)
+        _CACHE[key] = (np.random.default_rng(seed).standard_normal((N, K), dtype=np.float32) * std)
+    return _CACHE[key]
+
+
+# ------------------------------------------------------------------------------------------------ quantizer
+@pytest.mark.parametrize("fmt,group", [(0, 128), (0, 64), (0, 32), (1, 64)])
+@pytest.mark.parametrize("in_bf16", [False, True])
+def test_quantizer_bit_exact(ops, fmt, group, in_bf16):
+    w = _weights(96, 512, f"qz{fmt}{group}")
+    w[3, :group] = 0.0  # an all-zero group (scale 0)
+    w[5, 7] = 0.5  # an outlier
+    if in_bf16:
+        w = bf16_np(w)
+    wt = torch.from_numpy(w).to(DEV)
+    if in_bf16:
+        wt = wt.to(torch.bfloat16)
+    qw, sc = ops.quantize(wt, fmt, group)
+    if fmt == 0:
+        p_ref, s_ref = quant.quantize_q4g(w, group)
+        np.testing.assert_array_equal(sc.view(torch.int16).cpu().numpy().view(np.uint16), s_ref)
+    else:
+        p_ref, s_ref = quant.quantize_nf4(w, group)
+        np.testing.assert_array_equal(sc.cpu().numpy(), s_ref)
+    np.testing.assert_array_equal(qw.cpu().numpy(), p_ref)
+
+
+# ------------------------------------------------------------------------------------------------ GEMV
+def _ref_linear(x, wdeq, bias=None):
+    y = x.astype(np.float64) @ wdeq.astype(np.float64).T
+    return y if bias is None else y + bias
+
+
+def _deq(ops, w, fmt, group):
+    key = ("d", id(w), fmt, group)
+    if key not in _CACHE:
+        p, s = (quant.quantize_q4g(w, group) if fmt == 0 else quant.quantize_nf4(w, group))
+        _CACHE[key] = quant.dequantize_q4g(p, s, group) if fmt == 0 else quant.dequantize_nf4(p, s, group)
+    return _CACHE[key]
+
+
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (0, 32)])
+@pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 11008), (1000, 256), (77, 1376), (640, 4096)])
+@pytest.mark.parametrize("variant", [-1, 0, 3, 6])
+def test_gemv_matches_reference(ops, fmt, group, N, K, variant):
+    if K % group:
+        pytest.skip("group does not divide K")
+    w = _weights(N, K, f"gv{N}x{K}")
+    x = bf16_np(synth.normal((K,), f"x{K}", 5, 1.0))
+    wt = torch.from_numpy(w).to(DEV)
+    qw, sc = ops.quantize(wt, fmt, group)
+    y = ops.q4_gemv(to_dev_bf16(x), qw, sc, N, K, group, fmt, variant=variant).float().cpu().numpy()
+    ref = _ref_linear(x, _deq(ops, w, fmt, group))
+    # bf16 output rounding (2^-8 relative) + fp32 accumulation differences
+    tol = np.abs(ref) * 2 ** -7 + 1e-3 * np.sqrt(K / 4096) * 0.02 * np.abs(x).mean() * 4
+    assert np.all(np.abs(y - ref) <= tol), float(np.max(np.abs(y - ref) - tol))
+
+
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
+def test_gemv_fused_norm_residual_bias(ops, fmt, group):
+    N, K = 1536, 1024
+    w = _weights(N, K, "gvf")
+    x = bf16_np(synth.normal((K,), "xf", 5, 2.0))
+    nw = bf16_np(1.0 + synth.normal((K,), "nw", 5, 0.2))
+    res = bf16_np(synth.normal((N,), "res", 5, 1.0))
+    bias = bf16_np(synth.normal((N,), "bias", 5, 0.1))
+    qw, sc = ops.quantize(torch.from_numpy(w).to(DEV), fmt, group)
+    y = ops.q4_gemv(to_dev_bf16(x), qw, sc, N, K, group, fmt, bias=to_dev_bf16(bias), residual=to_dev_bf16(res),
+                    norm_weight=to_dev_bf16(nw), eps=1e-5).float().cpu().numpy()
+    xn = om.rms_norm(torch.from_numpy(x).bfloat16(), torch.from_numpy(nw).bfloat16(), 1e-5).float().numpy()
+    h = bf16_np((_ref_linear(xn, _deq(ops, w, fmt, group)) + bias).astype(np.float32))
+    ref = h + res
+    assert np.max(np.abs(y - ref) - np.abs(ref) * 2 ** -7 - np.abs(h) * 2 ** -7) <= 2e-3
+
+
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
+def test_gemv_swiglu(ops, fmt, group):
+    N, K = 11008, 4096
+    w1, w2 = _weights(N, K, "s1"), _weights(N, K, "s2")
+    x = bf16_np(synth.normal((K,), "xs", 5, 1.0))
+    nw = bf16_np(np.ones(K, np.float32))
+    q1, s1 = ops.quantize(torch.from_numpy(w1).to(DEV), fmt, group)
+    q2, s2 = ops.quantize(torch.from_numpy(w2).to(DEV), fmt, group)
+    y = ops.q4_gemv_swiglu(to_dev_bf16(x), q1, s1, q2, s2, N, K, group, fmt, norm_weight=to_dev_bf16(nw)
+                           ).float().cpu().numpy()
+    xn = om.rms_norm(torch.from_numpy(x).bfloat16(), torch.from_numpy(nw).bfloat16(), 1e-5).float().numpy()
+    a = _ref_linear(xn, _deq(ops, w1, fmt, group))
+    b = _ref_linear(xn, _deq(ops, w2, fmt, group))
+    ref = (a / (1 + np.exp(-a))) * b
+    assert np.max(np.abs(y - ref) - np.abs(ref) * 2 ** -6) <= 1e-3
+
+
+# ------------------------------------------------------------------------------------------------ GEMM (prefill)
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
+@pytest.mark.parametrize("M,N,K", [(200, 768, 256), (2048, 1024, 4096), (5, 640, 1376), (130, 4096, 11008)])
+def test_gemm_matches_reference(ops, fmt, group, M, N, K):
+    if K % group:
+        group = 32 if fmt == 0 else pytest.skip("nf4 block must divide K")
+    w = _weights(N, K, f"gm{N}x{K}")
+    x = bf16_np(synth.normal((M, K), f"gx{M}x{K}", 5, 1.0))
+    qw, sc = ops.quantize(torch.from_numpy(w).to(DEV), fmt, group)
+    res = bf16_np(synth.normal((M, N), "gres", 5, 1.0))
+    y = ops.q4_gemm(to_dev_bf16(x), qw, sc, N, K, group, fmt, residual=to_dev_bf16(res)).float().cpu().numpy()
+    wd = _deq(ops, w, fmt, group)
+    if fmt == 1:
+        wd = bf16_np(wd)  # nf4 feeds the MFMA bf16(NF4 * absmax), as bitsandbytes' dequantize_4bit does
+    h = _ref_linear(x, wd)
+    ref = bf16_np(h.astype(np.float32)) + res
+    err = np.abs(y - ref) - (np.abs(ref) + np.abs(h)) * 2 ** -7
+    assert np.max(err) <= 2e-3, float(np.max(err))
+
+
+# ------------------------------------------------------------------------------------------------ row ops
+def test_rmsnorm_matches_oracle(ops, golden):
+    g = golden("g3_ops.npz")
+    x = torch.from_numpy(g["rms_x"]).bfloat16()
+    w = torch.from_numpy(g["rms_w"]).bfloat16()
+    y = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-5).float().cpu()
+    ref = om.rms_norm(x, w, 1e-5).float()
+    # one bf16 ulp: the fp32 sum of squares is reduced in a different order than torch's CPU mean
+    assert torch.all((y - ref).abs() <= ref.abs() * 2 ** -7 + 1e-6)
+    assert (y == ref).float().mean() > 0.97
+
+
+@pytest.mark.parametrize("H,G,hs,n_elem", [(32, 32, 128, 128), (8, 2, 128, 128), (4, 1, 64, 64), (12, 12, 64, 16)])
+def test_rope_kv_append_bit_exact(ops, H, G, hs, n_elem):
+    T, S = 7, 40
+    qkv = bf16_np(synth.normal((T, (H + 2 * G) * hs), "qkv", 5, 1.0))
+    cos, sin = om.build_rope_cache(S, n_elem, 10000)
+    pos = torch.tensor([3, 4, 5, 6, 7, 8, 30])
+    kc = torch.zeros(G, S, hs, dtype=torch.bfloat16, device=DEV)
+    vc = torch.zeros_like(kc)
+    q = ops.rope_kv_append(to_dev_bf16(qkv), kc, vc, pos.to(DEV), pos.to(DEV), cos.to(DEV), sin.to(DEV), H, G, hs,
+                           n_elem).float().cpu()
+    qpk = H // G
+    t = torch.from_numpy(qkv).bfloat16().view(T, G, qpk + 2, hs)
+    c, s = cos[pos], sin[pos]
+    rq = t[:, :, :qpk].reshape(T, H, hs).transpose(0, 1)
+    rk = t[:, :, qpk].transpose(0, 1)
+    rq = torch.cat((om.apply_rope(rq[..., :n_elem], c, s), rq[..., n_elem:]), -1).transpose(0, 1)
+    rk = torch.cat((om.apply_rope(rk[..., :n_elem], c, s), rk[..., n_elem:]), -1)
+    assert torch.equal(q, rq.float())
+    kref = torch.zeros(G, S, hs, dtype=torch.bfloat16)
+    vref = torch.zeros_like(kref)
+    kref[:, pos] = rk
+    vref[:, pos] = t[:, :, qpk + 1].transpose(0, 1)
+    assert torch.equal(kc.cpu(), kref) and torch.equal(vc.cpu(), vref)
+
+
+@pytest.mark.parametrize("H,G,hs", [(32, 32, 128), (64, 8, 128), (8, 1, 128), (4, 2, 64)])
+@pytest.mark.parametrize("T,positions", [(1, [0]), (1, [2047]), (1, [2302]), (5, [100, 101, 102, 103, 104]),
+                                          (3, [0, 1, 2])])
+@pytest.mark.parametrize("splits", [1, 36])
+def test_attention_matches_reference(ops, H, G, hs, T, positions, splits):
+    S = 2304
+    q = bf16_np(synth.normal((T, H, hs), "aq", 5, 1.0))
+    k = bf16_np(synth.normal((G, S, hs), "ak", 5, 1.0))
+    v = bf16_np(synth.normal((G, S, hs), "av", 5, 1.0))
+    pos = torch.tensor(positions, dtype=torch.int64)
+    scale = 1.0 / math.sqrt(hs)
+    y = ops.attention(to_dev_bf16(q), to_dev_bf16(k), to_dev_bf16(v), pos.to(DEV), H, G, hs, scale,
+                      n_splits=splits).float().cpu().numpy().reshape(T, H, hs)
+    qpk = H // G
+    ref = np.zeros((T, H, hs))
+    for t, p in enumerate(positions):
+        for h in range(H):
+            kk, vv = k[h // qpk, : p + 1].astype(np.float64), v[h // qpk, : p + 1].astype(np.float64)
+            s = kk @ q[t, h].astype(np.float64) * scale
+            e = np.exp(s - s.max())
+            ref[t, h] = (e / e.sum()) @ vv
+    assert np.max(np.abs(y - ref) - np.abs(ref) * 2 ** -7) <= 1e-4
+
+
+def test_argmax_known_answers_and_ties(ops, golden):
+    g = golden("g3_ops.npz")
+    logits = torch.from_numpy(g["sample_logits"]).float()
+    assert ops.argmax(logits[0, -1].bfloat16().to(DEV)).item() == int(g["sample_t0"][0])
+    tl = torch.from_numpy(g["sample_ties_logits"])[0, -1]
+    assert ops.argmax(tl.bfloat16().to(DEV)).item() == int(g["sample_ties_t0"][0])
+    big = torch.full((32000,), -3.0)
+    big[[17, 31999, 20000]] = 5.0
+    tok = torch.zeros(1, dtype=torch.int32, device=DEV)
+    pos = torch.tensor([41], device=DEV)
+    assert ops.argmax(big.bfloat16().to(DEV), token_out=tok, pos_inout=pos).item() == 17
+    assert tok.item() == 17 and pos.item() == 42
+
+
+def test_embedding_and_add(ops):
+    V, C = 500, 256
+    table = bf16_np(synth.normal((V, C), "emb", 5, 1.0))
+    idx = torch.tensor([3, 499, 0, 3], dtype=torch.int32)
+    out = ops.embedding(idx.to(DEV), to_dev_bf16(table)).float().cpu().numpy()
+    np.testing.assert_array_equal(out, table[idx.numpy()])
+    a, b = to_dev_bf16(table[:4]), to_dev_bf16(table[4:8])
+    assert torch.equal(ops.add(a, b), (a.float() + b.float()).bfloat16())
+
+
+def test_errors_are_raised(ops):
+    x = torch.zeros(100, dtype=torch.bfloat16, device=DEV)
+    qw = torch.zeros(10, 50, dtype=torch.uint8, device=DEV)
+    sc = torch.zeros(10, 1, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError, match="multiple of 32"):
+        ops.q4_gemv(x, qw, sc, 10, 100, 100, 0)
+    with pytest.raises(RuntimeError, match="GPU tensor"):
+        ops.rmsnorm(torch.zeros(4, 8, dtype=torch.bfloat16), torch.ones(8, dtype=torch.bfloat16), 1e-5)

@@ -1,0 +1,192 @@
+"""Host-side logic on the CPU: Config, TP sharding (known answers from the reference), hook placement, gloo TP."""
+
+import os
+import socket
+from dataclasses import replace
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import model as om
+from oracle import synth
+from oracle.tp import shard_linear
+
+
+def test_config_derived_fields_match_reference():
+    from lit_gpt import Config
+
+    c = Config.from_name("Llama-2-7b-hf")
+    assert (c.n_layer, c.n_head, c.n_embd, c.n_query_groups, c.head_size) == (32, 32, 4096, 32, 128)
+    assert (c.padded_vocab_size, c.intermediate_size, c.rope_n_elem, c.block_size) == (32000, 11008, 128, 4096)
+    c = Config.from_name("Llama-2-70b-chat-hf")
+    assert (c.n_query_groups, c.head_size, c.intermediate_size) == (8, 128, 28672)
+    c = Config.from_name("Mixtral-8x7B-v0.1")
+    assert (c.n_expert, c.n_expert_per_token, c.rope_base, c.block_size, c.padded_vocab_size) == (8, 2, 1000000, 32768, 32000)
+    c = Config.from_name("pythia-160m")
+    assert (c.padded_vocab_size, c.rope_n_elem, c.intermediate_size) == (50304, 16, 3072)
+    with pytest.raises(ValueError, match="not a supported config"):
+        Config.from_name("nope")
+    with pytest.raises(ValueError, match="intermediate_size"):
+        Config(_mlp_class="LLaMAMLP")
+
+
+def test_config_from_json_and_checkpoint(tmp_path):
+    import json
+
+    from lit_gpt import Config
+
+    (tmp_path / "lit_config.json").write_text(json.dumps(
+        {"name": "x", "org": "me", "block_size": 128, "vocab_size": 50, "n_layer": 2, "n_head": 4, "n_embd": 8,
+         "condense_ratio": 2}))
+    c = Config.from_json(tmp_path / "lit_config.json")
+    assert c.hf_config == {"name": "x", "org": "me"} and c.rope_condense_ratio == 2 and c.padded_vocab_size == 512
+    assert Config.from_checkpoint(tmp_path).n_layer == 2
+    with pytest.raises(FileNotFoundError):
+        Config.from_checkpoint(tmp_path / "missing")
+
+
+def test_tensor_parallel_linear_known_answers(golden):
+    """Same known answers as the reference's tests/test_generate_tp.py:14-40 and golden g4."""
+    from generate.tp import Fabric, tensor_parallel_linear
+
+    def get_linear(bias=True):
+        lin = torch.nn.Linear(8, 8, bias=bias)
+        lin.weight.data = torch.arange(64, dtype=torch.float32).reshape(8, 8)
+        if bias:
+            lin.bias.data = torch.arange(8, dtype=torch.float32)
+        return lin
+
+    lin = get_linear()
+    tensor_parallel_linear(Fabric(4, 2), lin, "colwise")
+    torch.testing.assert_close(lin.weight, torch.arange(32, 48, dtype=torch.float32).reshape(2, 8))
+    torch.testing.assert_close(lin.bias, torch.arange(4, 6, dtype=torch.float32))
+    lin = get_linear(bias=False)
+    tensor_parallel_linear(Fabric(4, 2), lin, "rowwise")
+    e = torch.arange(4, 62, 8, dtype=torch.float32).reshape(8, 1)
+    torch.testing.assert_close(lin.weight, torch.cat([e, e + 1], dim=1))
+    g = golden("g4_tp.npz")
+    for world in (2, 4, 8):
+        for rank in range(world):
+            for style in ("colwise", "rowwise"):
+                key = f"w{world}_r{rank}_{style}"
+                lin = torch.nn.Linear(16, 24, bias=True)
+                lin.weight.data = torch.arange(24 * 16, dtype=torch.float32).reshape(24, 16)
+                lin.bias.data = torch.arange(24, dtype=torch.float32)
+                if f"{key}_error" in g:
+                    with pytest.raises(ValueError):
+                        tensor_parallel_linear(Fabric(world, rank), lin, style)
+                    continue
+                tensor_parallel_linear(Fabric(world, rank), lin, style)
+                np.testing.assert_array_equal(lin.weight.detach().numpy(), g[f"{key}_weight"])
+                np.testing.assert_array_equal(lin.bias.detach().numpy(), g[f"{key}_bias"])
+
+
+@pytest.mark.parametrize("name", ["Llama-2-70b-hf", "Mixtral-8x7B-v0.1"])
+def test_tensor_parallel_hook_placement(name):
+    """tests/test_generate_tp.py:43-103 analogue: hooks on attn and mlp (per expert for MoE), config / 8."""
+    from generate.tp import Fabric, tensor_parallel
+    from lit_gpt import GPT
+
+    with torch.device("meta"):
+        model = GPT.from_name(name, n_layer=3, n_expert=2)
+    config = replace(model.config)
+    tensor_parallel(Fabric(8, 1), model)
+    hooks = {}
+    for n, m in model.named_modules():
+        for h in m._forward_hooks.values():
+            hooks.setdefault(n, []).append((h.func.__name__, h.args))
+    if name.startswith("Mixtral"):
+        expected = {f"transformer.h.{i}.{s}" for i in range(3) for s in ("attn", "mlp.experts.0", "mlp.experts.1")}
+    else:
+        expected = {f"transformer.h.{i}.{s}" for i in range(3) for s in ("attn", "mlp")}
+    assert set(hooks) == expected
+    assert all(v == [("all_reduce_output", (8,))] for v in hooks.values())
+    assert model.config.n_embd * 8 == config.n_embd and model.config.n_head * 8 == config.n_head
+    assert model.config.n_query_groups * 8 == config.n_query_groups
+
+
+def test_tensor_parallel_divisibility_error():
+    from generate.tp import Fabric, tensor_parallel
+    from lit_gpt import GPT
+
+    with torch.device("meta"):
+        model = GPT.from_name("Llama-2-7b-hf", n_layer=1)
+    with pytest.raises(ValueError, match="not evenly divisible"):
+        tensor_parallel(Fabric(3, 0), model)
+
+
+# ---------------------------------------------------------------------------------------- gloo, world_size 2
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _tp_worker(rank, world, port, q):
+    """Each rank shards the float weights exactly as generate/tp.py does, computes its partial attention/MLP
+    outputs with the oracle's math and sums them with the same all_reduce_output hook function (gloo here,
+    RCCL on the GPU); logits must equal the single-process model."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from generate.tp import Fabric, all_reduce_output
+        from lit_gpt import Config
+
+        cfg = Config.from_name("Llama-2-70b-hf", n_layer=2, n_embd=256, n_head=4, n_query_groups=2,
+                               intermediate_size=512, vocab_size=500, padding_multiple=64, block_size=64)
+        sd = synth.state_dict(cfg, seed=3)
+        f = Fabric(world, rank)
+        local = dict(sd)
+        for i in range(cfg.n_layer):
+            p = f"transformer.h.{i}"
+            for name, style in (("attn.attn", "colwise"), ("attn.proj", "rowwise"), ("mlp.fc_1", "colwise"),
+                                ("mlp.fc_2", "colwise"), ("mlp.proj", "rowwise")):
+                local[f"{p}.{name}.weight"], _ = shard_linear(sd[f"{p}.{name}.weight"], None, style, world, rank)
+        lcfg = replace(cfg)
+        lcfg.n_head, lcfg.n_embd, lcfg.n_query_groups = cfg.n_head // world, cfg.n_embd // world, cfg.n_query_groups // world
+        lcfg.head_size = cfg.head_size
+        m = om.OracleGPT(lcfg, local)
+        m.cfg.n_embd = cfg.n_embd  # residual stream keeps the full width
+
+        orig_attn, orig_mlp = m._attn, m._mlp
+        m._attn = lambda *a: all_reduce_output(world, None, None, orig_attn(*a).contiguous())
+        m._mlp = lambda *a: all_reduce_output(world, None, None, orig_mlp(*a).contiguous())
+        m.set_kv_cache(20)
+        ids = torch.from_numpy(synth.token_ids(12, cfg.vocab_size, seed=3))
+        out = [m.forward(ids[:8], torch.arange(8))[-1]]
+        for t in range(8, 12):
+            out.append(m.forward(ids[t:t + 1], torch.tensor([t]))[-1])
+        if rank == 0:
+            q.put(torch.stack(out).numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_tp2_gloo_matches_single_process():
+    from lit_gpt import Config
+
+    cfg = Config.from_name("Llama-2-70b-hf", n_layer=2, n_embd=256, n_head=4, n_query_groups=2,
+                           intermediate_size=512, vocab_size=500, padding_multiple=64, block_size=64)
+    m = om.OracleGPT(cfg, synth.state_dict(cfg, seed=3))
+    m.set_kv_cache(20)
+    ids = torch.from_numpy(synth.token_ids(12, cfg.vocab_size, seed=3))
+    ref = [m.forward(ids[:8], torch.arange(8))[-1]]
+    for t in range(8, 12):
+        ref.append(m.forward(ids[t:t + 1], torch.tensor([t]))[-1])
+    ref = torch.stack(ref).numpy()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_tp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=300)
+        assert p.exitcode == 0
+    np.testing.assert_allclose(got, ref, rtol=0, atol=2e-5)
