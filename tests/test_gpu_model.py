@@ -39,9 +39,8 @@ def build_gpu_model(cfg, sd, mode, max_seq):
     from lit_gpt import GPT
     from lit_gpt.quantize import QuantizedPrecision
 
-    with torch.device("meta"):
-        model = GPT(cfg)
-    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()}, assign=True)
+    model = GPT(cfg)
+    model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     model = model.to(device=DEV, dtype=torch.bfloat16)
     QuantizedPrecision(mode).convert_module(model, DEV)
     model.max_seq_length = max_seq
