@@ -77,11 +77,13 @@ int lga_swiglu(const void* a, const void* b, void* y, long n, lga_stream_t strea
 
 /* -- attention over the KV cache (SDPA with the input_pos mask rows, lit_gpt/model.py:651,658-665) --------
  * q (T, H, hs); caches (G, max_seq, hs); query t attends keys 0..input_pos[t]; y (T, H*hs).
- * n_splits > 1 splits the sequence (flash-decoding) and needs `workspace` of
- * lga_attention_workspace_bytes(T, H, hs, n_splits) bytes. head_size in {64, 128}; H/G in {1,2,4,8}. */
+ * n_splits > 1 splits keys 0..input_pos[t] evenly (flash-decoding; the split merge happens in the same launch
+ * by the last-arriving workgroup) and needs `workspace` of lga_attention_workspace_bytes(T, H, hs, n_splits) bytes
+ * plus `counters` (T * G uint32, zeroed once at allocation; the kernel re-arms them).
+ * head_size in {64, 128}; H/G in {1,2,4,8}; n_splits * H/G <= 4 * head_size. */
 int lga_attention(const void* q, const void* k_cache, const void* v_cache, const int64_t* input_pos, void* y,
-                  float* workspace, int T, int n_head, int n_query_groups, int head_size, int max_seq, int n_splits,
-                  float scale, lga_stream_t stream);
+                  float* workspace, unsigned* counters, int T, int n_head, int n_query_groups, int head_size,
+                  int max_seq, int n_splits, float scale, lga_stream_t stream);
 size_t lga_attention_workspace_bytes(int T, int n_head, int head_size, int n_splits);
 
 /* -- greedy sampling (generate/base.py:30-47 at temperature 0): lowest index among the maxima; optionally

@@ -1,4 +1,4 @@
-// Cached causal attention for decode (T = 1, split over the sequence) and prefill (T rows, one split).
+// Cached causal attention for decode (T = 1, split over the sequence) and prefill (T rows).
 //
 // Replaces CausalSelfAttention.scaled_dot_product_attention (lit_gpt/model.py:651, :658-665): SDPA of q
 // against the full max_seq-long cache under the bool mask row(s) selected by input_pos (model.py:509). The
@@ -7,11 +7,14 @@
 // KV cache layout (HBM): k, v = [G][max_seq][hs] bf16 per layer (un-expanded query groups); one key row is
 // hs*2 contiguous bytes, read by a "row group" of hs/8 lanes at 16 B per lane.
 //
-// Work decomposition: grid (splits, G, T); a 256-thread workgroup owns one (split, group, query row) and all
-// q_per_kv query heads of that group (GQA/MQA read each K/V row once). Inside, every row group streams its
-// own keys with an independent online softmax; states are merged per wave with shuffles, then across the
-// 4 waves in LDS. With splits > 1 the per-split (m, l, o) go to an fp32 workspace that lga_attention_combine
-// merges (flash-decoding); with one split the bf16 output is written directly.
+// Work decomposition: grid (splits, G, T); a 256-thread workgroup owns one (split, query group, query row) and
+// all q_per_kv heads of that group (GQA/MQA read each K/V row once). The split boundaries are computed in the
+// kernel from the live position (chunk = ceil((p+1)/splits)), so every split is busy whatever the context
+// length and a captured HIP graph stays valid as p grows. Inside, each row group streams UNR keys per step
+// (2*UNR 16-B loads in flight per lane) with an online softmax; row groups merge with shuffles, waves via LDS.
+// With splits > 1 every workgroup publishes (m, l, o) write-through (sc1) and bumps a per-(t, group) counter;
+// the workgroup that arrives last merges the splits and writes the bf16 output (flash-decoding combine inside
+// the same launch; MI355X_MICROARCH.md "Valid forms" row 1), then re-arms the counter for the next launch.
 #include "common.h"
 
 namespace lga {
@@ -26,35 +29,46 @@ __device__ __forceinline__ float row_group_sum(float v) {
   return v;
 }
 
-template <int HS, int QPK>
+__device__ __forceinline__ void unpack8(const uint4 v, float* f) {
+  const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = bflo(d[i]);
+    f[2 * i + 1] = bfhi(d[i]);
+  }
+}
+
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+template <int HS, int QPK, int UNR>
 __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
                                                    const uint16_t* __restrict__ vc,
                                                    const int64_t* __restrict__ input_pos, uint16_t* __restrict__ y,
-                                                   float* __restrict__ ws, int n_head, int max_seq, int chunk,
-                                                   float scale) {
-  constexpr int LPR = HS / 8;      // lanes per key row
-  constexpr int RGW = 64 / LPR;    // row groups per wave
-  constexpr int RG = 4 * RGW;      // row groups per workgroup
+                                                   float* __restrict__ ws, unsigned* __restrict__ cnt, int n_head,
+                                                   int max_seq, float scale) {
+  constexpr int LPR = HS / 8;    // lanes per key row
+  constexpr int RGW = 64 / LPR;  // row groups per wave
+  constexpr int RG = 4 * RGW;    // row groups per workgroup
   const int split = blockIdx.x, g = blockIdx.y, t = blockIdx.z;
   const int n_splits = gridDim.x, G = gridDim.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int rg = wave * RGW + lane / LPR;  // row group id in the workgroup
-  const int sub = lane % LPR;              // 8-dim slice of the row
+  const int rg = wave * RGW + lane / LPR;
+  const int sub = lane % LPR;
   const long p = input_pos[t];
+  const int L = (int)min(p + 1, (long)max_seq);  // keys 0..p (never past the cache)
+  const int chunk = (L + n_splits - 1) / n_splits;
   const int k_lo = split * chunk;
-  const int k_hi = (int)min(min((long)k_lo + chunk, p + 1), (long)max_seq);  // never read past the cache
+  const int k_hi = min(k_lo + chunk, L);
 
   float qf[QPK][8];
 #pragma unroll
-  for (int h = 0; h < QPK; ++h) {
-    const uint4 qv = *(const uint4*)(q + ((size_t)t * n_head + (size_t)g * QPK + h) * HS + sub * 8);
-    const uint32_t d[4] = {qv.x, qv.y, qv.z, qv.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      qf[h][2 * j] = bflo(d[j]);
-      qf[h][2 * j + 1] = bfhi(d[j]);
-    }
-  }
+  for (int h = 0; h < QPK; ++h)
+    unpack8(*(const uint4*)(q + ((size_t)t * n_head + (size_t)g * QPK + h) * HS + sub * 8), qf[h]);
   float m[QPK], l[QPK], o[QPK][8];
 #pragma unroll
   for (int h = 0; h < QPK; ++h) {
@@ -65,32 +79,43 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
   }
   const uint16_t* kbase = kc + (size_t)g * max_seq * HS + sub * 8;
   const uint16_t* vbase = vc + (size_t)g * max_seq * HS + sub * 8;
-  for (int j = k_lo + rg; j < k_hi; j += RG) {
-    const uint4 kv = *(const uint4*)(kbase + (size_t)j * HS);
-    const uint4 vv = *(const uint4*)(vbase + (size_t)j * HS);
-    const uint32_t kd[4] = {kv.x, kv.y, kv.z, kv.w};
-    const uint32_t vd[4] = {vv.x, vv.y, vv.z, vv.w};
-    float kf[8], vf[8];
+  for (int j0 = k_lo + rg; j0 < k_hi; j0 += RG * UNR) {
+    uint4 kv[UNR], vv[UNR];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      kf[2 * i] = bflo(kd[i]);
-      kf[2 * i + 1] = bfhi(kd[i]);
-      vf[2 * i] = bflo(vd[i]);
-      vf[2 * i + 1] = bfhi(vd[i]);
+    for (int u = 0; u < UNR; ++u) {
+      const int j = min(j0 + u * RG, k_hi - 1);  // clamped duplicate rows are masked below
+      kv[u] = *(const uint4*)(kbase + (size_t)j * HS);
+      vv[u] = *(const uint4*)(vbase + (size_t)j * HS);
     }
 #pragma unroll
     for (int h = 0; h < QPK; ++h) {
-      float s = 0.0f;
+      float s[UNR];
+      float mx = m[h];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) s = fmaf(qf[h][i], kf[i], s);
-      s = row_group_sum<LPR>(s) * scale;
-      const float mn = fmaxf(m[h], s);
-      const float c = expf(m[h] - mn);  // m = -inf on the first key -> 0
-      const float e = expf(s - mn);
-      l[h] = fmaf(l[h], c, e);
+      for (int u = 0; u < UNR; ++u) {
+        float kf[8];
+        unpack8(kv[u], kf);
+        float d = 0.0f;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) o[h][i] = fmaf(o[h][i], c, e * vf[i]);
-      m[h] = mn;
+        for (int i = 0; i < 8; ++i) d = fmaf(qf[h][i], kf[i], d);
+        const float sd = row_group_sum<LPR>(d) * scale;  // whole row group active: DPP stays inside it
+        s[u] = (j0 + u * RG < k_hi) ? sd : -INFINITY;
+        mx = fmaxf(mx, s[u]);
+      }
+      const float c = expf(m[h] - mx);  // m = -inf (first step) -> 0
+      l[h] *= c;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[h][i] *= c;
+#pragma unroll
+      for (int u = 0; u < UNR; ++u) {
+        const float e = expf(s[u] - mx);  // masked keys: exp(-inf) = 0
+        l[h] += e;
+        float vf[8];
+        unpack8(vv[u], vf);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[h][i] = fmaf(e, vf[i], o[h][i]);
+      }
+      m[h] = mx;
     }
   }
   // merge the RGW row groups of this wave (lanes differing in the bits above log2(LPR))
@@ -104,16 +129,13 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
       const float cb = mn == -INFINITY ? 0.0f : expf(mo - mn);
       l[h] = l[h] * ca + lo * cb;
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const float oo = __shfl_xor(o[h][i], off);
-        o[h][i] = o[h][i] * ca + oo * cb;
-      }
+      for (int i = 0; i < 8; ++i) o[h][i] = o[h][i] * ca + __shfl_xor(o[h][i], off) * cb;
       m[h] = mn;
     }
   }
-  // merge the 4 waves through LDS
   __shared__ float sm[4][QPK], sl[4][QPK];
   __shared__ float so[4][QPK][HS];
+  __shared__ unsigned s_last;
   if (lane < LPR) {
 #pragma unroll
     for (int h = 0; h < QPK; ++h) {
@@ -126,6 +148,7 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
     }
   }
   __syncthreads();
+  const size_t row0 = (size_t)t * n_head + (size_t)g * QPK;  // first head row of this group
   for (int it = threadIdx.x; it < QPK * HS; it += 256) {
     const int h = it / HS, d = it % HS;
     float mx = -INFINITY;
@@ -138,76 +161,85 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
       lt += sl[w][h] * c;
       ot += so[w][h][d] * c;
     }
-    const int head = g * QPK + h;
     if (n_splits == 1) {
-      y[((size_t)t * n_head + head) * HS + d] = f2bf(ot / lt);
+      y[(row0 + h) * HS + d] = f2bf(ot / lt);
     } else {
-      float* wsr = ws + (((size_t)t * n_head + head) * n_splits + split) * (HS + 2);
-      wsr[2 + d] = ot;
+      float* wsr = ws + ((row0 + h) * n_splits + split) * (HS + 2);
+      st_sc1(wsr + 2 + d, ot);
       if (d == 0) {
-        wsr[0] = mx;
-        wsr[1] = lt;
+        st_sc1(wsr, mx);
+        st_sc1(wsr + 1, lt);
       }
     }
   }
-  (void)G;
-}
-
-template <int HS>
-__global__ void __launch_bounds__(HS) combine_kernel(const float* __restrict__ ws, uint16_t* __restrict__ y,
-                                                     int n_head, int n_splits) {
-  const int h = blockIdx.x, t = blockIdx.y, d = threadIdx.x;
-  const float* base = ws + ((size_t)t * n_head + h) * n_splits * (HS + 2);
-  float mx = -INFINITY;
-  for (int s = 0; s < n_splits; ++s) mx = fmaxf(mx, base[s * (HS + 2)]);
-  float lt = 0.0f, ot = 0.0f;
-  for (int s = 0; s < n_splits; ++s) {
-    const float* r = base + s * (HS + 2);
-    if (r[1] == 0.0f) continue;
-    const float c = expf(r[0] - mx);
-    lt += r[1] * c;
-    ot += r[2 + d] * c;
+  if (n_splits == 1) return;
+  // ---- publish, then the last-arriving split of this (t, group) merges all splits ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_last = __hip_atomic_fetch_add(cnt + (size_t)t * G + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_last != (unsigned)(n_splits - 1)) return;
+  float* wm = &so[0][0][0];  // reuse LDS: [QPK][n_splits] weights (n_splits <= 4*HS)
+  for (int it = threadIdx.x; it < QPK * n_splits; it += 256) {
+    const int h = it / n_splits, s = it % n_splits;
+    wm[it] = ld_sc1(ws + ((row0 + h) * n_splits + s) * (HS + 2));
   }
-  y[((size_t)t * n_head + h) * HS + d] = f2bf(ot / lt);
+  __syncthreads();
+  for (int it = threadIdx.x; it < QPK * HS; it += 256) {
+    const int h = it / HS, d = it % HS;
+    float mx = -INFINITY;
+    for (int s = 0; s < n_splits; ++s) mx = fmaxf(mx, wm[h * n_splits + s]);
+    float lt = 0.0f, ot = 0.0f;
+    const float* base = ws + (row0 + h) * n_splits * (HS + 2);
+    for (int s = 0; s < n_splits; ++s) {
+      const float ms = wm[h * n_splits + s];
+      if (ms == -INFINITY) continue;  // empty split (l = 0, o = 0)
+      const float c = expf(ms - mx);
+      lt = fmaf(ld_sc1(base + s * (HS + 2) + 1), c, lt);
+      ot = fmaf(ld_sc1(base + s * (HS + 2) + 2 + d), c, ot);
+    }
+    y[(row0 + h) * HS + d] = f2bf(ot / lt);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(cnt + (size_t)t * G + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int HS>
-static int launch_hs(const void* q, const void* kc, const void* vc, const int64_t* pos, void* y, float* ws, int T,
-                     int H, int G, int max_seq, int n_splits, float scale, hipStream_t stream) {
-  const int qpk = H / G;
-  const int chunk = (max_seq + n_splits - 1) / n_splits;
+static int launch_hs(const void* q, const void* kc, const void* vc, const int64_t* pos, void* y, float* ws,
+                     unsigned* cnt, int T, int H, int G, int max_seq, int n_splits, float scale, hipStream_t stream) {
   const dim3 grid(n_splits, G, T);
-#define LGA_ATTN(QPK)                                                                                         \
-  attn_kernel<HS, QPK><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)kc, (const uint16_t*)vc, \
-                                                 pos, (uint16_t*)y, ws, H, max_seq, chunk, scale)
-  switch (qpk) {
-    case 1: LGA_ATTN(1); break;
-    case 2: LGA_ATTN(2); break;
-    case 4: LGA_ATTN(4); break;
-    case 8: LGA_ATTN(8); break;
+#define LGA_ATTN(QPK, UNR)                                                                                    \
+  attn_kernel<HS, QPK, UNR><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)kc,                 \
+                                                      (const uint16_t*)vc, pos, (uint16_t*)y, ws, cnt, H, max_seq, \
+                                                      scale)
+  switch (H / G) {
+    case 1: LGA_ATTN(1, 4); break;
+    case 2: LGA_ATTN(2, 4); break;
+    case 4: LGA_ATTN(4, 2); break;
+    case 8: LGA_ATTN(8, 2); break;
     default: lga_set_error("lga_attention: q_per_kv must be 1, 2, 4 or 8"); return (int)hipErrorInvalidValue;
   }
 #undef LGA_ATTN
-  if (n_splits > 1) combine_kernel<HS><<<dim3(H, T), HS, 0, stream>>>(ws, (uint16_t*)y, H, n_splits);
   return 0;
 }
 
 }  // namespace lga
 
 extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_cache, const int64_t* input_pos,
-                             void* y, float* workspace, int T, int n_head, int n_query_groups, int head_size,
-                             int max_seq, int n_splits, float scale, hipStream_t stream) {
+                             void* y, float* workspace, unsigned* counters, int T, int n_head, int n_query_groups,
+                             int head_size, int max_seq, int n_splits, float scale, hipStream_t stream) {
   LGA_CHECK_ARG(q && k_cache && v_cache && input_pos && y, "lga_attention: null pointer");
   LGA_CHECK_ARG(T > 0 && n_query_groups > 0 && n_head % n_query_groups == 0, "lga_attention: bad head geometry");
-  LGA_CHECK_ARG(n_splits >= 1 && n_splits <= max_seq, "lga_attention: bad n_splits");
-  LGA_CHECK_ARG(n_splits == 1 || workspace, "lga_attention: split attention needs a workspace");
+  LGA_CHECK_ARG(n_splits >= 1 && n_splits <= 512, "lga_attention: n_splits must be in [1, 512]");
+  LGA_CHECK_ARG(n_splits == 1 || (workspace && counters), "lga_attention: split attention needs workspace + counters");
+  LGA_CHECK_ARG(n_splits * (n_head / n_query_groups) <= 4 * head_size, "lga_attention: too many splits for the LDS merge");
   int rc;
   if (head_size == 128)
-    rc = lga::launch_hs<128>(q, k_cache, v_cache, input_pos, y, workspace, T, n_head, n_query_groups, max_seq,
-                             n_splits, scale, stream);
+    rc = lga::launch_hs<128>(q, k_cache, v_cache, input_pos, y, workspace, counters, T, n_head, n_query_groups,
+                             max_seq, n_splits, scale, stream);
   else if (head_size == 64)
-    rc = lga::launch_hs<64>(q, k_cache, v_cache, input_pos, y, workspace, T, n_head, n_query_groups, max_seq,
-                            n_splits, scale, stream);
+    rc = lga::launch_hs<64>(q, k_cache, v_cache, input_pos, y, workspace, counters, T, n_head, n_query_groups,
+                            max_seq, n_splits, scale, stream);
   else {
     lga_set_error("lga_attention: head_size must be 64 or 128");
     return (int)hipErrorInvalidValue;
@@ -216,6 +248,7 @@ extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_c
   LGA_LAUNCH_RETURN();
 }
 
+// fp32 partials (T * H * n_splits * (hs + 2)); the counters (T * G uint32) must be zeroed once at allocation
 extern "C" size_t lga_attention_workspace_bytes(int T, int n_head, int head_size, int n_splits) {
   return n_splits <= 1 ? 0 : (size_t)T * n_head * n_splits * (head_size + 2) * sizeof(float);
 }

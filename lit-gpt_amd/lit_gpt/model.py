@@ -30,7 +30,6 @@ from lit_gpt import ops
 from lit_gpt.config import Config
 from lit_gpt.rmsnorm import RMSNorm
 
-_SPLIT_CHUNK = 64  # keys per decode-attention workgroup (flash-decoding split size)
 
 
 def _gpu_only(what: str) -> None:
@@ -215,8 +214,14 @@ class CausalSelfAttention(nn.Module):
         sin = sin.to(device=dev, dtype=torch.float32).contiguous()
         q = ops.rope_kv_append(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem)
         S = kc.size(-2)
-        n_splits = max(1, math.ceil(S / _SPLIT_CHUNK)) if T == 1 else 1
-        y = ops.attention(q, kc, vc, pos, H, G, hs, 1.0 / math.sqrt(hs), n_splits)
+        ws = None
+        n_splits = 1
+        if T == 1:
+            n_splits = ops.decode_splits(G, H // G, hs, S)
+            ws = getattr(self, "_attn_ws", None)
+            if ws is None or ws.key != (1, H, G, hs, n_splits) or ws.counters.device != dev:
+                ws = self._attn_ws = ops.AttentionWorkspace(1, H, G, hs, n_splits, dev)
+        y = ops.attention(q, kc, vc, pos, H, G, hs, 1.0 / math.sqrt(hs), n_splits, workspace=ws)
         out = _lin(self.proj, y.view(1, T, H * hs), residual=residual)
         return out.view(B, T, -1)
 

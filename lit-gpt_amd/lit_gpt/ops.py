@@ -43,7 +43,7 @@ SIGNATURES = {
     "lga_embedding": [_P, _I, _P, _P, _I, _I, _I, _P],
     "lga_add": [_P, _P, _P, _L, _P],
     "lga_swiglu": [_P, _P, _P, _L, _P],
-    "lga_attention": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
+    "lga_attention": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_attention_workspace_bytes": [_I, _I, _I, _I],
     "lga_argmax": [_P, _I, _P, _P, _P, _P],
 }
@@ -174,20 +174,43 @@ def rope_kv_append(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin, n_head,
     return q
 
 
+class AttentionWorkspace:
+    """Persistent split-attention scratch: fp32 partials + per-(row, group) arrival counters. The counters are
+    zeroed once here; the kernel's last-arriving workgroup re-arms them, so the buffers are reusable across
+    launches and HIP-graph replays (allocate before capture)."""
+
+    def __init__(self, T: int, n_head: int, n_query_groups: int, head_size: int, n_splits: int, device) -> None:
+        nbytes = load_library().lga_attention_workspace_bytes(T, n_head, head_size, n_splits)
+        self.key = (T, n_head, n_query_groups, head_size, n_splits)
+        self.partials = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=device)
+        self.counters = torch.zeros(T * n_query_groups, dtype=torch.int32, device=device)
+
+
 def attention(q, k_cache, v_cache, input_pos, n_head, n_query_groups, head_size, scale, n_splits=1,
-              workspace=None, out=None):
+              workspace: Optional[AttentionWorkspace] = None, out=None):
+    """y (T, H*hs): causal attention of q (T, H, hs) over the (G, max_seq, hs) caches, keys <= input_pos[t]."""
     T = q.shape[0]
     max_seq = k_cache.shape[-2]
     y = out if out is not None else torch.empty(T, n_head * head_size, dtype=torch.bfloat16, device=q.device)
-    if n_splits > 1 and workspace is None:
-        nbytes = load_library().lga_attention_workspace_bytes(T, n_head, head_size, n_splits)
-        workspace = torch.empty(nbytes // 4, dtype=torch.float32, device=q.device)
+    if n_splits > 1:
+        if workspace is None or workspace.key != (T, n_head, n_query_groups, head_size, n_splits):
+            workspace = AttentionWorkspace(T, n_head, n_query_groups, head_size, n_splits, q.device)
+        ws, cnt = _dev(workspace.partials, "workspace", torch.float32), _dev(workspace.counters, "counters", torch.int32)
+    else:
+        ws = cnt = None
     _check(load_library().lga_attention(
         _dev(q, "q", torch.bfloat16), _dev(k_cache, "k_cache", torch.bfloat16),
         _dev(v_cache, "v_cache", torch.bfloat16), _dev(input_pos, "input_pos", torch.int64),
-        _dev(y, "y", torch.bfloat16), None if workspace is None else _dev(workspace, "workspace", torch.float32),
-        T, n_head, n_query_groups, head_size, max_seq, n_splits, float(scale), _stream()))
+        _dev(y, "y", torch.bfloat16), ws, cnt, T, n_head, n_query_groups, head_size, max_seq, n_splits, float(scale),
+        _stream()))
     return y
+
+
+def decode_splits(n_query_groups: int, q_per_kv: int, head_size: int, max_seq: int, n_cu: int = 256) -> int:
+    """Sequence splits for T = 1 attention: ~2 workgroups per CU across all query groups."""
+    s = max(1, (2 * n_cu) // max(1, n_query_groups))
+    s = min(s, max(1, max_seq // 16), 512, (4 * head_size) // q_per_kv)
+    return s
 
 
 def embedding(idx, table, out=None):

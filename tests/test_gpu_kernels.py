@@ -213,6 +213,23 @@ def test_attention_matches_reference(ops, H, G, hs, T, positions, splits):
     assert np.max(np.abs(y - ref) - np.abs(ref) * 2 ** -7) <= 1e-4
 
 
+def test_attention_split_counters_rearm_across_launches(ops):
+    """The in-launch split merge re-arms its counters: repeated launches on one workspace stay correct."""
+    H, G, hs, S = 32, 32, 128, 2304
+    q = to_dev_bf16(synth.normal((1, H, hs), "rq", 5, 1.0))
+    k = to_dev_bf16(synth.normal((G, S, hs), "rk", 5, 1.0))
+    v = to_dev_bf16(synth.normal((G, S, hs), "rv", 5, 1.0))
+    ws = ops.AttentionWorkspace(1, H, G, hs, 16, DEV)
+    outs = []
+    for p in (2047, 5, 2047, 0, 2047):
+        pos = torch.tensor([p], device=DEV)
+        outs.append(ops.attention(q, k, v, pos, H, G, hs, 0.1, n_splits=16, workspace=ws).clone())
+    assert torch.equal(outs[0], outs[2]) and torch.equal(outs[0], outs[4])
+    assert int(ws.counters.abs().sum()) == 0
+    ref0 = v[:, 0].reshape(-1)  # position 0: softmax over one key -> exactly v[0]
+    assert torch.equal(outs[3].view(-1), ref0)
+
+
 def test_argmax_known_answers_and_ties(ops, golden):
     g = golden("g3_ops.npz")
     logits = torch.from_numpy(g["sample_logits"]).float()
