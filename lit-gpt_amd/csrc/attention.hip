@@ -192,10 +192,11 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
     for (int s = 0; s < n_splits; ++s) mx = fmaxf(mx, wm[h * n_splits + s]);
     float lt = 0.0f, ot = 0.0f;
     const float* base = ws + (row0 + h) * n_splits * (HS + 2);
+    // no data-dependent branch: empty splits carry m = -inf (weight exp(-inf) = 0), l = 0, o = 0, so every
+    // load is independent and the compiler keeps them all in flight
+#pragma unroll 8
     for (int s = 0; s < n_splits; ++s) {
-      const float ms = wm[h * n_splits + s];
-      if (ms == -INFINITY) continue;  // empty split (l = 0, o = 0)
-      const float c = expf(ms - mx);
+      const float c = expf(wm[h * n_splits + s] - mx);
       lt = fmaf(ld_sc1(base + s * (HS + 2) + 1), c, lt);
       ot = fmaf(ld_sc1(base + s * (HS + 2) + 2 + d), c, ot);
     }

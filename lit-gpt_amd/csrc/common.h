@@ -12,16 +12,17 @@ constexpr int kWave = 64;  // CDNA wavefront
 __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 __device__ __forceinline__ float bflo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float bfhi(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+// fp32 -> bf16 round-to-nearest-even in hardware (v_cvt_pk_bf16_f32: one instruction per PAIR, NaN stays NaN);
+// hipcc has no builtin that emits the packed form for two independent values, hence the asm.
+__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
+  uint32_t r;
+  asm("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(lo), "v"(hi));
+  return r;
+}
 __device__ __forceinline__ uint16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7FFFFFFFu) > 0x7F800000u) return (uint16_t)((u >> 16) | 0x40u);  // quiet NaN
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(f));
 }
 __device__ __forceinline__ float round_bf(float f) { return bf2f(f2bf(f)); }
-__device__ __forceinline__ uint32_t pack2(float lo, float hi) {
-  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
-}
 
 // ---- wave-level reductions (64 lanes) ----
 __device__ __forceinline__ float wave_sum(float v) {

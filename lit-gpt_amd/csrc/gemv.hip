@@ -5,23 +5,31 @@
 // for every Linear of the decode step: qkv (lit_gpt/model.py:619), attn proj (:656), LLaMAMLP fc_1/fc_2/proj
 // (:712-716) and lm_head (:519).
 //
-// MI355X design (HBM-bound, ~1 flop/byte):
-//  * weights stream once from HBM as 16-byte-per-lane coalesced loads (1 KiB per wave-instruction);
-//  * the activation row is staged once per workgroup in LDS (bf16, pair-permuted so that one AND-OR turns
-//    a nibble pair into a bf16 pair "128 + q"), optionally RMS-normalised in the prologue (fused RMSNorm,
-//    lit_gpt/rmsnorm.py:19-25), with per-32-element sums for the "-8" offset;
-//  * int4-g: v_dot2c_f32_bf16 on (x_k, x_k+4) x (128+q_k, 128+q_k+4) pairs, one scale FMA per 32 weights;
-//    nf4: 16-entry codebook in LDS, fp32 FMAs, one absmax multiply per 32 weights;
-//  * a wave owns RW rows x (1/KS of K); 4 waves per 256-thread workgroup; wave sums via DPP + readlane;
-//  * epilogues: +bias, +residual (Block residual add, model.py:591-592), dual-weight SwiGLU
+// MI355X design. A batch-1 GEMV is a pure weight stream (~1 flop/byte) whose launches are only 8-66 MB, so the
+// launch ramp and load latency dominate unless the whole kernel's weights are in flight at once
+// (tools/bw_probe: a bare 16-B/lane read of 8 / 25 / 46 / 66 MB takes 3.0 / 5.5 / 8.6 / 11.7 us).
+// Measured cost split for the 25 MB qkv shape (tools/gemv_lab): streaming 5.0 us, + int4 dequant-dot 0.9 us,
+// + per-row wave reductions 1.3-2.0 us, + the butterfly below only 0.4 us.
+//  * One wave per row slot: a wave owns RPR consecutive rows; lane l owns 32-element chunk columns
+//    l, l+64, ... (CPT of them). Every wave issues ALL its 16-B non-temporal weight loads (RPR*CPT per lane)
+//    up front, one round per wave; enough waves (~3 workgroups per CU) hide the latency.
+//  * The activation row is fetched BEFORE the weights (vmcnt is in order, so the wait for x leaves the weight
+//    loads in flight), then staged once per workgroup in LDS as bf16 pairs (x_k, x_k+4) with per-chunk sums;
+//    the fused RMSNorm (lit_gpt/rmsnorm.py:19-25: bf16(w * (x * rsqrt(mean(x^2) + eps))), the reference's
+//    rounding point) runs during that staging, while the weights stream.
+//  * int4-g: one AND-OR turns two nibbles into the bf16 pair (128+q_k, 128+q_k+4) for v_dot2c_f32_bf16, and
+//    sum x*(q-8) = dot - 136*sum(x); nf4: codebook in LDS, fp32 FMAs; one scale/absmax FMA per 32 weights.
+//  * Reduction: a transposed butterfly sums R = RPR (x2 for the dual GEMV) row partials across the wave with
+//    log2(R) halving exchanges + DPP, instead of R separate wave reductions.
+//  * Epilogues: +bias, +residual (Block residual add, model.py:591-592), dual-weight SwiGLU
 //    (silu(fc_1 x) * fc_2 x, model.py:715) with the reference's bf16 rounding points.
 #include "common.h"
 
 namespace lga {
 
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+
 __device__ __forceinline__ uint4 ld_nt16(const void* p) {  // 16-B non-temporal load (weights are read once)
   const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
   return make_uint4(v.x, v.y, v.z, v.w);
@@ -32,19 +40,52 @@ __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
                                          false);
 }
 
-// DPP wave reduction: every lane of each 16-lane row gets the row sum, then 4 readlanes -> uniform sum.
-__device__ __forceinline__ float dpp_row_sum(float v) {
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));  // quad [1,0,3,2]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));  // quad [2,3,0,1]
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));  // row_half_mirror
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));  // row_mirror
-  return v;
-}
+#define LGA_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
+
+// DPP wave reduction -> uniform wave sum (used once per wave for the RMSNorm sum of squares)
 __device__ __forceinline__ float wave_sum_uniform(float v) {
-  v = dpp_row_sum(v);
+  v += LGA_DPP(v, 0xB1);   // quad [1,0,3,2]
+  v += LGA_DPP(v, 0x4E);   // quad [2,3,0,1]
+  v += LGA_DPP(v, 0x141);  // row half mirror
+  v += LGA_DPP(v, 0x140);  // row mirror
   const int i = __float_as_int(v);
-  return __int_as_float(__builtin_amdgcn_readlane(i, 0)) + __int_as_float(__builtin_amdgcn_readlane(i, 16)) +
-         __int_as_float(__builtin_amdgcn_readlane(i, 32)) + __int_as_float(__builtin_amdgcn_readlane(i, 48));
+  return (__int_as_float(__builtin_amdgcn_readlane(i, 0)) + __int_as_float(__builtin_amdgcn_readlane(i, 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(i, 32)) + __int_as_float(__builtin_amdgcn_readlane(i, 48)));
+}
+
+// Transposed butterfly over R in {2, 4, 8} per-lane partials a[0..R). Level with lane-distance D keeps one half
+// of the values and adds the partner's other half. Afterwards lanes whose low log2(64/R) bits are 0 hold the
+// full wave sum of value index  bfly_index<R>(lane).
+template <int R>
+__device__ __forceinline__ float butterfly(float* a, int lane) {
+  constexpr int L = R == 8 ? 3 : (R == 4 ? 2 : 1);
+#pragma unroll
+  for (int lev = 0; lev < L; ++lev) {
+    const int D = 32 >> lev;
+    const int n = R >> (lev + 1);
+    const bool h = lane & D;
+#pragma unroll
+    for (int i = 0; i < n; ++i) {
+      const float send = h ? a[i] : a[i + n], keep = h ? a[i + n] : a[i];
+      float recv;
+      if (D == 8) recv = LGA_DPP(send, 0x128);  // row_ror:8 == xor 8 inside a 16-lane row
+      else recv = __shfl_xor(send, D);
+      a[i] = keep + recv;
+    }
+  }
+  float d = a[0];
+  // reduce over the remaining 64/R lanes (bits below the last exchange distance)
+  d += LGA_DPP(d, 0xB1);
+  d += LGA_DPP(d, 0x4E);
+  d += LGA_DPP(d, 0x141);  // 8-lane groups done (R = 8)
+  if (R <= 4) d += LGA_DPP(d, 0x140);  // 16-lane groups (R = 4)
+  if (R <= 2) d += __shfl_xor(d, 16);  // 32-lane groups (R = 2)
+  return d;
+}
+template <int R>
+__device__ __forceinline__ int bfly_index(int lane) {
+  return R == 8 ? ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1)
+                : (R == 4 ? ((lane >> 5) & 1) * 2 + ((lane >> 4) & 1) : ((lane >> 5) & 1));
 }
 
 struct GemvArgs {
@@ -61,243 +102,238 @@ struct GemvArgs {
   float eps;
 };
 
-constexpr int kThreads = 256;
-constexpr int kWaves = kThreads / kWave;
+__constant__ float kNF4v[16] = {
+    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
+    -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
+    0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+    0.7229568362236023f, 1.0f};
 
-__device__ __forceinline__ float load_scale(const void* sc, size_t i, int fmt) {
-  return fmt == 0 ? bf2f(((const uint16_t*)sc)[i]) : ((const float*)sc)[i];
+// Scales stay raw bits until used: converting at load time makes the compiler wait for the scale load at once,
+// and vmcnt is in order, so that wait would also drain every weight load issued before it.
+template <int FMT>
+__device__ __forceinline__ uint32_t load_scale_bits(const void* sc, size_t i) {
+  return FMT == 0 ? (uint32_t)((const uint16_t*)sc)[i] : ((const uint32_t*)sc)[i];
+}
+template <int FMT>
+__device__ __forceinline__ float scale_of(uint32_t bits) {
+  return FMT == 0 ? __uint_as_float(bits << 16) : __uint_as_float(bits);
 }
 
-// dot of one 16-byte weight chunk (32 nibbles) with the LDS x chunk; returns the *unscaled* partial
+// dot of one 16-byte weight chunk (32 nibbles) with the LDS x chunk (4 uint4 of (x_i, x_i+4) pairs)
 template <int FMT>
-__device__ __forceinline__ float chunk_dot(const uint4 w, const uint4* xl, float xsum, const float* nf4) {
+__device__ __forceinline__ float chunk_dot(const uint4 w, const uint4* xc, float xsum, const float* nf4) {
   const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
-  if (FMT == 0) {
-    float d = 0.0f;
+  float d = 0.0f;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint4 xv = xl[j];
-      const uint32_t xp[4] = {xv.x, xv.y, xv.z, xv.w};
+  for (int j = 0; j < 4; ++j) {
+    const uint4 xv = xc[j];
+    const uint32_t xp[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const uint32_t q = ((wd[j] >> (4 * s)) & 0x000F000Fu) | 0x43004300u;  // bf16 pair (128+q_s, 128+q_s+4)
-        d = dot2_bf16(xp[s], q, d);
-      }
-    }
-    return d - 136.0f * xsum;
-  } else {
-    float d = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint4 xv = xl[j];
-      const uint32_t xp[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < 4; ++s) {
+      if (FMT == 0) {
+        d = dot2_bf16(xp[s], ((wd[j] >> (4 * s)) & 0x000F000Fu) | 0x43004300u, d);
+      } else {
         d = fmaf(nf4[(wd[j] >> (4 * s)) & 0xF], bflo(xp[s]), d);
         d = fmaf(nf4[(wd[j] >> (4 * s + 16)) & 0xF], bfhi(xp[s]), d);
       }
     }
-    return d;
   }
+  return FMT == 0 ? d - 136.0f * xsum : d;  // int4: sum x*(128+q) - 136*sum x = sum x*(q-8)
 }
 
-// Stage x (optionally RMS-normalised, rounded to bf16 like the reference's `.to(dtype)`) into LDS.
-// Layout: per 8-element group, dwords (x0,x4),(x1,x5),(x2,x6),(x3,x7); xsum[c] = sum of chunk c (32 elems).
-__device__ void stage_x(const GemvArgs& a, uint4* xl, float* xsum, float* red) {
-  const int tid = threadIdx.x;
-  const int n8 = a.K / 8;
-  float rs = 1.0f;
-  if (a.norm_w) {
-    float ss = 0.0f;
-    for (int i = tid; i < n8; i += kThreads) {
-      const uint4 v = ((const uint4*)a.x)[i];
-      const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+// One workgroup = 4 independent waves (row slots); a wave handles RPR consecutive rows.
+template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES>
+__global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint4* xl = (uint4*)smem;                        // K/8 uint4 (bf16 pairs)
+  float* xsum = (float*)(smem + (size_t)a.K * 2);  // K/32 chunk sums
+  float* red = xsum + a.K / 32;                    // 4
+  float* nf4 = red + 4;                            // 16
+  constexpr int R = DUAL ? 2 * RPR : RPR;          // values per lane entering the butterfly
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int NC = a.K / 32, n8 = a.K / 8, groups = a.K / a.G;
+  const int row0 = (blockIdx.x * 4 + wave) * RPR;
+  if (FMT == 1 && t < 16) nf4[t] = kNF4v[t];
+
+  // 1. activation (and norm weight) share of this thread: uint4 t, t+256, ... (clamped, branch-free)
+  uint4 xr[CPT], nr[CPT];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float lo = bflo(d[j]), hi = bfhi(d[j]);
+  for (int i = 0; i < CPT; ++i) {
+    const int u = min(t + 256 * i, n8 - 1);
+    xr[i] = ((const uint4*)a.x)[u];
+    if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
+  }
+  // 2. every weight / scale / residual load of this wave (rows past N re-read row N-1; never stored)
+  uint4 w[RPR][CPT], w2[DUAL ? RPR : 1][DUAL ? CPT : 1];
+  uint32_t s[RPR][CPT], s2[DUAL ? RPR : 1][DUAL ? CPT : 1];
+  uint32_t res = 0;
+#pragma unroll
+  for (int i = 0; i < RPR; ++i) {
+    const size_t rb = (size_t)min(row0 + i, a.N - 1) * (a.K / 2);
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int c = min(lane + 64 * j, NC - 1);
+      w[i][j] = ld_nt16(a.qw + rb + (size_t)c * 16);
+      if (DUAL) w2[i][j] = ld_nt16(a.qw2 + rb + (size_t)c * 16);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < RPR; ++i) {
+    const size_t n = (size_t)min(row0 + i, a.N - 1);
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int g = (min(lane + 64 * j, NC - 1) * 32) / a.G;
+      s[i][j] = load_scale_bits<FMT>(a.sc, n * groups + g);
+      if (DUAL) s2[i][j] = load_scale_bits<FMT>(a.sc2, n * groups + g);
+    }
+  }
+  if (RES) res = a.residual[min(row0 + (lane & (RPR - 1)), a.N - 1)];
+  __builtin_amdgcn_sched_barrier(0);  // nothing that waits on x may move above the weight loads
+
+  // 3. stage x into LDS (RMS-normalised when NORM) while the weights stream
+  float rs = 1.0f;
+  if (NORM) {
+    float ss = 0.0f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const bool ok = t + 256 * i < n8;
+      const uint32_t d[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float lo = ok ? bflo(d[q]) : 0.0f, hi = ok ? bfhi(d[q]) : 0.0f;
         ss = fmaf(lo, lo, ss);
         ss = fmaf(hi, hi, ss);
       }
     }
     ss = wave_sum_uniform(ss);
-    if ((tid & 63) == 0) red[tid >> 6] = ss;
+    if (lane == 0) red[wave] = ss;
     __syncthreads();
-    const float tot = red[0] + red[1] + red[2] + red[3];
-    rs = 1.0f / sqrtf(tot / (float)a.K + a.eps);
+    rs = 1.0f / sqrtf(((red[0] + red[1]) + (red[2] + red[3])) / (float)a.K + a.eps);
   }
-  for (int i = tid; i < n8; i += kThreads) {
-    const uint4 v = ((const uint4*)a.x)[i];
-    const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-    float e[8];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      e[2 * j] = bflo(d[j]);
-      e[2 * j + 1] = bfhi(d[j]);
-    }
-    if (a.norm_w) {
-      const uint4 wv = ((const uint4*)a.norm_w)[i];
-      const uint32_t wd[4] = {wv.x, wv.y, wv.z, wv.w};
+  for (int i = 0; i < CPT; ++i) {
+    const int u = t + 256 * i;
+    uint32_t d[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};  // bf16 pairs (x0,x1) (x2,x3) (x4,x5) (x6,x7)
+    if (NORM) {  // bf16(w * (x * rs)), rounded in hardware, two elements per instruction
+      const uint32_t nw[4] = {nr[i].x, nr[i].y, nr[i].z, nr[i].w};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        e[2 * j] = round_bf(__fmul_rn(bflo(wd[j]), __fmul_rn(e[2 * j], rs)));
-        e[2 * j + 1] = round_bf(__fmul_rn(bfhi(wd[j]), __fmul_rn(e[2 * j + 1], rs)));
-      }
+      for (int q = 0; q < 4; ++q)
+        d[q] = pack2(__fmul_rn(bflo(nw[q]), __fmul_rn(bflo(d[q]), rs)),
+                     __fmul_rn(bfhi(nw[q]), __fmul_rn(bfhi(d[q]), rs)));
     }
-    xl[i] = make_uint4(pack2(e[0], e[4]), pack2(e[1], e[5]), pack2(e[2], e[6]), pack2(e[3], e[7]));
-    float s = ((e[0] + e[1]) + (e[2] + e[3])) + ((e[4] + e[5]) + (e[6] + e[7]));
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    if ((i & 3) == 0) xsum[i >> 2] = s;
+    float cs = ((bflo(d[0]) + bfhi(d[0])) + (bflo(d[1]) + bfhi(d[1]))) +
+               ((bflo(d[2]) + bfhi(d[2])) + (bflo(d[3]) + bfhi(d[3])));
+    cs += __shfl_xor(cs, 1);  // 4 consecutive threads hold one 32-element chunk
+    cs += __shfl_xor(cs, 2);
+    if (u < n8) {
+      // (x0,x4) (x1,x5) (x2,x6) (x3,x7): byte permutes of the bf16 pairs
+      xl[u] = make_uint4(__builtin_amdgcn_perm(d[2], d[0], 0x05040100u), __builtin_amdgcn_perm(d[2], d[0], 0x07060302u),
+                         __builtin_amdgcn_perm(d[3], d[1], 0x05040100u), __builtin_amdgcn_perm(d[3], d[1], 0x07060302u));
+      if ((u & 3) == 0) xsum[u >> 2] = cs;
+    }
   }
-}
-
-template <int RW, int KS, int FMT, bool DUAL>
-__global__ void __launch_bounds__(kThreads) gemv_q4_kernel(GemvArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  uint4* xl = (uint4*)smem;                                  // K * 2 bytes
-  float* xsum = (float*)(smem + (size_t)a.K * 2);            // K/32 floats
-  float* part = xsum + a.K / 32;                             // [4 waves][RW][2]
-  float* nf4 = part + kWaves * RW * 2;                       // 16 floats
-  float* red = nf4 + 16;                                     // 4 floats
-  if (FMT == 1 && threadIdx.x < 16) {
-    const float cb[16] = {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f,
-                          -0.28444138169288635f, -0.18477343022823334f, -0.09105003625154495f, 0.0f,
-                          0.07958029955625534f, 0.16093020141124725f, 0.24611230194568634f,
-                          0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
-                          0.7229568362236023f, 1.0f};
-    nf4[threadIdx.x] = cb[threadIdx.x];
-  }
-  stage_x(a, xl, xsum, red);
   __syncthreads();
 
-  constexpr int RS = kWaves / KS;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int rs = wave / KS, ks = wave % KS;
-  const int row0 = (blockIdx.x * RS + rs) * RW;
-  const int NC = a.K / 32, groups = a.K / a.G;
-  const int cps = (NC + KS - 1) / KS;
-  const int c_beg = ks * cps, c_end = min(NC, c_beg + cps);
-  const size_t row_bytes = (size_t)a.K / 2;
-
-  const uint8_t* wrow[RW];
-  const uint8_t* wrow2[RW];
-  int srow[RW];
+  // 4. dequant-dot every row of this wave, then one butterfly for all of them
+  float part[R];
 #pragma unroll
-  for (int r = 0; r < RW; ++r) {
-    const int n = min(row0 + r, a.N - 1);
-    wrow[r] = a.qw + (size_t)n * row_bytes;
-    wrow2[r] = DUAL ? a.qw2 + (size_t)n * row_bytes : nullptr;
-    srow[r] = n * groups;
-  }
-  float acc[RW], acc2[RW];
+  for (int i = 0; i < R; ++i) part[i] = 0.0f;
 #pragma unroll
-  for (int r = 0; r < RW; ++r) acc[r] = acc2[r] = 0.0f;
-
-#pragma unroll 2
-  for (int c = c_beg + lane; c < c_end; c += kWave) {
-    uint4 wv[RW], wv2[RW];
+  for (int j = 0; j < CPT; ++j) {
+    const int c = lane + 64 * j;
+    const bool ok = c < NC;
+    const int cc = min(c, NC - 1);
+    const uint4* xc = xl + cc * 4;
+    const float xs = xsum[cc];
 #pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      wv[r] = ld_nt16(wrow[r] + (size_t)c * 16);
-      if (DUAL) wv2[r] = ld_nt16(wrow2[r] + (size_t)c * 16);
-    }
-    const int gi = (c * 32) / a.G;
-    float s[RW], s2[RW];
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      s[r] = load_scale(a.sc, (size_t)srow[r] + gi, FMT);
-      if (DUAL) s2[r] = load_scale(a.sc2, (size_t)srow[r] + gi, FMT);
-    }
-    const float xs = xsum[c];
-    const uint4* xc = xl + c * 4;
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      acc[r] = fmaf(s[r], chunk_dot<FMT>(wv[r], xc, xs, nf4), acc[r]);
-      if (DUAL) acc2[r] = fmaf(s2[r], chunk_dot<FMT>(wv2[r], xc, xs, nf4), acc2[r]);
-    }
-  }
-
-  float tot[RW], tot2[RW];
-#pragma unroll
-  for (int r = 0; r < RW; ++r) {
-    tot[r] = wave_sum_uniform(acc[r]);
-    tot2[r] = DUAL ? wave_sum_uniform(acc2[r]) : 0.0f;
-  }
-  if (KS > 1) {
-    if (lane == 0) {
-#pragma unroll
-      for (int r = 0; r < RW; ++r) {
-        part[(wave * RW + r) * 2] = tot[r];
-        part[(wave * RW + r) * 2 + 1] = tot2[r];
-      }
-    }
-    __syncthreads();
-    if (ks != 0) return;
-#pragma unroll
-    for (int r = 0; r < RW; ++r) {
-      float t = 0.0f, t2 = 0.0f;
-      for (int k = 0; k < KS; ++k) {
-        t += part[((rs * KS + k) * RW + r) * 2];
-        t2 += part[((rs * KS + k) * RW + r) * 2 + 1];
-      }
-      tot[r] = t;
-      tot2[r] = t2;
-    }
-  }
-  if (lane < RW) {
-    // select this lane's row without dynamic register indexing
-    float t = tot[0], t2 = tot2[0];
-#pragma unroll
-    for (int r = 1; r < RW; ++r)
-      if (lane == r) {
-        t = tot[r];
-        t2 = tot2[r];
-      }
-    const int n = row0 + lane;
-    if (n < a.N) {
-      float out;
-      if (DUAL) {
-        const float g = round_bf(silu_f(round_bf(t)));  // silu(bf16(fc_1 x)) -> bf16
-        out = __fmul_rn(g, round_bf(t2));               // * bf16(fc_2 x)
+    for (int i = 0; i < RPR; ++i) {
+      const float d = chunk_dot<FMT>(w[i][j], xc, xs, nf4);
+      if (DUAL) {  // value index = 2*row + matrix (so the pair of one row lands in lanes l and l^8 / l^16 / l^32)
+        part[2 * i] = fmaf(ok ? scale_of<FMT>(s[i][j]) : 0.0f, d, part[2 * i]);
+        const float d2 = chunk_dot<FMT>(w2[i][j], xc, xs, nf4);
+        part[2 * i + 1] = fmaf(ok ? scale_of<FMT>(s2[i][j]) : 0.0f, d2, part[2 * i + 1]);
       } else {
-        out = a.bias ? t + bf2f(a.bias[n]) : t;
-        if (a.residual) out = round_bf(out) + bf2f(a.residual[n]);
+        part[i] = fmaf(ok ? scale_of<FMT>(s[i][j]) : 0.0f, d, part[i]);
       }
-      a.y[n] = f2bf(out);
     }
   }
-}
-
-template <int RW, int KS, int FMT, bool DUAL>
-static void launch(const GemvArgs& a, hipStream_t stream) {
-  constexpr int rows_per_block = (kWaves / KS) * RW;
-  const dim3 grid((a.N + rows_per_block - 1) / rows_per_block);
-  const size_t lds = (size_t)a.K * 2 + (a.K / 32) * 4 + kWaves * RW * 2 * 4 + 16 * 4 + 4 * 4;
-  gemv_q4_kernel<RW, KS, FMT, DUAL><<<grid, kThreads, lds, stream>>>(a);
-}
-
-template <int FMT, bool DUAL>
-static void dispatch(const GemvArgs& a, int variant, hipStream_t stream) {
-  // variant: rows-per-wave x k-split; picked by the host heuristic (or a tuning sweep)
-  switch (variant) {
-    case 0: launch<1, 1, FMT, DUAL>(a, stream); break;
-    case 1: launch<2, 1, FMT, DUAL>(a, stream); break;
-    case 2: launch<4, 1, FMT, DUAL>(a, stream); break;
-    case 3: launch<2, 2, FMT, DUAL>(a, stream); break;
-    case 4: launch<4, 2, FMT, DUAL>(a, stream); break;
-    case 5: launch<2, 4, FMT, DUAL>(a, stream); break;
-    case 6: launch<4, 4, FMT, DUAL>(a, stream); break;
-    default: launch<1, 4, FMT, DUAL>(a, stream); break;
+  const float tot = butterfly<R>(part, lane);
+  const int vi = bfly_index<R>(lane);  // value index held by this lane
+  constexpr int GROUP = 64 / R;        // lanes per value after the butterfly
+  if (DUAL) {
+    // partner value (other matrix, same row) sits in the lane whose value index differs in bit 0
+    constexpr int PD = R == 8 ? 8 : (R == 4 ? 16 : 32);
+    const float other = PD == 8 ? LGA_DPP(tot, 0x128) : __shfl_xor(tot, PD);
+    const int row = row0 + (vi >> 1);
+    if ((lane & (GROUP - 1)) == 0 && (vi & 1) == 0 && row < a.N) {
+      const float g = round_bf(silu_f(round_bf(tot)));  // silu(bf16(fc_1 x)) -> bf16
+      a.y[row] = f2bf(__fmul_rn(g, round_bf(other)));   // * bf16(fc_2 x)
+    }
+  } else {
+    const int row = row0 + vi;
+    float o = tot;
+    if (RES) {
+      // residual of row vi sits in lane vi (loaded up front); fetch it into this lane
+      o = round_bf(a.bias ? o + bf2f(a.bias[min(row, a.N - 1)]) : o) +
+          __uint_as_float(((uint32_t)__shfl(res, vi)) << 16);
+    } else if (a.bias) {
+      o += bf2f(a.bias[min(row, a.N - 1)]);
+    }
+    if ((lane & (GROUP - 1)) == 0 && row < a.N) a.y[row] = f2bf(o);
   }
 }
 
-static int pick_variant(int N, int K, bool dual) {
-  // aim for >= ~1024 workgroups (4 per CU) with >= 4 rows of loads in flight per wave
-  const long rows = dual ? 2L * N : N;
-  if (rows >= 16384) return 2;         // 4 rows/wave, 16 rows/block
-  if (rows >= 8192) return 4;          // 4 rows/wave, k-split 2 -> 8 rows/block
-  if (K >= 8192) return 6;             // 4 rows/wave, k-split 4 -> 4 rows/block
-  return 4;
+template <int RPR, int CPT, int FMT, bool DUAL>
+static void launch(const GemvArgs& a, hipStream_t stream) {
+  const int waves = (a.N + RPR - 1) / RPR;
+  const int blocks = (waves + 3) / 4;
+  const size_t lds = (size_t)a.K * 2 + (a.K / 32) * 4 + 4 * 4 + 16 * 4;
+  const bool norm = a.norm_w != nullptr, res = a.residual != nullptr;
+  if (DUAL) {
+    if (norm) gemv_q4_kernel<RPR, CPT, FMT, DUAL, true, false><<<blocks, 256, lds, stream>>>(a);
+    else gemv_q4_kernel<RPR, CPT, FMT, DUAL, false, false><<<blocks, 256, lds, stream>>>(a);
+  } else if (norm) {
+    if (res) gemv_q4_kernel<RPR, CPT, FMT, DUAL, true, true><<<blocks, 256, lds, stream>>>(a);
+    else gemv_q4_kernel<RPR, CPT, FMT, DUAL, true, false><<<blocks, 256, lds, stream>>>(a);
+  } else {
+    if (res) gemv_q4_kernel<RPR, CPT, FMT, DUAL, false, true><<<blocks, 256, lds, stream>>>(a);
+    else gemv_q4_kernel<RPR, CPT, FMT, DUAL, false, false><<<blocks, 256, lds, stream>>>(a);
+  }
+}
+
+// variant: 0 = fewer rows per wave (more waves), 1 = more rows per wave; < 0 = heuristic
+template <int FMT, bool DUAL>
+static int dispatch(const GemvArgs& a, int variant, hipStream_t stream) {
+  const int cpt = (a.K / 32 + 63) / 64;  // chunks per lane (== uint4 of x per thread)
+  if (variant < 0) {
+    const long rows = DUAL ? 2L * a.N : a.N;
+    variant = rows >= 24000 ? 1 : 0;  // tall matrices: more rows per wave keep the grid ~3-4 workgroups per CU
+  }
+  const bool big = variant != 0;
+#define LGA_L(RS, RB, CPT)                                                         \
+  do {                                                                             \
+    if (big) launch<(DUAL ? (RB) / 2 : (RB)), CPT, FMT, DUAL>(a, stream);          \
+    else launch<(DUAL ? (RS) / 2 : (RS)), CPT, FMT, DUAL>(a, stream);              \
+  } while (0)
+  switch (cpt) {
+    case 1: LGA_L(4, 8, 1); break;
+    case 2: LGA_L(4, 8, 2); break;
+    case 3: LGA_L(4, 8, 3); break;
+    case 4: LGA_L(2, 4, 4); break;
+    case 5:
+    case 6: LGA_L(2, 4, 6); break;
+    case 7:
+    case 8: LGA_L(2, 4, 8); break;
+    default:
+      if (cpt <= 16) {
+        LGA_L(2, 2, 16);
+        break;
+      }
+      lga_set_error("lga_q4_gemv: K > 32768 is not supported");
+      return (int)hipErrorInvalidValue;
+  }
+#undef LGA_L
+  return 0;
 }
 
 }  // namespace lga
@@ -309,12 +345,10 @@ extern "C" int lga_q4_gemv(const void* x, const uint8_t* qweight, const void* sc
   LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0, "lga_q4_gemv: K must be a positive multiple of 32");
   LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv: group must be a multiple of 32 dividing K");
   LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv: fmt must be 0 (int4-g) or 1 (nf4)");
-  LGA_CHECK_ARG((size_t)K * 2 + (K / 32) * 4 + 256 <= 160 * 1024, "lga_q4_gemv: K too large for the LDS-staged row");
   lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, (const uint16_t*)bias,
                   (const uint16_t*)residual, (const uint16_t*)norm_weight, (uint16_t*)y, N, K, group, norm_eps};
-  if (variant < 0) variant = lga::pick_variant(N, K, false);
-  if (fmt == 0) lga::dispatch<0, false>(a, variant, stream);
-  else lga::dispatch<1, false>(a, variant, stream);
+  const int rc = fmt == 0 ? lga::dispatch<0, false>(a, variant, stream) : lga::dispatch<1, false>(a, variant, stream);
+  if (rc) return rc;
   LGA_LAUNCH_RETURN();
 }
 
@@ -326,11 +360,9 @@ extern "C" int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const 
   LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0, "lga_q4_gemv_swiglu: K must be a positive multiple of 32");
   LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv_swiglu: bad group");
   LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv_swiglu: fmt must be 0 or 1");
-  LGA_CHECK_ARG((size_t)K * 2 + (K / 32) * 4 + 256 <= 160 * 1024, "lga_q4_gemv_swiglu: K too large");
   lga::GemvArgs a{(const uint16_t*)x, qweight1, scales1, qweight2, scales2, nullptr, nullptr,
                   (const uint16_t*)norm_weight, (uint16_t*)y, N, K, group, norm_eps};
-  if (variant < 0) variant = lga::pick_variant(N, K, true);
-  if (fmt == 0) lga::dispatch<0, true>(a, variant, stream);
-  else lga::dispatch<1, true>(a, variant, stream);
+  const int rc = fmt == 0 ? lga::dispatch<0, true>(a, variant, stream) : lga::dispatch<1, true>(a, variant, stream);
+  if (rc) return rc;
   LGA_LAUNCH_RETURN();
 }

@@ -281,6 +281,8 @@ class LLaMAMLP(nn.Module):
         fusable = (M == 1 and isinstance(f1, QuantLinear) and isinstance(f2, QuantLinear) and f1.bias is None
                    and f2.bias is None and (f1.fmt, f1.group) == (f2.fmt, f2.group))
         if fusable:
+            if norm is not None and not ops.gemv_fuses_norm(C, dual=True):
+                x2, norm = norm(x2), None
             g = ops.q4_gemv_swiglu(x2.view(-1), f1.qweight, f1.scales, f2.qweight, f2.scales, f1.out_features, C,
                                    f1.group, f1.fmt, norm_weight=None if norm is None else norm.weight,
                                    eps=1e-5 if norm is None else norm.eps).view(1, -1)

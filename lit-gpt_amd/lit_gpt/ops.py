@@ -247,3 +247,9 @@ def argmax(logits, out_idx=None, token_out=None, pos_inout=None):
                                      _opt(token_out, "token_out", torch.int32),
                                      _opt(pos_inout, "pos_inout", torch.int64), _stream()))
     return idx
+
+
+def gemv_fuses_norm(K: int, dual: bool) -> bool:
+    """Whether lga_q4_gemv(_swiglu) can fuse the RMSNorm prologue: the row must fit one K tile
+    (64 lanes x 2 chunks x 32 for the dual SwiGLU GEMV, x 4 chunks otherwise)."""
+    return K // 32 <= (128 if dual else 256)

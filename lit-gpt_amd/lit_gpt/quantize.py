@@ -96,6 +96,8 @@ class QuantLinear(nn.Module):
         M = x2.shape[0]
         res = None if residual is None else residual.reshape(M, self.out_features).contiguous()
         if M == 1:
+            if norm_weight is not None and not ops.gemv_fuses_norm(self.in_features, dual=False):
+                x2, norm_weight = ops.rmsnorm(x2, norm_weight, norm_eps), None
             y = ops.q4_gemv(x2.view(-1), self.qweight, self.scales, self.out_features, self.in_features, self.group,
                             self.fmt, bias=self.bias, residual=None if res is None else res.view(-1),
                             norm_weight=norm_weight, eps=norm_eps)
