@@ -79,12 +79,23 @@ int lga_swiglu(const void* a, const void* b, void* y, long n, lga_stream_t strea
  * q (T, H, hs); caches (G, max_seq, hs); query t attends keys 0..input_pos[t]; y (T, H*hs).
  * n_splits > 1 splits keys 0..input_pos[t] evenly (flash-decoding; the split merge happens in the same launch
  * by the last-arriving workgroup) and needs `workspace` of lga_attention_workspace_bytes(T, H, hs, n_splits) bytes
- * plus `counters` (T * G uint32, zeroed once at allocation; the kernel re-arms them).
- * head_size in {64, 128}; H/G in {1,2,4,8}; n_splits * H/G <= 4 * head_size. */
+ * plus `counters` (T * G * 64 uint32 — one per (t, group) at a 256-B stride so the device-scope atomics do not
+ * share a line; zeroed once at allocation, re-armed by the kernel).
+ * head_size in {64, 128}; H/G in {1,2,4,8}; 1 <= n_splits <= 256. */
 int lga_attention(const void* q, const void* k_cache, const void* v_cache, const int64_t* input_pos, void* y,
                   float* workspace, unsigned* counters, int T, int n_head, int n_query_groups, int head_size,
                   int max_seq, int n_splits, float scale, lga_stream_t stream);
 size_t lga_attention_workspace_bytes(int T, int n_head, int head_size, int n_splits);
+/* Decode step (T = 1) with RoPE + KV-append fused into the attention launch (apply_rope lit_gpt/model.py:641-644,
+ * KVCache.forward :788-795, SDPA :651): qkv is the fused projection row ([G][q_per_kv + 2][hs], the layout of
+ * CausalSelfAttention.attn); q and k are roped with row rope_pos[0] of cos/sin (rope_rows x 128 fp32); k, v are
+ * stored at cache_pos[0]; y (H*hs) = attention of the roped q over keys 0..cache_pos[0]. Caches bit-identical to
+ * lga_rope_kv_append; y equals lga_attention's up to fp32 summation order (the new key is scored last).
+ * Requires head_size == rope_n_elem == 128. */
+int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, const int64_t* cache_pos,
+                               const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, void* y,
+                               float* workspace, unsigned* counters, int n_head, int n_query_groups, int head_size,
+                               int rope_n_elem, int max_seq, int n_splits, float scale, lga_stream_t stream);
 
 /* -- greedy sampling (generate/base.py:30-47 at temperature 0): lowest index among the maxima; optionally
  *    writes the token (int32) and advances *pos_inout by one (generate/base.py:92) -------------------------- */

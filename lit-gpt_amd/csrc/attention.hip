@@ -38,6 +38,31 @@ __device__ __forceinline__ void unpack8(const uint4 v, float* f) {
   }
 }
 
+#ifdef LGA_ATTN_TRACE  // lab builds only (tools/attn_trace.py): per-block phase timestamps, 100 MHz clock
+__device__ unsigned long long g_attn_trace[8192 * 8];
+#define LGA_TRACE(i)                                                                            \
+  do {                                                                                          \
+    if (threadIdx.x == 0) {                                                                     \
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                              \
+      g_attn_trace[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    }                                                                                           \
+  } while (0)
+#else
+#define LGA_TRACE(i) \
+  do {               \
+  } while (0)
+#endif
+
+// per-(t, group) arrival counters sit 256 B apart: same-line device-scope atomics serialize
+constexpr int kCounterStride = 64;
+
+// K/V rows are streamed once per step (the next step's re-read comes after ~1 GB of other traffic): nt loads
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_kv(const uint16_t* p) {
+  const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
 __device__ __forceinline__ void st_sc1(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -45,30 +70,78 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int HS, int QPK, int UNR>
-__global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ q, const uint16_t* __restrict__ kc,
-                                                   const uint16_t* __restrict__ vc,
-                                                   const int64_t* __restrict__ input_pos, uint16_t* __restrict__ y,
-                                                   float* __restrict__ ws, unsigned* __restrict__ cnt, int n_head,
-                                                   int max_seq, float scale) {
+// RoPE of the 8 dims a lane holds (full rotary, n_elem == HS == 128): rotate-half partner dims live 8 lanes away
+// inside the 16-lane row group (DPP row_ror:8). Same math and rounding as lga_rope_kv_append / the reference
+// (x*cos + rotated*sin in fp32, no FMA contraction, one bf16 cast).
+__device__ __forceinline__ uint4 rope8(const uint4 raw, const float* cr, const float* sr, int sub) {
+  const uint32_t d[4] = {raw.x, raw.y, raw.z, raw.w};
+  uint32_t pd[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) pd[i] = __builtin_amdgcn_update_dpp(0, d[i], 0x128, 0xF, 0xF, false);
+  const bool lo_half = sub < 8;
+  uint32_t out[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float r0 = bflo(pd[i]), r1 = bfhi(pd[i]);
+    if (lo_half) {
+      r0 = -r0;
+      r1 = -r1;
+    }
+    const float x0 = bflo(d[i]), x1 = bfhi(d[i]);
+    out[i] = pack2(add_rn(mul_rn(x0, cr[2 * i]), mul_rn(r0, sr[2 * i])),
+                   add_rn(mul_rn(x1, cr[2 * i + 1]), mul_rn(r1, sr[2 * i + 1])));
+  }
+  return make_uint4(out[0], out[1], out[2], out[3]);
+}
+
+// FUSED (decode, T = 1): q, k, v come straight from the qkv projection row; every workgroup ropes its group's
+// q heads itself, and the workgroup whose split owns the new position p ropes k, appends k and v to the cache
+// at p (KVCache.forward, lit_gpt/model.py:788-795) and scores that key from registers — replacing the separate
+// lga_rope_kv_append launch of the decode step.
+template <int HS, int QPK, int UNR, int NW, bool FUSED>
+__global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
+                                                   uint16_t* __restrict__ vc, const int64_t* __restrict__ input_pos,
+                                                   uint16_t* __restrict__ y, float* __restrict__ ws,
+                                                   unsigned* __restrict__ cnt, int n_head, int max_seq, float scale,
+                                                   const int64_t* __restrict__ rope_pos, const float* __restrict__ cos,
+                                                   const float* __restrict__ sin, int rope_rows) {
   constexpr int LPR = HS / 8;    // lanes per key row
   constexpr int RGW = 64 / LPR;  // row groups per wave
-  constexpr int RG = 4 * RGW;    // row groups per workgroup
+  constexpr int RG = NW * RGW;   // row groups per workgroup
+  constexpr int NT = NW * 64;
   const int split = blockIdx.x, g = blockIdx.y, t = blockIdx.z;
   const int n_splits = gridDim.x, G = gridDim.y;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int rg = wave * RGW + lane / LPR;
   const int sub = lane % LPR;
+  LGA_TRACE(0);
   const long p = input_pos[t];
   const int L = (int)min(p + 1, (long)max_seq);  // keys 0..p (never past the cache)
   const int chunk = (L + n_splits - 1) / n_splits;
   const int k_lo = split * chunk;
   const int k_hi = min(k_lo + chunk, L);
+  LGA_TRACE(1);
+  const bool owns_new = FUSED && p < max_seq && k_lo <= p && p < k_hi;
+  const int k_end = FUSED ? min(k_hi, (int)p) : k_hi;  // fused: key p is scored from registers below
+  const float* cr = nullptr;
+  const float* sr = nullptr;
+  if (FUSED) {
+    const long rp = min(max(rope_pos[t], 0L), (long)rope_rows - 1);
+    cr = cos + (size_t)rp * HS + sub * 8;
+    sr = sin + (size_t)rp * HS + sub * 8;
+  }
 
   float qf[QPK][8];
 #pragma unroll
-  for (int h = 0; h < QPK; ++h)
-    unpack8(*(const uint4*)(q + ((size_t)t * n_head + (size_t)g * QPK + h) * HS + sub * 8), qf[h]);
+  for (int h = 0; h < QPK; ++h) {
+    if (FUSED) {  // qkv row layout per group: [q_0 .. q_{QPK-1}, k, v] x HS (scripts/convert_hf_checkpoint.py:181-187)
+      const uint4 raw = *(const uint4*)(q + ((size_t)g * (QPK + 2) + h) * HS + sub * 8);
+      unpack8(rope8(raw, cr, sr, sub), qf[h]);
+    } else {
+      unpack8(*(const uint4*)(q + ((size_t)t * n_head + (size_t)g * QPK + h) * HS + sub * 8), qf[h]);
+    }
+  }
+  LGA_TRACE(2);
   float m[QPK], l[QPK], o[QPK][8];
 #pragma unroll
   for (int h = 0; h < QPK; ++h) {
@@ -79,13 +152,13 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
   }
   const uint16_t* kbase = kc + (size_t)g * max_seq * HS + sub * 8;
   const uint16_t* vbase = vc + (size_t)g * max_seq * HS + sub * 8;
-  for (int j0 = k_lo + rg; j0 < k_hi; j0 += RG * UNR) {
+  for (int j0 = k_lo + rg; j0 < k_end; j0 += RG * UNR) {
     uint4 kv[UNR], vv[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
-      const int j = min(j0 + u * RG, k_hi - 1);  // clamped duplicate rows are masked below
-      kv[u] = *(const uint4*)(kbase + (size_t)j * HS);
-      vv[u] = *(const uint4*)(vbase + (size_t)j * HS);
+      const int j = min(j0 + u * RG, k_end - 1);  // clamped duplicate rows are masked below
+      kv[u] = ld_kv(kbase + (size_t)j * HS);
+      vv[u] = ld_kv(vbase + (size_t)j * HS);
     }
 #pragma unroll
     for (int h = 0; h < QPK; ++h) {
@@ -99,7 +172,7 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
 #pragma unroll
         for (int i = 0; i < 8; ++i) d = fmaf(qf[h][i], kf[i], d);
         const float sd = row_group_sum<LPR>(d) * scale;  // whole row group active: DPP stays inside it
-        s[u] = (j0 + u * RG < k_hi) ? sd : -INFINITY;
+        s[u] = (j0 + u * RG < k_end) ? sd : -INFINITY;
         mx = fmaxf(mx, s[u]);
       }
       const float c = expf(m[h] - mx);  // m = -inf (first step) -> 0
@@ -118,6 +191,31 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
       m[h] = mx;
     }
   }
+  LGA_TRACE(3);
+  if (FUSED && owns_new && rg == 0) {  // the new key/value: rope k, append both to the cache, score from registers
+    const uint16_t* kvrow = q + ((size_t)g * (QPK + 2) + QPK) * HS + sub * 8;
+    const uint4 kr = rope8(*(const uint4*)kvrow, cr, sr, sub);
+    const uint4 vr = *(const uint4*)(kvrow + HS);
+    *(uint4*)(kc + ((size_t)g * max_seq + p) * HS + sub * 8) = kr;
+    *(uint4*)(vc + ((size_t)g * max_seq + p) * HS + sub * 8) = vr;
+    float kf[8], vf[8];
+    unpack8(kr, kf);
+    unpack8(vr, vf);
+#pragma unroll
+    for (int h = 0; h < QPK; ++h) {
+      float d = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) d = fmaf(qf[h][i], kf[i], d);
+      const float s = row_group_sum<LPR>(d) * scale;
+      const float mx = fmaxf(m[h], s);
+      const float c = expf(m[h] - mx);
+      const float e = expf(s - mx);
+      l[h] = l[h] * c + e;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[h][i] = fmaf(e, vf[i], o[h][i] * c);
+      m[h] = mx;
+    }
+  }
   // merge the RGW row groups of this wave (lanes differing in the bits above log2(LPR))
 #pragma unroll
   for (int off = LPR; off < 64; off <<= 1) {
@@ -133,8 +231,8 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
       m[h] = mn;
     }
   }
-  __shared__ float sm[4][QPK], sl[4][QPK];
-  __shared__ float so[4][QPK][HS];
+  __shared__ float sm[NW][QPK], sl[NW][QPK];
+  __shared__ float so[NW][QPK][HS];
   __shared__ unsigned s_last;
   if (lane < LPR) {
 #pragma unroll
@@ -149,14 +247,14 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
   }
   __syncthreads();
   const size_t row0 = (size_t)t * n_head + (size_t)g * QPK;  // first head row of this group
-  for (int it = threadIdx.x; it < QPK * HS; it += 256) {
+  for (int it = threadIdx.x; it < QPK * HS; it += NT) {
     const int h = it / HS, d = it % HS;
     float mx = -INFINITY;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) mx = fmaxf(mx, sm[w][h]);
+    for (int w = 0; w < NW; ++w) mx = fmaxf(mx, sm[w][h]);
     float lt = 0.0f, ot = 0.0f;
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
+    for (int w = 0; w < NW; ++w) {
       const float c = mx == -INFINITY ? 0.0f : expf(sm[w][h] - mx);
       lt += sl[w][h] * c;
       ot += so[w][h][d] * c;
@@ -164,60 +262,85 @@ __global__ void __launch_bounds__(256) attn_kernel(const uint16_t* __restrict__ 
     if (n_splits == 1) {
       y[(row0 + h) * HS + d] = f2bf(ot / lt);
     } else {
-      float* wsr = ws + ((row0 + h) * n_splits + split) * (HS + 2);
-      st_sc1(wsr + 2 + d, ot);
+      float* wsr = ws + ((row0 + h) * n_splits + split) * (HS + 4);
+      st_sc1(wsr + 4 + d, ot);
       if (d == 0) {
         st_sc1(wsr, mx);
         st_sc1(wsr + 1, lt);
       }
     }
   }
+  LGA_TRACE(4);
   if (n_splits == 1) return;
   // ---- publish, then the last-arriving split of this (t, group) merges all splits ----
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
-  if (threadIdx.x == 0)
-    s_last = __hip_atomic_fetch_add(cnt + (size_t)t * G + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned* ctr = cnt + ((size_t)t * G + g) * kCounterStride;
+  if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
+  LGA_TRACE(5);
   if (s_last != (unsigned)(n_splits - 1)) return;
-  float* wm = &so[0][0][0];  // reuse LDS: [QPK][n_splits] weights (n_splits <= 4*HS)
-  for (int it = threadIdx.x; it < QPK * n_splits; it += 256) {
+  // combine: split weights exp(m_s - max) staged in LDS, then one column per thread; empty splits carry
+  // m = -inf, l = 0, o = 0 (weight 0), so the split loop has no data-dependent branch and every load stays in flight
+  float* wm = &so[0][0][0];  // reuse LDS: [QPK][n_splits] (host caps n_splits at 256 <= NW * HS)
+  for (int it = threadIdx.x; it < QPK * n_splits; it += NT) {
     const int h = it / n_splits, s = it % n_splits;
-    wm[it] = ld_sc1(ws + ((row0 + h) * n_splits + s) * (HS + 2));
+    wm[it] = ld_sc1(ws + ((row0 + h) * n_splits + s) * (HS + 4));
   }
   __syncthreads();
-  for (int it = threadIdx.x; it < QPK * HS; it += 256) {
+  for (int it = threadIdx.x; it < QPK * HS; it += NT) {
     const int h = it / HS, d = it % HS;
     float mx = -INFINITY;
     for (int s = 0; s < n_splits; ++s) mx = fmaxf(mx, wm[h * n_splits + s]);
     float lt = 0.0f, ot = 0.0f;
-    const float* base = ws + (row0 + h) * n_splits * (HS + 2);
-    // no data-dependent branch: empty splits carry m = -inf (weight exp(-inf) = 0), l = 0, o = 0, so every
-    // load is independent and the compiler keeps them all in flight
+    const float* base = ws + (row0 + h) * n_splits * (HS + 4);
 #pragma unroll 8
     for (int s = 0; s < n_splits; ++s) {
       const float c = expf(wm[h * n_splits + s] - mx);
-      lt = fmaf(ld_sc1(base + s * (HS + 2) + 1), c, lt);
-      ot = fmaf(ld_sc1(base + s * (HS + 2) + 2 + d), c, ot);
+      lt = fmaf(ld_sc1(base + s * (HS + 4) + 1), c, lt);
+      ot = fmaf(ld_sc1(base + s * (HS + 4) + 4 + d), c, ot);
     }
     y[(row0 + h) * HS + d] = f2bf(ot / lt);
   }
-  if (threadIdx.x == 0) __hip_atomic_store(cnt + (size_t)t * G + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  LGA_TRACE(6);
 }
 
-template <int HS>
-static int launch_hs(const void* q, const void* kc, const void* vc, const int64_t* pos, void* y, float* ws,
-                     unsigned* cnt, int T, int H, int G, int max_seq, int n_splits, float scale, hipStream_t stream) {
+// (keys in flight per row group, waves per workgroup) by q_per_kv; -D overrides are for tools/attn_sweep.py
+#ifndef LGA_ATTN_Q1
+#define LGA_ATTN_Q1 4, 4
+#endif
+#ifndef LGA_ATTN_Q2
+#define LGA_ATTN_Q2 4, 4
+#endif
+#ifndef LGA_ATTN_Q4
+#define LGA_ATTN_Q4 2, 4
+#endif
+#ifndef LGA_ATTN_Q8
+#define LGA_ATTN_Q8 2, 4
+#endif
+
+template <int HS, int QPK, int UNR, int NW, bool FUSED>
+static void launch_one(dim3 grid, hipStream_t stream, const void* q, void* kc, void* vc, const int64_t* pos, void* y,
+                       float* ws, unsigned* cnt, int H, int max_seq, float scale, const int64_t* rope_pos,
+                       const float* cos, const float* sin, int rope_rows) {
+  attn_kernel<HS, QPK, UNR, NW, FUSED><<<grid, NW * 64, 0, stream>>>((const uint16_t*)q, (uint16_t*)kc, (uint16_t*)vc,
+                                                                     pos, (uint16_t*)y, ws, cnt, H, max_seq, scale,
+                                                                     rope_pos, cos, sin, rope_rows);
+}
+
+template <int HS, bool FUSED>
+static int launch_hs(const void* q, void* kc, void* vc, const int64_t* pos, void* y, float* ws, unsigned* cnt, int T,
+                     int H, int G, int max_seq, int n_splits, float scale, const int64_t* rope_pos, const float* cos,
+                     const float* sin, int rope_rows, hipStream_t stream) {
   const dim3 grid(n_splits, G, T);
-#define LGA_ATTN(QPK, UNR)                                                                                    \
-  attn_kernel<HS, QPK, UNR><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)kc,                 \
-                                                      (const uint16_t*)vc, pos, (uint16_t*)y, ws, cnt, H, max_seq, \
-                                                      scale)
+#define LGA_ATTN(QPK, CFG) \
+  launch_one<HS, QPK, CFG, FUSED>(grid, stream, q, kc, vc, pos, y, ws, cnt, H, max_seq, scale, rope_pos, cos, sin, rope_rows)
   switch (H / G) {
-    case 1: LGA_ATTN(1, 4); break;
-    case 2: LGA_ATTN(2, 4); break;
-    case 4: LGA_ATTN(4, 2); break;
-    case 8: LGA_ATTN(8, 2); break;
+    case 1: LGA_ATTN(1, LGA_ATTN_Q1); break;
+    case 2: LGA_ATTN(2, LGA_ATTN_Q2); break;
+    case 4: LGA_ATTN(4, LGA_ATTN_Q4); break;
+    case 8: LGA_ATTN(8, LGA_ATTN_Q8); break;
     default: lga_set_error("lga_attention: q_per_kv must be 1, 2, 4 or 8"); return (int)hipErrorInvalidValue;
   }
 #undef LGA_ATTN
@@ -231,16 +354,17 @@ extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_c
                              int head_size, int max_seq, int n_splits, float scale, hipStream_t stream) {
   LGA_CHECK_ARG(q && k_cache && v_cache && input_pos && y, "lga_attention: null pointer");
   LGA_CHECK_ARG(T > 0 && n_query_groups > 0 && n_head % n_query_groups == 0, "lga_attention: bad head geometry");
-  LGA_CHECK_ARG(n_splits >= 1 && n_splits <= 512, "lga_attention: n_splits must be in [1, 512]");
+  LGA_CHECK_ARG(n_splits >= 1 && n_splits <= 256, "lga_attention: n_splits must be in [1, 256]");
   LGA_CHECK_ARG(n_splits == 1 || (workspace && counters), "lga_attention: split attention needs workspace + counters");
-  LGA_CHECK_ARG(n_splits * (n_head / n_query_groups) <= 4 * head_size, "lga_attention: too many splits for the LDS merge");
   int rc;
   if (head_size == 128)
-    rc = lga::launch_hs<128>(q, k_cache, v_cache, input_pos, y, workspace, counters, T, n_head, n_query_groups,
-                             max_seq, n_splits, scale, stream);
+    rc = lga::launch_hs<128, false>((const void*)q, (void*)k_cache, (void*)v_cache, input_pos, y, workspace, counters,
+                                    T, n_head, n_query_groups, max_seq, n_splits, scale, nullptr, nullptr, nullptr, 0,
+                                    stream);
   else if (head_size == 64)
-    rc = lga::launch_hs<64>(q, k_cache, v_cache, input_pos, y, workspace, counters, T, n_head, n_query_groups,
-                            max_seq, n_splits, scale, stream);
+    rc = lga::launch_hs<64, false>((const void*)q, (void*)k_cache, (void*)v_cache, input_pos, y, workspace, counters,
+                                   T, n_head, n_query_groups, max_seq, n_splits, scale, nullptr, nullptr, nullptr, 0,
+                                   stream);
   else {
     lga_set_error("lga_attention: head_size must be 64 or 128");
     return (int)hipErrorInvalidValue;
@@ -249,7 +373,43 @@ extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_c
   LGA_LAUNCH_RETURN();
 }
 
-// fp32 partials (T * H * n_splits * (hs + 2)); the counters (T * G uint32) must be zeroed once at allocation
+// Decode step (T = 1) with RoPE + KV-append fused in: qkv is the fused projection row ([G][q_per_kv + 2][hs]
+// bf16); q and k are roped with cos/sin row rope_pos[0], k and v are written to the caches at cache_pos[0] and
+// the attention output over keys 0..cache_pos[0] lands in y ([n_head][hs]). Replaces lga_rope_kv_append +
+// lga_attention for a token step; full rotary only (rope_n_elem == head_size == 128).
+extern "C" int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, const int64_t* cache_pos,
+                                          const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows,
+                                          void* y, float* workspace, unsigned* counters, int n_head,
+                                          int n_query_groups, int head_size, int rope_n_elem, int max_seq,
+                                          int n_splits, float scale, hipStream_t stream) {
+  LGA_CHECK_ARG(qkv && k_cache && v_cache && cache_pos && rope_pos && cos && sin && y,
+                "lga_attention_decode_fused: null pointer");
+  LGA_CHECK_ARG(n_query_groups > 0 && n_head % n_query_groups == 0, "lga_attention_decode_fused: bad head geometry");
+  LGA_CHECK_ARG(head_size == 128 && rope_n_elem == 128,
+                "lga_attention_decode_fused: needs head_size == rope_n_elem == 128 (use rope_kv_append + attention)");
+  LGA_CHECK_ARG(rope_rows > 0 && max_seq > 0, "lga_attention_decode_fused: empty rope cache or kv cache");
+  LGA_CHECK_ARG(n_splits >= 1 && n_splits <= 256, "lga_attention_decode_fused: n_splits must be in [1, 256]");
+  LGA_CHECK_ARG(n_splits == 1 || (workspace && counters),
+                "lga_attention_decode_fused: split attention needs workspace + counters");
+  const int rc = lga::launch_hs<128, true>(qkv, k_cache, v_cache, cache_pos, y, workspace, counters, 1, n_head,
+                                           n_query_groups, max_seq, n_splits, scale, rope_pos, cos, sin, rope_rows,
+                                           stream);
+  if (rc) return rc;
+  LGA_LAUNCH_RETURN();
+}
+
+#ifdef LGA_ATTN_TRACE
+extern "C" int lga_attn_trace_read(unsigned long long* host, int n) {
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(lga::g_attn_trace), (size_t)n * sizeof(unsigned long long));
+  void* dptr = nullptr;
+  if (e == hipSuccess) e = hipGetSymbolAddress(&dptr, HIP_SYMBOL(lga::g_attn_trace));
+  if (e == hipSuccess) e = hipMemset(dptr, 0, sizeof(lga::g_attn_trace));  // read-and-clear
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return (int)e;
+}
+#endif
+
+// fp32 partials (T * H * n_splits * (hs + 4)); the counters (T * G * 64 uint32) must be zeroed once at allocation
 extern "C" size_t lga_attention_workspace_bytes(int T, int n_head, int head_size, int n_splits) {
-  return n_splits <= 1 ? 0 : (size_t)T * n_head * n_splits * (head_size + 2) * sizeof(float);
+  return n_splits <= 1 ? 0 : (size_t)T * n_head * n_splits * (head_size + 4) * sizeof(float);
 }

@@ -182,6 +182,10 @@ class CausalSelfAttention(nn.Module):
         self.kv_cache: Optional[KVCache] = None
         self.config = config
 
+    # decode tokens (T = 1) with full 128-dim rotary use lga_attention_decode_fused; False keeps the two-launch
+    # rope_kv_append + attention path (bit-identical; tests compare the two)
+    fuse_decode = True
+
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
                 input_pos: Optional[torch.Tensor] = None, *, norm: Optional["RMSNorm"] = None,
                 residual: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -212,7 +216,6 @@ class CausalSelfAttention(nn.Module):
             rope_pos = pos if (cos.size(0) != T or T == kc.size(-2)) else torch.arange(T, device=dev)
         cos = cos.to(device=dev, dtype=torch.float32).contiguous()
         sin = sin.to(device=dev, dtype=torch.float32).contiguous()
-        q = ops.rope_kv_append(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem)
         S = kc.size(-2)
         ws = None
         n_splits = 1
@@ -221,7 +224,13 @@ class CausalSelfAttention(nn.Module):
             ws = getattr(self, "_attn_ws", None)
             if ws is None or ws.key != (1, H, G, hs, n_splits) or ws.counters.device != dev:
                 ws = self._attn_ws = ops.AttentionWorkspace(1, H, G, hs, n_splits, dev)
-        y = ops.attention(q, kc, vc, pos, H, G, hs, 1.0 / math.sqrt(hs), n_splits, workspace=ws)
+        if T == 1 and self.fuse_decode and ops.decode_fusable(hs, c.rope_n_elem):
+            # decode token: RoPE + KV-append + attention in a single launch
+            y = ops.attention_decode_fused(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem,
+                                           1.0 / math.sqrt(hs), n_splits, workspace=ws)
+        else:
+            q = ops.rope_kv_append(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem)
+            y = ops.attention(q, kc, vc, pos, H, G, hs, 1.0 / math.sqrt(hs), n_splits, workspace=ws)
         out = _lin(self.proj, y.view(1, T, H * hs), residual=residual)
         return out.view(B, T, -1)
 

@@ -45,6 +45,7 @@ SIGNATURES = {
     "lga_swiglu": [_P, _P, _P, _L, _P],
     "lga_attention": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_attention_workspace_bytes": [_I, _I, _I, _I],
+    "lga_attention_decode_fused": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_argmax": [_P, _I, _P, _P, _P, _P],
 }
 _RESTYPES = {"lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t}
@@ -174,6 +175,9 @@ def rope_kv_append(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin, n_head,
     return q
 
 
+ATTN_COUNTER_STRIDE = 64  # uint32 per (row, group) arrival counter (kCounterStride in attention.hip)
+
+
 class AttentionWorkspace:
     """Persistent split-attention scratch: fp32 partials + per-(row, group) arrival counters. The counters are
     zeroed once here; the kernel's last-arriving workgroup re-arms them, so the buffers are reusable across
@@ -183,7 +187,7 @@ class AttentionWorkspace:
         nbytes = load_library().lga_attention_workspace_bytes(T, n_head, head_size, n_splits)
         self.key = (T, n_head, n_query_groups, head_size, n_splits)
         self.partials = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=device)
-        self.counters = torch.zeros(T * n_query_groups, dtype=torch.int32, device=device)
+        self.counters = torch.zeros(T * n_query_groups * ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
 
 
 def attention(q, k_cache, v_cache, input_pos, n_head, n_query_groups, head_size, scale, n_splits=1,
@@ -206,11 +210,40 @@ def attention(q, k_cache, v_cache, input_pos, n_head, n_query_groups, head_size,
     return y
 
 
+def attention_decode_fused(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin, n_head, n_query_groups,
+                           head_size, rope_n_elem, scale, n_splits=1, workspace: Optional[AttentionWorkspace] = None,
+                           out=None):
+    """One decode token: RoPE + KV-append + attention in one launch. qkv (1, (H+2G)*hs) is the fused projection
+    row; returns y (1, H*hs) and leaves roped k / v stored in the caches at cache_pos[0]."""
+    if qkv.shape[0] != 1:
+        raise ValueError("attention_decode_fused handles exactly one token (T = 1)")
+    max_seq = k_cache.shape[-2]
+    y = out if out is not None else torch.empty(1, n_head * head_size, dtype=torch.bfloat16, device=qkv.device)
+    if n_splits > 1:
+        if workspace is None or workspace.key != (1, n_head, n_query_groups, head_size, n_splits):
+            workspace = AttentionWorkspace(1, n_head, n_query_groups, head_size, n_splits, qkv.device)
+        ws, cnt = _dev(workspace.partials, "workspace", torch.float32), _dev(workspace.counters, "counters", torch.int32)
+    else:
+        ws = cnt = None
+    _check(load_library().lga_attention_decode_fused(
+        _dev(qkv, "qkv", torch.bfloat16), _dev(k_cache, "k_cache", torch.bfloat16),
+        _dev(v_cache, "v_cache", torch.bfloat16), _dev(cache_pos, "cache_pos", torch.int64),
+        _dev(rope_pos, "rope_pos", torch.int64), _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32),
+        cos.shape[0], _dev(y, "y", torch.bfloat16), ws, cnt, n_head, n_query_groups, head_size, rope_n_elem, max_seq,
+        n_splits, float(scale), _stream()))
+    return y
+
+
+def decode_fusable(head_size: int, rope_n_elem: int) -> bool:
+    """Whether lga_attention_decode_fused covers this geometry (full rotary over 128-dim heads)."""
+    return head_size == 128 and rope_n_elem == 128
+
+
 def decode_splits(n_query_groups: int, q_per_kv: int, head_size: int, max_seq: int, n_cu: int = 256) -> int:
-    """Sequence splits for T = 1 attention: ~2 workgroups per CU across all query groups."""
-    s = max(1, (2 * n_cu) // max(1, n_query_groups))
-    s = min(s, max(1, max_seq // 16), 512, (4 * head_size) // q_per_kv)
-    return s
+    """Sequence splits for T = 1 attention: one workgroup per CU across all query groups (tools/attn_sweep.py:
+    8 splits beat 16 for Llama-2-7B at p = 128..4000 on MI355X — every extra split adds publish/combine work)."""
+    s = max(1, n_cu // max(1, n_query_groups))
+    return min(s, max(1, max_seq // 16), 256)
 
 
 def embedding(idx, table, out=None):

@@ -192,7 +192,7 @@ def test_rope_kv_append_bit_exact(ops, H, G, hs, n_elem):
 @pytest.mark.parametrize("H,G,hs", [(32, 32, 128), (64, 8, 128), (8, 1, 128), (4, 2, 64)])
 @pytest.mark.parametrize("T,positions", [(1, [0]), (1, [2047]), (1, [2302]), (5, [100, 101, 102, 103, 104]),
                                           (3, [0, 1, 2])])
-@pytest.mark.parametrize("splits", [1, 36])
+@pytest.mark.parametrize("splits", [1, 36, 256])
 def test_attention_matches_reference(ops, H, G, hs, T, positions, splits):
     S = 2304
     q = bf16_np(synth.normal((T, H, hs), "aq", 5, 1.0))
@@ -211,6 +211,48 @@ def test_attention_matches_reference(ops, H, G, hs, T, positions, splits):
             e = np.exp(s - s.max())
             ref[t, h] = (e / e.sum()) @ vv
     assert np.max(np.abs(y - ref) - np.abs(ref) * 2 ** -7) <= 1e-4
+
+
+@pytest.mark.parametrize("H,G", [(32, 32), (64, 8), (8, 1), (16, 8)])
+@pytest.mark.parametrize("p", [0, 1, 37, 2047, 2303])
+@pytest.mark.parametrize("splits", [1, 7, 36])
+def test_attention_decode_fused_matches_two_launch_path(ops, H, G, p, splits):
+    """RoPE + KV-append + attention in one launch == lga_rope_kv_append then lga_attention: caches bit-exact,
+    y within fp32 reordering (the new key is accumulated last), and both close to an fp64 softmax."""
+    hs, S = 128, 2304
+    qkv = to_dev_bf16(synth.normal((1, (H + 2 * G) * hs), "fq", 7, 1.0))
+    k0 = to_dev_bf16(synth.normal((G, S, hs), "fk", 7, 1.0))
+    v0 = to_dev_bf16(synth.normal((G, S, hs), "fv", 7, 1.0))
+    cos, sin = om.build_rope_cache(S, hs, 10000)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pos = torch.tensor([p], device=DEV)
+    scale = 1.0 / math.sqrt(hs)
+    ka, va = k0.clone(), v0.clone()
+    q = ops.rope_kv_append(qkv, ka, va, pos, pos, cos, sin, H, G, hs, hs)
+    ya = ops.attention(q, ka, va, pos, H, G, hs, scale, n_splits=splits).float()
+    kb, vb = k0.clone(), v0.clone()
+    yb = ops.attention_decode_fused(qkv, kb, vb, pos, pos, cos, sin, H, G, hs, hs, scale, n_splits=splits).float()
+    assert torch.equal(ka, kb) and torch.equal(va, vb)
+    assert torch.all((ya - yb).abs() <= ya.abs() * 2 ** -7 + 2e-3)
+    # fp64 reference from the (bit-exact) cache contents
+    qpk = H // G
+    qd = q.double().cpu()
+    kd, vd = ka[:, : p + 1].double().cpu(), va[:, : p + 1].double().cpu()
+    ref = torch.empty(H, hs, dtype=torch.float64)
+    for h in range(H):
+        s = kd[h // qpk] @ qd[0, h] * scale
+        ref[h] = torch.softmax(s, 0) @ vd[h // qpk]
+    yb = yb.double().cpu().view(H, hs)
+    assert torch.max((yb - ref).abs() - ref.abs() * 2 ** -7) <= 1e-4
+
+
+def test_attention_decode_fused_rejects_unsupported_geometry(ops):
+    qkv = torch.zeros(1, 3 * 64 * 4, dtype=torch.bfloat16, device=DEV)
+    kc = torch.zeros(4, 16, 64, dtype=torch.bfloat16, device=DEV)
+    cos = torch.ones(16, 64, device=DEV)
+    pos = torch.zeros(1, dtype=torch.int64, device=DEV)
+    with pytest.raises(RuntimeError, match="head_size == rope_n_elem == 128"):
+        ops.attention_decode_fused(qkv, kc, kc.clone(), pos, pos, cos, cos, 4, 4, 64, 64, 0.125)
 
 
 def test_attention_split_counters_rearm_across_launches(ops):
