@@ -12,7 +12,8 @@ barrier; the max over ranks is reported.
 
 Extra objects in the JSON line:
   roofline      the dominant kernel (fused RMSNorm + fc_1/fc_2 int4 GEMV + SwiGLU of one block, 46.5 MB of
-                algorithmic bytes per launch) timed with HIP events on the launch stream; peak 8 TB/s
+                algorithmic bytes per launch) timed with HIP events on the launch stream (all 32 blocks back to
+                back in a HIP graph); peak 8 TB/s; traffic = HBM bytes per launch from a rocprofv3 FETCH_SIZE pass
   step_roofline the whole decode step: algorithmic bytes per token (weights + KV read/write) x tok/s
   cpu_baseline  the CPU oracle (restatement of the reference's bf16 math) timed on this host on a bounded sample
 """
@@ -52,38 +53,103 @@ def algorithmic_bytes_per_token(cfg, pos: float, group: int = 128, tp: int = 1) 
     return weights + norms + C * 2 + kv
 
 
-def time_dominant_kernel(model, reps: int = 50):
-    """Average duration of the fused RMSNorm + SwiGLU GEMV of block 0 with HIP events on its launch stream."""
+DOMINANT = "gemv_q4_kernel<.., DUAL> (RMSNorm + fc_1/fc_2 int4 GEMV + SwiGLU of one block)"
+
+
+def _dual_gemv_bytes(f1, C: int) -> int:
+    """Algorithmic bytes of one dual-GEMV launch: both packed weight matrices + their group scales, the norm weight,
+    x, and the bf16 output (kernel table)."""
+    return (2 * f1.qweight.numel() + 2 * f1.scales.numel() * f1.scales.element_size() + 2 * C * 2
+            + f1.out_features * 2)
+
+
+def time_dominant_kernel(model, replays: int = 5):
+    """Average launch duration of the dominant kernel, measured with HIP events on the stream the launches run on:
+    the fused RMSNorm + fc_1/fc_2 + SwiGLU GEMV of every block (32 distinct 46.5 MB weight sets, 1.5 GB, so every
+    launch streams from HBM as in the decode step), captured back to back in one HIP graph and replayed."""
     from lit_gpt import ops
 
-    blk = model.transformer.h[0]
-    f1, f2 = blk.mlp.fc_1, blk.mlp.fc_2
+    blocks = model.transformer.h
+    f1 = blocks[0].mlp.fc_1
     C = f1.in_features
     x = torch.randn(C, device="cuda").to(torch.bfloat16)
     out = torch.empty(f1.out_features, dtype=torch.bfloat16, device="cuda")
+
+    def launch_all():
+        for blk in blocks:
+            a, b = blk.mlp.fc_1, blk.mlp.fc_2
+            ops.q4_gemv_swiglu(x, a.qweight, a.scales, b.qweight, b.scales, a.out_features, C, a.group, a.fmt,
+                               norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps, out=out)
+
+    launch_all()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        launch_all()
+    graph.replay()
+    torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for _ in range(replays):
+        graph.replay()
+    e.record(stream)
+    e.synchronize()
+    avg_ms = s.elapsed_time(e) / (replays * len(blocks))
+    return avg_ms, _dual_gemv_bytes(f1, C)
 
-    def launch():
-        ops.q4_gemv_swiglu(x, f1.qweight, f1.scales, f2.qweight, f2.scales, f1.out_features, C, f1.group, f1.fmt,
-                           norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps, out=out)
 
-    for _ in range(5):
-        launch()
-    # flush caches between launches so each reads its weights from HBM as in the decode step
-    flush = torch.empty(512 * 1024 * 1024 // 4, dtype=torch.float32, device="cuda")
-    times = []
-    for _ in range(reps):
-        flush.zero_()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record(stream)
-        launch()
-        e.record(stream)
-        e.synchronize()
-        times.append(s.elapsed_time(e))
-    times.sort()
-    avg_ms = sum(times) / len(times)
-    nbytes = 2 * f1.qweight.numel() + 2 * f1.scales.numel() * f1.scales.element_size() + 2 * C * 2 + f1.out_features * 2
-    return avg_ms, nbytes
+def pmc_child() -> None:
+    """Run under `rocprofv3 --pmc FETCH_SIZE` by measure_traffic(): the dominant kernel at Llama-2-7B shape over
+    24 distinct weight sets (1.1 GB, beyond the 256 MB Infinity Cache), one launch each."""
+    from lit_gpt import ops
+
+    C, N, copies = 4096, 11008, 24
+    dev = torch.device("cuda")
+    sets = []
+    for _ in range(copies):
+        q1, s1 = ops.quantize(torch.randn(N, C, device=dev) * 0.02, 0, 128)
+        q2, s2 = ops.quantize(torch.randn(N, C, device=dev) * 0.02, 0, 128)
+        sets.append((q1, s1, q2, s2))
+    x = torch.randn(C, device=dev).to(torch.bfloat16)
+    nw = torch.ones(C, device=dev).to(torch.bfloat16)
+    out = torch.empty(N, dtype=torch.bfloat16, device=dev)
+    torch.cuda.synchronize()
+    for q1, s1, q2, s2 in sets:
+        ops.q4_gemv_swiglu(x, q1, s1, q2, s2, N, C, 128, 0, norm_weight=nw, out=out)
+    torch.cuda.synchronize()
+
+
+def measure_traffic(timeout_s: float = 240.0):
+    """HBM bytes per launch of the dominant kernel from the PMC counters, collected as MI355X_MICROARCH.md's HBM
+    section prescribes: FETCH_SIZE (KiB, TCC_EA0_RDREQ x 64 B) in its own rocprofv3 pass, doubled (gfx950 tallies
+    128-B requests of a 16-B/lane streaming read at 64 B). Runs in a child process started BEFORE this process
+    touches the GPU. Returns (bytes per launch or None, note)."""
+    import csv
+    import shutil
+    import statistics
+    import subprocess
+    import tempfile
+
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not Path(exe).exists():
+        return None, "rocprofv3 not found"
+    out = Path(tempfile.mkdtemp(prefix="lga_pmc_"))
+    cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", str(out), "-o", "pmc", "--",
+           sys.executable, str(Path(__file__).resolve()), "--pmc-child"]
+    try:
+        subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=timeout_s, check=True)
+        files = list(out.rglob("*counter_collection.csv"))
+        vals = [float(r["Counter_Value"]) for f in files for r in csv.DictReader(open(f))
+                if "gemv_q4_kernel" in r.get("Kernel_Name", "") and r.get("Counter_Name") == "FETCH_SIZE"]
+        if not vals:
+            return None, "no FETCH_SIZE rows for the dominant kernel"
+        kib = statistics.median(vals)
+        return 2.0 * kib * 1024.0, f"median FETCH_SIZE {kib:.0f} KiB over {len(vals)} launches, x2 (gfx950)"
+    except Exception as e:  # traffic is diagnostic; never lose the bench line over it
+        return None, f"pmc pass failed: {type(e).__name__}"
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
 
 
 def cpu_baseline(cfg, threads: int, seconds: float = 15.0):
@@ -140,14 +206,24 @@ def cpu_baseline(cfg, threads: int, seconds: float = 15.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=128)
-    ap.add_argument("--warmup", type=int, default=16)
+    # defaults: the eager capture step (p = 2048) + 14 warm-up + 240 timed steps = the 255 decode steps of
+    # SURVEY §8d (p = 2048 ... 2302)
+    ap.add_argument("--steps", type=int, default=240)
+    ap.add_argument("--warmup", type=int, default=14)
     ap.add_argument("--quantize", default="int4-g128")
     ap.add_argument("--prompt_len", type=int, default=PROMPT_LEN)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC pass for roofline.traffic")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.pmc_child:
+        return pmc_child()
+    traffic, traffic_note = None, "skipped"
+    under_profiler = any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_traffic and not under_profiler:
+        traffic, traffic_note = measure_traffic()  # before this process initialises the GPU
 
     import torch.distributed as dist
 
@@ -242,9 +318,11 @@ def main():
                                                                                    T + args.warmup + args.steps],
                    "global_batch": 1, "seq_len": T, "parallelism": f"tp{world}",
                    "graph": not args.no_graph},
-        "roofline": {"bound": "hbm", "kernel": "gemv_q4_kernel<.., DUAL> (RMSNorm+fc_1/fc_2+SwiGLU, block 0)",
+        "roofline": {"bound": "hbm", "kernel": DOMINANT,
                      "achieved": round(kern_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(kern_gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                     "frac": round(kern_gbs / HBM_PEAK_GBS, 4),
+                     "traffic": None if traffic is None else int(traffic),
+                     "traffic_note": traffic_note,
                      "bytes_per_launch": int(kbytes), "avg_launch_us": round(avg_ms * 1e3, 2)},
         "step_roofline": {"bytes_per_token": int(step_bytes), "achieved": round(step_gbs, 1),
                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(step_gbs / HBM_PEAK_GBS, 4),

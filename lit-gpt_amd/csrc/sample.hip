@@ -17,26 +17,51 @@ __device__ __forceinline__ bool better(float v, int i, float bv, int bi) {
   return (v > bv) || (v == bv && i < bi);
 }
 
+__device__ __forceinline__ void take(float v, int i, float& bv, int& bi) {
+  const bool t = better(v, i, bv, bi);
+  bv = t ? v : bv;
+  bi = t ? i : bi;
+}
+
+// One workgroup; every lane issues all of its 16-B loads (8 logits each, up to kVec per lane per pass) before
+// comparing, so a 32000-entry vocabulary costs one memory round trip instead of one per element.
+constexpr int kVec = 8;
+
+template <bool VEC>
 __global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict__ logits, int n,
                                                       int64_t* __restrict__ out_idx, int32_t* __restrict__ token_out,
                                                       int64_t* __restrict__ pos_inout) {
   float bv = -INFINITY;
   int bi = 0x7FFFFFFF;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const float v = bf2f(logits[i]);
-    if (better(v, i, bv, bi)) {
-      bv = v;
-      bi = i;
+  int done = 0;
+  if (VEC) {
+    const int nvec = n / 8;
+    const uint4* lv = (const uint4*)logits;
+    for (int base = 0; base < nvec; base += 1024 * kVec) {
+      uint4 r[kVec];
+#pragma unroll
+      for (int u = 0; u < kVec; ++u) r[u] = lv[min(base + u * 1024 + (int)threadIdx.x, nvec - 1)];
+#pragma unroll
+      for (int u = 0; u < kVec; ++u) {
+        const int vi = base + u * 1024 + threadIdx.x;
+        const uint32_t d[4] = {r[u].x, r[u].y, r[u].z, r[u].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (vi < nvec) {  // clamped duplicate vectors are skipped (the loads above stay unconditional)
+            take(bflo(d[e]), vi * 8 + 2 * e, bv, bi);
+            take(bfhi(d[e]), vi * 8 + 2 * e + 1, bv, bi);
+          }
+        }
+      }
     }
+    done = nvec * 8;
   }
+  for (int i = done + threadIdx.x; i < n; i += blockDim.x) take(bf2f(logits[i]), i, bv, bi);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     const float ov = __shfl_xor(bv, off);
     const int oi = __shfl_xor(bi, off);
-    if (better(ov, oi, bv, bi)) {
-      bv = ov;
-      bi = oi;
-    }
+    take(ov, oi, bv, bi);
   }
   __shared__ float sv[16];
   __shared__ int si[16];
@@ -48,11 +73,7 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict
   __syncthreads();
   if (threadIdx.x == 0) {
     const int nw = blockDim.x >> 6;
-    for (int w = 1; w < nw; ++w)
-      if (better(sv[w], si[w], bv, bi)) {
-        bv = sv[w];
-        bi = si[w];
-      }
+    for (int w = 1; w < nw; ++w) take(sv[w], si[w], bv, bi);
     if (bi >= n) bi = 0;
     if (out_idx) *out_idx = bi;
     if (token_out) *token_out = bi;
@@ -65,6 +86,9 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict
 extern "C" int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
                           hipStream_t stream) {
   LGA_CHECK_ARG(logits && n > 0, "lga_argmax: bad arguments");
-  lga::argmax_kernel<<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, out_idx, token_out, pos_inout);
+  if (((uintptr_t)logits & 15) == 0 && n >= 8)
+    lga::argmax_kernel<true><<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, out_idx, token_out, pos_inout);
+  else
+    lga::argmax_kernel<false><<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, out_idx, token_out, pos_inout);
   LGA_LAUNCH_RETURN();
 }

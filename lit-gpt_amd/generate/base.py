@@ -98,10 +98,16 @@ def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temp
 
 def build_model(config: Config, *, quantize: Optional[str], device: torch.device, seed: int = 1234,
                 checkpoint_path: Optional[Path] = None, max_seq_length: Optional[int] = None,
-                tp=None) -> GPT:
+                tp=None, rope_positions: str = "reference") -> GPT:
     """Instantiate on the meta device, load (or random-init, as GPT._init_weights) the float weights layer by
     layer on the GPU, optionally shard them (``tp(model)``), quantize every Linear on the device, then build the
-    rope tables and the KV cache. Mirrors generate/base.py:151-171 / generate/tp.py:157-190."""
+    rope tables and the KV cache. Mirrors generate/base.py:151-171 / generate/tp.py:157-190.
+
+    ``rope_positions="reference"`` builds the rope tables under a bf16 default dtype, as the reference's
+    ``with fabric.init_tensor(): model.max_seq_length = ...`` does under bf16-true / bnb precision
+    (generate/base.py:153-157): positions above 256 round to bf16. ``"exact"`` keeps fp32 positions."""
+    if rope_positions not in ("reference", "exact"):
+        raise ValueError(f"rope_positions must be 'reference' or 'exact', got {rope_positions!r}")
     from lit_gpt.quantize import QuantizedPrecision
 
     if quantize is None:
@@ -131,8 +137,13 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
         tp(model)
     QuantizedPrecision(quantize).convert_module(model, device)
     torch.cuda.empty_cache()
-    model.max_seq_length = max_seq_length or config.block_size
-    model.cos, model.sin = model.rope_cache(device=device)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.bfloat16 if rope_positions == "reference" else torch.float32)
+    try:
+        model.max_seq_length = max_seq_length or config.block_size
+        model.cos, model.sin = model.rope_cache(device=device)
+    finally:
+        torch.set_default_dtype(prev)
     model.set_kv_cache(batch_size=1, device=device)
     return model.eval()
 

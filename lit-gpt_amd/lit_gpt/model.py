@@ -13,9 +13,10 @@ What runs underneath (GPU, bf16 activations, Linears converted by ``QuantizedPre
 kernel from ``liblitgpt_amd.so`` — embedding gather, RMSNorm fused into the qkv / fc GEMV prologue, RoPE fused
 with the KV-cache append, split-sequence decode attention, the out-projections with the residual add in their
 epilogue, SwiGLU fused into the dual fc_1/fc_2 GEMV, and greedy argmax. Differences from the reference that do
-not change results: the KV cache holds ``n_query_groups`` heads (un-expanded GQA), RoPE positions are exact
-fp32 (the reference's bf16 default-dtype rounding of positions > 256 is not reproduced), and the
-bool mask is never materialised on the hot path (the kernels read keys ``<= input_pos``).
+not change results: the KV cache holds ``n_query_groups`` heads (un-expanded GQA) and the bool mask is never
+materialised on the hot path (the kernels read keys ``<= input_pos``). RoPE positions follow the reference's
+default-dtype semantics (``build_rope_cache``), so ``generate.base.build_model`` reproduces the bf16 rounding of
+positions > 256 that the reference's bf16 ``init_tensor`` context produces.
 """
 
 from __future__ import annotations
@@ -338,11 +339,17 @@ class KVCache(nn.Module):
 
 def build_rope_cache(seq_len: int, n_elem: int, device: Optional[torch.device] = None, base: int = 10000,
                      condense_ratio: int = 1) -> Tuple[torch.Tensor, torch.Tensor]:
-    """cos/sin tables (seq_len, n_elem) in fp32 (model.py:746-764) with exact fp32 positions."""
-    theta = 1.0 / (base ** (torch.arange(0, n_elem, 2, device=device, dtype=torch.float32) / n_elem))
-    seq_idx = torch.arange(seq_len, device=device, dtype=torch.float32) / condense_ratio
-    idx_theta = torch.outer(seq_idx, theta).repeat(1, 2)
-    return torch.cos(idx_theta), torch.sin(idx_theta)
+    """cos/sin tables (seq_len, n_elem) in fp32 (model.py:746-764).
+
+    The positions are a true division of an integer range, so (as in the reference) they take the DEFAULT dtype:
+    under a bf16 default — the reference's ``fabric.init_tensor()`` with bf16-true / bnb precision around
+    ``model.max_seq_length = ...`` (generate/base.py:153-157, generate/tp.py) — positions above 256 round to bf16
+    before the fp32 outer product. ``generate.base.build_model(rope_positions=...)`` chooses that context."""
+    inv_freq = torch.arange(0, n_elem, 2, device=device).float().div(n_elem)
+    theta = 1.0 / torch.pow(float(base), inv_freq)
+    positions = torch.arange(seq_len, device=device).div(condense_ratio)  # default dtype, see above
+    angles = torch.outer(positions, theta).repeat(1, 2)
+    return torch.cos(angles), torch.sin(angles)
 
 
 def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:

@@ -286,6 +286,24 @@ def test_argmax_known_answers_and_ties(ops, golden):
     assert tok.item() == 17 and pos.item() == 42
 
 
+@pytest.mark.parametrize("n", [1, 7, 8, 1001, 32000, 65549, 150001])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_argmax_matches_torch_random(ops, n, offset):
+    """Vector path (16-B aligned) and scalar path (odd offset), multi-pass vocabularies, ties, NaN."""
+    g = torch.Generator().manual_seed(n + offset)
+    x = (torch.randint(-50, 50, (n + offset,), generator=g).float() / 4).bfloat16()  # many exact ties
+    view = x[offset:]
+    dev = x.to(DEV)[offset:]
+    assert ops.argmax(dev).item() == int(torch.argmax(view.float()))
+    if n > 3:
+        x2 = x.clone()
+        x2[offset + n // 2] = float("nan")
+        x2[offset + n - 1] = float("nan")
+        assert ops.argmax(x2.to(DEV)[offset:]).item() == n // 2  # first NaN wins (torch.argmax)
+    neg = torch.full((n,), float("-inf")).bfloat16()
+    assert ops.argmax(neg.to(DEV)).item() == 0
+
+
 def test_embedding_and_add(ops):
     V, C = 500, 256
     table = bf16_np(synth.normal((V, C), "emb", 5, 1.0))

@@ -190,3 +190,23 @@ def test_tp2_gloo_matches_single_process():
         p.join(timeout=300)
         assert p.exitcode == 0
     np.testing.assert_allclose(got, ref, rtol=0, atol=2e-5)
+
+
+def test_rope_cache_follows_reference_default_dtype(golden):
+    """build_rope_cache takes its positions in the default dtype like the reference (lit_gpt/model.py:758): fp32
+    positions by default, bf16-rounded positions under a bf16 default (the reference's init_tensor context)."""
+    from lit_gpt.model import build_rope_cache
+
+    g = golden("g3_ops.npz")
+    for dt, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+        prev = torch.get_default_dtype()
+        torch.set_default_dtype(dt)
+        try:
+            cos, sin = build_rope_cache(2304, 128)
+        finally:
+            torch.set_default_dtype(prev)
+        assert cos.dtype == torch.float32
+        np.testing.assert_array_equal(cos[2040:2050].numpy(), g[f"rope_cos_{tag}"])
+        np.testing.assert_array_equal(sin[2040:2050].numpy(), g[f"rope_sin_{tag}"])
+    cos, _ = build_rope_cache(64, 16, base=1000000, condense_ratio=2)
+    np.testing.assert_array_equal(cos.numpy(), g["rope_small_cos"])

@@ -40,7 +40,7 @@ def test_python_binding_covers_header(lib_path):
     assert sorted(ops.SIGNATURES) == header_symbols()
     lib = ops.load_library()
     assert lib.lga_version() >= 1
-    assert lib.lga_attention_workspace_bytes(1, 32, 128, 36) == 32 * 36 * 130 * 4
+    assert lib.lga_attention_workspace_bytes(1, 32, 128, 36) == 32 * 36 * 132 * 4  # (m, l, 2 pad, o[hs]) fp32
 
 
 def test_argument_validation_without_gpu(lib_path):
