@@ -262,7 +262,19 @@ def main():
         first = ops.argmax(logits.reshape(-1)).to(torch.int32)
         torch.cuda.synchronize()
         prefill_s = time.perf_counter() - t0
-        if args.no_graph:
+        use_graph = not args.no_graph
+        graph_note = None
+        if use_graph:
+            try:
+                dg = DecodeGraph(model, first, T)  # first decode step runs eagerly, then the step is captured
+            except Exception as e:  # e.g. a collective backend that cannot be captured: time the eager loop
+                use_graph, graph_note = False, f"graph capture failed ({type(e).__name__}); eager steps"
+                torch.cuda.synchronize()
+                barrier()
+        if use_graph:
+            def step():
+                dg.step()
+        else:
             from generate.base import next_token
 
             tok = first.view(1, 1)
@@ -272,11 +284,6 @@ def main():
                 nonlocal tok
                 tok = next_token(model, pos, tok.view(1, 1), temperature=0.0)
                 pos.add_(1)
-        else:
-            dg = DecodeGraph(model, first, T)  # first decode step runs eagerly, then the step is captured
-
-            def step():
-                dg.step()
         for _ in range(args.warmup):
             step()
         torch.cuda.synchronize()
@@ -317,7 +324,7 @@ def main():
                    "weights": args.quantize, "prompt_len": T, "decode_positions": [T + args.warmup + 1,
                                                                                    T + args.warmup + args.steps],
                    "global_batch": 1, "seq_len": T, "parallelism": f"tp{world}",
-                   "graph": not args.no_graph},
+                   "graph": use_graph, **({"graph_note": graph_note} if graph_note else {})},
         "roofline": {"bound": "hbm", "kernel": DOMINANT,
                      "achieved": round(kern_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(kern_gbs / HBM_PEAK_GBS, 4),
