@@ -27,6 +27,29 @@
 
 namespace lga {
 
+#ifdef LGA_GEMV_TRACE  // lab builds only (tools/gemv_trace.py): per-wave phase timestamps, 100 MHz clock
+__device__ unsigned long long g_gemv_trace[65536 * 8];
+#define LGA_GTRACE(i)                                                                                        \
+  do {                                                                                                     \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                          \
+    if ((threadIdx.x & 63) == 0)                                                                         \
+      g_gemv_trace[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define LGA_GTRACE_NOWAIT(i)                                                                                 \
+  do {                                                                                                     \
+    if ((threadIdx.x & 63) == 0)                                                                         \
+      g_gemv_trace[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LGA_GTRACE(i) \
+  do {                \
+  } while (0)
+#define LGA_GTRACE_NOWAIT(i) \
+  do {                       \
+  } while (0)
+#endif
+
+
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 
@@ -119,9 +142,23 @@ __device__ __forceinline__ float scale_of(uint32_t bits) {
   return FMT == 0 ? __uint_as_float(bits << 16) : __uint_as_float(bits);
 }
 
+// (v & mask) | 0x43004300 in ONE VOP3 op: the compiler only emits the two-op VOP2 and/or pair (gfx9 VOP3 takes
+// no literal), which makes the nibble unpack 2 ops per bf16 pair instead of 1 (+1 shift for nibbles 1-3)
+__device__ __forceinline__ uint32_t and_or_magic(uint32_t v, uint32_t mask_vgpr) {
+  uint32_t r;
+  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(mask_vgpr), "s"(0x43004300u));
+  return r;
+}
+__device__ __forceinline__ uint32_t nibble_mask() {  // 0x000F000F in a VGPR, materialised once per kernel
+  uint32_t m;
+  asm volatile("v_mov_b32 %0, 0x000F000F" : "=v"(m));
+  return m;
+}
+
 // dot of one 16-byte weight chunk (32 nibbles) with the LDS x chunk (4 uint4 of (x_i, x_i+4) pairs)
 template <int FMT>
-__device__ __forceinline__ float chunk_dot(const uint4 w, const uint4* xc, float xsum, const float* nf4) {
+__device__ __forceinline__ float chunk_dot(const uint4 w, const uint4* xc, float xsum, const float* nf4,
+                                           uint32_t mask) {
   const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
   float d = 0.0f;
 #pragma unroll
@@ -131,7 +168,7 @@ __device__ __forceinline__ float chunk_dot(const uint4 w, const uint4* xc, float
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       if (FMT == 0) {
-        d = dot2_bf16(xp[s], ((wd[j] >> (4 * s)) & 0x000F000Fu) | 0x43004300u, d);
+        d = dot2_bf16(xp[s], and_or_magic(s == 0 ? wd[j] : wd[j] >> (4 * s), mask), d);
       } else {
         d = fmaf(nf4[(wd[j] >> (4 * s)) & 0xF], bflo(xp[s]), d);
         d = fmaf(nf4[(wd[j] >> (4 * s + 16)) & 0xF], bfhi(xp[s]), d);
@@ -154,6 +191,7 @@ __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
   const int NC = a.K / 32, n8 = a.K / 8, groups = a.K / a.G;
   const int row0 = (blockIdx.x * 4 + wave) * RPR;
   if (FMT == 1 && t < 16) nf4[t] = kNF4v[t];
+  LGA_GTRACE_NOWAIT(0);
 
   // 1. activation (and norm weight) share of this thread: uint4 t, t+256, ... (clamped, branch-free)
   uint4 xr[CPT], nr[CPT];
@@ -189,6 +227,7 @@ __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
   }
   if (RES) res = a.residual[min(row0 + (lane & (RPR - 1)), a.N - 1)];
   __builtin_amdgcn_sched_barrier(0);  // nothing that waits on x may move above the weight loads
+  LGA_GTRACE_NOWAIT(1);
 
   // 3. stage x into LDS (RMS-normalised when NORM) while the weights stream
   float rs = 1.0f;
@@ -207,6 +246,7 @@ __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
     }
     ss = wave_sum_uniform(ss);
     if (lane == 0) red[wave] = ss;
+    LGA_GTRACE_NOWAIT(2);
     __syncthreads();
     rs = 1.0f / sqrtf(((red[0] + red[1]) + (red[2] + red[3])) / (float)a.K + a.eps);
   }
@@ -233,8 +273,11 @@ __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
     }
   }
   __syncthreads();
+  LGA_GTRACE_NOWAIT(3);
+  LGA_GTRACE(4);
 
   // 4. dequant-dot every row of this wave, then one butterfly for all of them
+  const uint32_t nmask = nibble_mask();
   float part[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) part[i] = 0.0f;
@@ -247,10 +290,10 @@ __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
     const float xs = xsum[cc];
 #pragma unroll
     for (int i = 0; i < RPR; ++i) {
-      const float d = chunk_dot<FMT>(w[i][j], xc, xs, nf4);
+      const float d = chunk_dot<FMT>(w[i][j], xc, xs, nf4, nmask);
       if (DUAL) {  // value index = 2*row + matrix (so the pair of one row lands in lanes l and l^8 / l^16 / l^32)
         part[2 * i] = fmaf(ok ? scale_of<FMT>(s[i][j]) : 0.0f, d, part[2 * i]);
-        const float d2 = chunk_dot<FMT>(w2[i][j], xc, xs, nf4);
+        const float d2 = chunk_dot<FMT>(w2[i][j], xc, xs, nf4, nmask);
         part[2 * i + 1] = fmaf(ok ? scale_of<FMT>(s2[i][j]) : 0.0f, d2, part[2 * i + 1]);
       } else {
         part[i] = fmaf(ok ? scale_of<FMT>(s[i][j]) : 0.0f, d, part[i]);
@@ -269,6 +312,7 @@ __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
       const float g = round_bf(silu_f(round_bf(tot)));  // silu(bf16(fc_1 x)) -> bf16
       a.y[row] = f2bf(__fmul_rn(g, round_bf(other)));   // * bf16(fc_2 x)
     }
+    LGA_GTRACE(5);
   } else {
     const int row = row0 + vi;
     float o = tot;
@@ -280,6 +324,7 @@ __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
       o += bf2f(a.bias[min(row, a.N - 1)]);
     }
     if ((lane & (GROUP - 1)) == 0 && row < a.N) a.y[row] = f2bf(o);
+    LGA_GTRACE(5);
   }
 }
 
@@ -309,7 +354,9 @@ static int dispatch(const GemvArgs& a, int variant, hipStream_t stream) {
     const long rows = DUAL ? 2L * a.N : a.N;
     variant = rows >= 24000 ? 1 : 0;  // tall matrices: more rows per wave keep the grid ~3-4 workgroups per CU
   }
-  const bool big = variant != 0;
+  // A persistent, double-buffered streaming form of this kernel (few workgroups per CU walking row tiles) measured
+  // 10-70 % slower on every decode shape (tools/gemv_sweep.py, round 1) and was dropped.
+  const bool big = (variant & 1) != 0;
 #define LGA_L(RS, RB, CPT)                                                         \
   do {                                                                             \
     if (big) launch<(DUAL ? (RB) / 2 : (RB)), CPT, FMT, DUAL>(a, stream);          \
@@ -366,3 +413,14 @@ extern "C" int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const 
   if (rc) return rc;
   LGA_LAUNCH_RETURN();
 }
+
+#ifdef LGA_GEMV_TRACE
+extern "C" int lga_gemv_trace_read(unsigned long long* host, int n) {
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(lga::g_gemv_trace), (size_t)n * sizeof(unsigned long long));
+  void* dptr = nullptr;
+  if (e == hipSuccess) e = hipGetSymbolAddress(&dptr, HIP_SYMBOL(lga::g_gemv_trace));
+  if (e == hipSuccess) e = hipMemset(dptr, 0, sizeof(lga::g_gemv_trace));
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return (int)e;
+}
+#endif

@@ -4,6 +4,7 @@ Weights are rotated over enough copies (> 1 GiB) that each launch streams from H
 launches run back to back between two HIP events (as inside the captured step).
 """
 
+import os
 import sys
 from pathlib import Path
 
@@ -28,7 +29,7 @@ def main(fmt=0, group=128):
     res = {}
     for name, (N, K, dual) in SHAPES.items():
         per = N * K // 2 * (2 if dual else 1)
-        copies = max(2, int(1.5e9 // per))
+        copies = int(os.environ["GEMV_COPIES"]) if "GEMV_COPIES" in os.environ else max(2, int(1.5e9 // per))
         mats = []
         for c in range(copies):
             w = torch.randn(N, K, device=dev) * 0.02
@@ -40,9 +41,10 @@ def main(fmt=0, group=128):
         y = torch.empty(N, device=dev, dtype=torch.bfloat16)
         nbytes = per + (N * K // group) * (2 if fmt == 0 else 4) * (2 if dual else 1)
         best = None
-        for rw in (0, 1):  # rows per wave: small / large
-            for blocks in (0,):
-                v = rw | (blocks << 4)
+        variants = [int(v) for v in os.environ.get("GEMV_VARIANTS", "0,1").split(",")]
+        for v in variants:  # bit0: rows per wave small/large
+            rw, blocks = v & 1, v >> 4
+            if True:
 
                 def run(i):
                     (qa, sa), q2 = mats[i % copies]
@@ -73,7 +75,8 @@ def main(fmt=0, group=128):
                 gbs = nbytes / us / 1e3
                 if best is None or us < best[0]:
                     best = (us, v, gbs)
-                print(f"{name:8s} rw_sel={rw} blocks={blocks:5d}  {us:8.2f} us  {gbs:8.1f} GB/s", flush=True)
+                print(f"{name:8s} variant={v:3d} (big={rw} stream={(v >> 2) & 1} bpc={blocks})  {us:8.2f} us  "
+                      f"{gbs:8.1f} GB/s", flush=True)
         res[name] = best
         print(f"BEST {name}: variant={best[1]} ({best[1] & 15}, {best[1] >> 4}) {best[0]:.2f} us {best[2]:.1f} GB/s",
               flush=True)
