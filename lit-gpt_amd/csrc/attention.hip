@@ -306,6 +306,163 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
   LGA_TRACE(6);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Prefill (T > 1): flash attention on MFMA (v_mfma_f32_16x16x32_bf16). A workgroup = 4 waves = 64 query rows of one
+// head; each wave owns 16 rows. Key tiles of 32 rows stream through LDS: K as stored ([key][hs], XOR-swizzled 16-B
+// chunks) is the B operand of S = Q.K^T directly; V is staged transposed ([hs][key]) so it is the B operand of
+// O += P.V; P goes through a per-wave LDS tile to change from the accumulator layout (lane = key column) to the A
+// operand layout (lane = query row). Online softmax in fp32 per query row (16-lane shuffles). Query t sees keys
+// <= input_pos[t] (the reference's mask rows, lit_gpt/model.py:509,651); the key loop stops at the block's
+// largest position.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + 16 * (chunk ^ ((row >> 2) & 3)); }
+__device__ __forceinline__ int swz256(int row, int chunk) { return row * 256 + 16 * (chunk ^ (row & 15)); }
+
+template <int HS>
+__global__ void __launch_bounds__(256) attn_prefill_kernel(const uint16_t* __restrict__ q,
+                                                           const uint16_t* __restrict__ kc,
+                                                           const uint16_t* __restrict__ vc,
+                                                           const int64_t* __restrict__ input_pos,
+                                                           uint16_t* __restrict__ y, int T, int n_head, int G,
+                                                           int max_seq, float scale) {
+  constexpr int KB = 32;          // keys per tile
+  constexpr int KS = HS / 32;     // MFMA k-steps over the head dim
+  constexpr int NT = HS / 16;     // output column tiles
+  __shared__ __attribute__((aligned(16))) unsigned char k_lds[KB * HS * 2];
+  __shared__ __attribute__((aligned(16))) unsigned char vt_lds[HS * KB * 2];
+  __shared__ __attribute__((aligned(16))) unsigned char p_lds[4][16 * KB * 2];
+  __shared__ long s_kmax;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int fr = lane & 15, fk = lane >> 4;
+  const int h = blockIdx.y, g = h / (n_head / G);
+  const int q0 = blockIdx.x * 64, qw = q0 + wave * 16;
+
+  // the block's key range: max position over its rows
+  if (tid < 64) {
+    long pm = tid < T - q0 ? input_pos[q0 + tid] : -1;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) pm = max(pm, (long)__shfl_xor(pm, o));
+    if (tid == 0) s_kmax = min(pm, (long)max_seq - 1);
+  }
+  // Q fragments (A operand): row fr of this wave, k-slice ks*32 + fk*8
+  bf16x8_t qa[KS];
+  const int qrow = min(qw + fr, T - 1);
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks)
+    qa[ks] = *(const bf16x8_t*)(q + ((size_t)qrow * n_head + h) * HS + ks * 32 + fk * 8);
+  // positions of the 4 accumulator rows this lane holds
+  long rpos[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int t = qw + fk * 4 + r;
+    rpos[r] = t < T ? input_pos[t] : -1;
+  }
+  __syncthreads();
+  const int kend = (int)s_kmax + 1;
+
+  f32x4_t o[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) o[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  float m[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    m[r] = -INFINITY;
+    l[r] = 0.f;
+  }
+  const uint16_t* kbase = kc + (size_t)g * max_seq * HS;
+  const uint16_t* vbase = vc + (size_t)g * max_seq * HS;
+  constexpr int CPR = HS / 8;                // 16-B chunks per key row
+  constexpr int LPT = KB * CPR / 256;        // chunks per thread per tile (K and V each)
+  for (int k0 = 0; k0 < kend; k0 += KB) {
+    // stage K (row-major, swizzled) and V^T
+    uint4 kr[LPT], vr[LPT];
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i, row = c / CPR, ch = c % CPR;
+      const int key = min(k0 + row, max_seq - 1);
+      kr[i] = *(const uint4*)(kbase + (size_t)key * HS + ch * 8);
+      vr[i] = *(const uint4*)(vbase + (size_t)key * HS + ch * 8);
+    }
+    __syncthreads();  // previous tile's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int c = tid + 256 * i, row = c / CPR, ch = c % CPR;
+      *(uint4*)(k_lds + (HS == 128 ? swz256(row, ch) : row * HS * 2 + 16 * (ch ^ (row & 7)))) = kr[i];
+      const uint32_t d[4] = {vr[i].x, vr[i].y, vr[i].z, vr[i].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int col = ch * 8 + e;  // hs index -> row of V^T
+        const uint16_t val = (uint16_t)(e & 1 ? d[e >> 1] >> 16 : d[e >> 1] & 0xFFFF);
+        *(uint16_t*)(vt_lds + swz64(col, row >> 3) + (row & 7) * 2) = val;
+      }
+    }
+    __syncthreads();
+    // S = Q K^T for this wave's 16 rows x 32 keys (2 column tiles)
+    f32x4_t sacc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int krow = j * 16 + fr, ch = ks * 4 + fk;
+        const bf16x8_t kb =
+            *(const bf16x8_t*)(k_lds + (HS == 128 ? swz256(krow, ch) : krow * HS * 2 + 16 * (ch ^ (krow & 7))));
+        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], kb, sacc[j], 0, 0, 0);
+      }
+    // online softmax per row (lane holds rows fk*4+r, key columns fr and 16+fr)
+    float pr[2][4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float s0 = (k0 + fr <= rpos[r]) ? sacc[0][r] * scale : -INFINITY;
+      float s1 = (k0 + 16 + fr <= rpos[r]) ? sacc[1][r] * scale : -INFINITY;
+      float mx = fmaxf(s0, s1);
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+      const float mn = fmaxf(m[r], mx);
+      const float c = mn == -INFINITY ? 1.0f : expf(m[r] - mn);
+      const float e0 = mn == -INFINITY ? 0.0f : expf(s0 - mn);
+      const float e1 = mn == -INFINITY ? 0.0f : expf(s1 - mn);
+      float rs = e0 + e1;
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off);
+      l[r] = l[r] * c + rs;
+      m[r] = mn;
+#pragma unroll
+      for (int j = 0; j < NT; ++j) o[j][r] *= c;
+      pr[0][r] = e0;
+      pr[1][r] = e1;
+    }
+    // P -> LDS (bf16, [16 rows][32 keys]) -> A fragments
+    unsigned char* pl = p_lds[wave];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = fk * 4 + r, key = j * 16 + fr;
+        *(uint16_t*)(pl + swz64(row, key >> 3) + (key & 7) * 2) = f2bf(pr[j][r]);
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed (the tile is wave-private)
+    __builtin_amdgcn_wave_barrier();
+    const bf16x8_t pa = *(const bf16x8_t*)(pl + swz64(fr, fk));
+    // O += P V
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const bf16x8_t vb = *(const bf16x8_t*)(vt_lds + swz64(j * 16 + fr, fk));
+      o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[j], 0, 0, 0);
+    }
+  }
+  // y[t][h*HS + col] = O / l
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int t = qw + fk * 4 + r;
+    if (t >= T) continue;
+    const float inv = 1.0f / l[r];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) y[((size_t)t * n_head + h) * HS + j * 16 + fr] = f2bf(o[j][r] * inv);
+  }
+}
+
 // (keys in flight per row group, waves per workgroup) by q_per_kv; -D overrides are for tools/attn_sweep.py
 #ifndef LGA_ATTN_Q1
 #define LGA_ATTN_Q1 4, 4
@@ -356,6 +513,18 @@ extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_c
   LGA_CHECK_ARG(T > 0 && n_query_groups > 0 && n_head % n_query_groups == 0, "lga_attention: bad head geometry");
   LGA_CHECK_ARG(n_splits >= 1 && n_splits <= 256, "lga_attention: n_splits must be in [1, 256]");
   LGA_CHECK_ARG(n_splits == 1 || (workspace && counters), "lga_attention: split attention needs workspace + counters");
+  if (T >= 16 && n_splits == 1 && (head_size == 128 || head_size == 64)) {  // prefill: flash attention on MFMA
+    const dim3 grid((T + 63) / 64, n_head);
+    if (head_size == 128)
+      lga::attn_prefill_kernel<128><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+                                                              (const uint16_t*)v_cache, input_pos, (uint16_t*)y, T,
+                                                              n_head, n_query_groups, max_seq, scale);
+    else
+      lga::attn_prefill_kernel<64><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+                                                             (const uint16_t*)v_cache, input_pos, (uint16_t*)y, T,
+                                                             n_head, n_query_groups, max_seq, scale);
+    LGA_LAUNCH_RETURN();
+  }
   int rc;
   if (head_size == 128)
     rc = lga::launch_hs<128, false>((const void*)q, (void*)k_cache, (void*)v_cache, input_pos, y, workspace, counters,

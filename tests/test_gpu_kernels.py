@@ -213,6 +213,33 @@ def test_attention_matches_reference(ops, H, G, hs, T, positions, splits):
     assert np.max(np.abs(y - ref) - np.abs(ref) * 2 ** -7) <= 1e-4
 
 
+@pytest.mark.parametrize("H,G,hs", [(8, 8, 128), (8, 2, 128), (4, 1, 64), (6, 3, 64)])
+@pytest.mark.parametrize("T,start", [(16, 0), (100, 0), (300, 0), (77, 500), (64, 1)])
+def test_prefill_flash_attention_matches_reference(ops, H, G, hs, T, start):
+    """T >= 16 takes the MFMA flash-attention kernel: query t attends keys 0..start+t of the cache (keys beyond
+    the query block and past max_seq masked), fp64 softmax reference; bf16 P/V products -> 2^-7 relative."""
+    S = start + T + 40
+    q = bf16_np(synth.normal((T, H, hs), "pq", 9, 1.0))
+    k = bf16_np(synth.normal((G, S, hs), "pk", 9, 1.0))
+    v = bf16_np(synth.normal((G, S, hs), "pv", 9, 1.0))
+    positions = list(range(start, start + T))
+    pos = torch.tensor(positions, dtype=torch.int64)
+    scale = 1.0 / math.sqrt(hs)
+    y = ops.attention(to_dev_bf16(q), to_dev_bf16(k), to_dev_bf16(v), pos.to(DEV), H, G, hs, scale,
+                      n_splits=1).float().cpu().numpy().reshape(T, H, hs)
+    qpk = H // G
+    ref = np.zeros((T, H, hs))
+    for t, p in enumerate(positions):
+        for h in range(H):
+            kk, vv = k[h // qpk, : p + 1].astype(np.float64), v[h // qpk, : p + 1].astype(np.float64)
+            s = kk @ q[t, h].astype(np.float64) * scale
+            e = np.exp(s - s.max())
+            ref[t, h] = (e / e.sum()) @ vv
+    # P enters the PV product as bf16 (as SDPA's bf16 math does): ~2^-8 relative per term
+    err = np.abs(y - ref) - np.abs(ref) * 2 ** -6
+    assert np.max(err) <= 5e-3, float(np.max(err))
+
+
 @pytest.mark.parametrize("H,G", [(32, 32), (64, 8), (8, 1), (16, 8)])
 @pytest.mark.parametrize("p", [0, 1, 37, 2047, 2303])
 @pytest.mark.parametrize("splits", [1, 7, 36])
