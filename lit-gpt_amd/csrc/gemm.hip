@@ -5,13 +5,13 @@
 // (next_token(model, arange(0, T), prompt), generate/base.py:83-85).
 //
 // MI355X design: 128x128 output tile per 256-thread workgroup (2x2 waves, 64x64 per wave = 4x4 tiles of
-// v_mfma_f32_16x16x32_bf16), K-step 32, double-buffered LDS (X and dequantised W tiles, 16-B chunks XOR-swizzled
-// by row so the 16-lane ds_read_b128 groups are conflict-free), next tile's global loads issued before the
-// current tile's MFMAs.
-//   int4-g: W enters the MFMA as the exact small integers (q - 8) in bf16; per-column group scales are applied
-//           to a per-group fp32 partial accumulator (exact dequant semantics, like the decode GEMV);
-//   nf4   : W is dequantised to bf16(NF4[c] * absmax) — the same rounding bitsandbytes' dequantize_4bit applies
-//           before its GEMM.
+// v_mfma_f32_16x16x32_bf16), K-step 64 (two MFMA k-slices per LDS tile, half the barriers of a 32-deep step),
+// double-buffered LDS (X and dequantised W tiles, 128-B rows of 16-B chunks XOR-swizzled by row so the 16-lane
+// ds_read_b128 groups are conflict-free), next tile's global loads issued before the current tile's MFMAs.
+// W is dequantised while it is staged, to bf16(value(nibble) * scale) — the rounding the reference's path applies
+// (bitsandbytes dequantize_4bit to the bf16 weight, then the GEMM), and exactly the bf16 weights the CPU oracle
+// multiplies: int4-g value = nibble - 8 with the bf16 group scale, nf4 value = NF4[nibble] with the fp32 absmax.
+// (An exact-integer-B variant with per-group fp32 partial sums needed 324 VGPRs and ran at half the speed.)
 #include "common.h"
 
 namespace lga {
@@ -19,9 +19,10 @@ namespace lga {
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-constexpr int BM = 128, BN = 128, BK = 32;
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE_BYTES = BM * BK * 2;  // one operand tile in LDS (128 rows x 128 B)
 
-__device__ __forceinline__ int swz(int row, int chunk) { return row * 64 + 16 * (chunk ^ ((row >> 2) & 3)); }
+__device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
 
 __constant__ float kNF4g[16] = {
     -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
@@ -41,97 +42,84 @@ struct GemmArgs {
 
 template <int FMT>
 __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * 2 * BM * BK * 2];  // [buf][A|B][128 rows][64 B]
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * 2 * TILE_BYTES];  // [buf][A|B]
+  __shared__ float wtab[16];  // nibble -> value: nibble - 8 (int4-g) or the NF4 codebook
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int nk = a.K / BK, groups = a.K / a.G;
+  const int nk = (a.K + BK - 1) / BK, groups = a.K / a.G;
   const size_t wrow_bytes = (size_t)a.K / 2;
+  if (tid < 16) wtab[tid] = FMT == 0 ? (float)(tid - 8) : kNF4g[tid];
 
-  // global -> register staging
-  uint4 xa[2];
-  uint2 wq;
-  float wscale = 0.0f;  // nf4 absmax for this thread's W row / block
-  const int a_row0 = tid >> 2, a_chunk = tid & 3;
+  // global -> register staging: X 4 x 16 B per thread (row tid/8 + 32 i, chunk tid%8); W one row-half of 32 k
+  uint4 xa[4];
+  uint4 wq;
+  float wscale = 0.0f;  // group scale (int4-g, bf16) / block absmax (nf4, fp32) of this thread's 32 weights
+  const int a_row = tid >> 3, a_chunk = tid & 7;
   const int w_row = tid >> 1, w_half = tid & 1;
   const int w_n = min(n0 + w_row, a.N - 1);
 
   auto gload = [&](int kt) {
+    // K % 64 == 32 leaves a half tile at the end: its upper X half is zero-filled (so it adds nothing) and its W
+    // half re-reads the row start (in bounds, multiplied by those zeros)
+    const bool a_in = kt * BK + a_chunk * 8 < a.K;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int r = m0 + a_row0 + 64 * i;
-      xa[i] = r < a.M ? *(const uint4*)(a.x + (size_t)r * a.K + kt * BK + a_chunk * 8) : make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < 4; ++i) {
+      const int r = min(m0 + a_row + 32 * i, a.M - 1);  // rows past M duplicate row M-1 (never stored)
+      const uint4 v = *(const uint4*)(a.x + (size_t)r * a.K + (a_in ? kt * BK + a_chunk * 8 : 0));
+      xa[i] = a_in ? v : make_uint4(0, 0, 0, 0);
     }
-    wq = *(const uint2*)(a.qw + (size_t)w_n * wrow_bytes + (kt * BK + w_half * 16) / 2);
-    if (FMT == 1) wscale = ((const float*)a.sc)[(size_t)w_n * groups + (kt * BK) / a.G];
+    const int wk = kt * BK + w_half * 32 < a.K ? kt * BK + w_half * 32 : 0;
+    wq = *(const uint4*)(a.qw + (size_t)w_n * wrow_bytes + wk / 2);
+    const size_t si = (size_t)w_n * groups + wk / a.G;
+    wscale = FMT == 0 ? bf2f(((const uint16_t*)a.sc)[si]) : ((const float*)a.sc)[si];
   };
   auto lstore = [&](int buf) {
-    unsigned char* A = lds + buf * (2 * BM * BK * 2);
-    unsigned char* B = A + BM * BK * 2;
+    unsigned char* A = lds + buf * (2 * TILE_BYTES);
+    unsigned char* B = A + TILE_BYTES;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) *(uint4*)(A + swz(a_row0 + 64 * i, a_chunk)) = xa[i];
-    uint32_t out[8];
-    const uint32_t wd[2] = {wq.x, wq.y};
+    for (int i = 0; i < 4; ++i) *(uint4*)(A + swz(a_row + 32 * i, a_chunk)) = xa[i];
+    const uint32_t wd[4] = {wq.x, wq.y, wq.z, wq.w};  // 32 nibbles = 4 chunks of 8 k
 #pragma unroll
-    for (int e = 0; e < 16; e += 2) {
-      const uint32_t n_lo = (wd[e / 8] >> (4 * (e % 8))) & 0xF, n_hi = (wd[e / 8] >> (4 * (e % 8) + 4)) & 0xF;
-      float lo, hi;
-      if (FMT == 0) {
-        lo = (float)((int)n_lo - 8);
-        hi = (float)((int)n_hi - 8);
-      } else {
-        lo = __fmul_rn(kNF4g[n_lo], wscale);
-        hi = __fmul_rn(kNF4g[n_hi], wscale);
+    for (int c = 0; c < 4; ++c) {
+      uint32_t o4[4];
+#pragma unroll
+      for (int e = 0; e < 8; e += 2) {
+        const uint32_t lo = (wd[c] >> (4 * e)) & 0xF, hi = (wd[c] >> (4 * e + 4)) & 0xF;
+        o4[e / 2] = pack2(__fmul_rn(wtab[lo], wscale), __fmul_rn(wtab[hi], wscale));
       }
-      out[e / 2] = pack2(lo, hi);
+      *(uint4*)(B + swz(w_row, w_half * 4 + c)) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
     }
-    *(uint4*)(B + swz(w_row, 2 * w_half)) = make_uint4(out[0], out[1], out[2], out[3]);
-    *(uint4*)(B + swz(w_row, 2 * w_half + 1)) = make_uint4(out[4], out[5], out[6], out[7]);
   };
 
-  f32x4_t acc[4][4], tmp[4][4];
+  f32x4_t acc[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-      tmp[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
   gload(0);
+  __syncthreads();  // nf4 table
   lstore(0);
   __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < nk) gload(kt + 1);
-    const unsigned char* A = lds + cur * (2 * BM * BK * 2);
-    const unsigned char* B = A + BM * BK * 2;
-    bf16x8_t af[4], bfr[4];
+    const unsigned char* A = lds + cur * (2 * TILE_BYTES);
+    const unsigned char* B = A + TILE_BYTES;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      af[i] = *(const bf16x8_t*)(A + swz(wm * 64 + i * 16 + fr, fk));
-      bfr[i] = *(const bf16x8_t*)(B + swz(wn * 64 + i * 16 + fr, fk));
-    }
+    for (int sub = 0; sub < 2; ++sub) {  // two 32-deep MFMA k-slices per tile
+      bf16x8_t af[4], bfr[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        if (FMT == 0) tmp[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], tmp[i][j], 0, 0, 0);
-        else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      for (int i = 0; i < 4; ++i) {
+        af[i] = *(const bf16x8_t*)(A + swz(wm * 64 + i * 16 + fr, sub * 4 + fk));
+        bfr[i] = *(const bf16x8_t*)(B + swz(wn * 64 + i * 16 + fr, sub * 4 + fk));
       }
-    if (FMT == 0 && ((kt + 1) * BK) % a.G == 0) {
-      const int g = (kt * BK) / a.G;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int n = min(n0 + wn * 64 + j * 16 + fr, a.N - 1);
-        const float s = bf2f(((const uint16_t*)a.sc)[(size_t)n * groups + g]);
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          acc[i][j] += tmp[i][j] * s;
-          tmp[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        }
-      }
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < nk) lstore(cur ^ 1);
     __syncthreads();

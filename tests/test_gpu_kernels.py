@@ -143,9 +143,8 @@ def test_gemm_matches_reference(ops, fmt, group, M, N, K):
     qw, sc = ops.quantize(torch.from_numpy(w).to(DEV), fmt, group)
     res = bf16_np(synth.normal((M, N), "gres", 5, 1.0))
     y = ops.q4_gemm(to_dev_bf16(x), qw, sc, N, K, group, fmt, residual=to_dev_bf16(res)).float().cpu().numpy()
-    wd = _deq(ops, w, fmt, group)
-    if fmt == 1:
-        wd = bf16_np(wd)  # nf4 feeds the MFMA bf16(NF4 * absmax), as bitsandbytes' dequantize_4bit does
+    # the MFMA is fed bf16(value * scale) — the reference's dequantize-to-bf16-then-GEMM rounding
+    wd = bf16_np(_deq(ops, w, fmt, group))
     h = _ref_linear(x, wd)
     ref = bf16_np(h.astype(np.float32)) + res
     err = np.abs(y - ref) - (np.abs(ref) + np.abs(h)) * 2 ** -7
