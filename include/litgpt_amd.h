@@ -97,6 +97,24 @@ int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, co
                                float* workspace, unsigned* counters, int n_head, int n_query_groups, int head_size,
                                int rope_n_elem, int max_seq, int n_splits, float scale, lga_stream_t stream);
 
+/* -- one Llama decode block (Block.forward, lit_gpt/model.py:572-593, T = 1) in ONE persistent launch --------
+ * h_out = h_mid + mlp(norm_2(h_mid)), h_mid = h_in + attn(norm_1(h_in)) with RoPE + KV append of position *pos
+ * (model.py:609-665, 712-716, 767-795). Weights int4-g128 (LGA_FMT_Q4G, group 128): wq (qkv), wo (attn.proj),
+ * w1/w2 (fc_1/fc_2), wd (mlp.proj) with their bf16 scales. Scratch: qkv ((H+2G)*hs), y (H*hs), act (I) bf16,
+ * attn_ws (H * (n_cu/G) * (hs+4) fp32), counters (lga_decode_layer_counters(G) uint32, zeroed once; re-armed
+ * by the kernel), err (1 uint32: bit 0 = a hand-off wait timed out, results invalid). Grid = one workgroup per CU
+ * (n_cu = compute units of the device). Geometry limits (checked, error otherwise): head_size 128, q_per_kv 1,
+ * n_cu a multiple of n_query_groups dividing the qkv rows and n_embd, the qkv rows of one group = that group's
+ * attention workgroups, n_embd 4096, intermediate <= 12288. */
+size_t lga_decode_layer_counters(int n_query_groups);
+int lga_decode_layer(const void* h_in, void* h_mid, void* h_out, const void* norm1, const void* norm2, float eps,
+                     const uint8_t* wq, const void* sq, const uint8_t* wo, const void* so, const uint8_t* w1,
+                     const void* s1, const uint8_t* w2, const void* s2, const uint8_t* wd, const void* sd,
+                     void* k_cache, void* v_cache, const float* cos, const float* sin, int rope_rows,
+                     const int64_t* pos, void* qkv_scratch, void* y_scratch, void* act_scratch, float* attn_ws,
+                     unsigned* counters, unsigned* err, int n_embd, int intermediate, int n_head,
+                     int n_query_groups, int head_size, int max_seq, float scale, int n_cu, lga_stream_t stream);
+
 /* -- greedy sampling (generate/base.py:30-47 at temperature 0): lowest index among the maxima; optionally
  *    writes the token (int32) and advances *pos_inout by one (generate/base.py:92) -------------------------- */
 int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,

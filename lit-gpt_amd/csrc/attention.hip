@@ -15,28 +15,9 @@
 // With splits > 1 every workgroup publishes (m, l, o) write-through (sc1) and bumps a per-(t, group) counter;
 // the workgroup that arrives last merges the splits and writes the bf16 output (flash-decoding combine inside
 // the same launch; MI355X_MICROARCH.md "Valid forms" row 1), then re-arms the counter for the next launch.
-#include "common.h"
+#include "decode_ops.h"
 
 namespace lga {
-
-template <int LPR>
-__device__ __forceinline__ float row_group_sum(float v) {
-  // LPR = 16: full DPP row; LPR = 8: half row
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false));
-  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false));
-  if (LPR == 16) v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false));
-  return v;
-}
-
-__device__ __forceinline__ void unpack8(const uint4 v, float* f) {
-  const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    f[2 * i] = bflo(d[i]);
-    f[2 * i + 1] = bfhi(d[i]);
-  }
-}
 
 #ifdef LGA_ATTN_TRACE  // lab builds only (tools/attn_trace.py): per-block phase timestamps, 100 MHz clock
 __device__ unsigned long long g_attn_trace[8192 * 8];
@@ -61,37 +42,6 @@ typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint4 ld_kv(const uint16_t* p) {
   const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
   return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-__device__ __forceinline__ void st_sc1(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// RoPE of the 8 dims a lane holds (full rotary, n_elem == HS == 128): rotate-half partner dims live 8 lanes away
-// inside the 16-lane row group (DPP row_ror:8). Same math and rounding as lga_rope_kv_append / the reference
-// (x*cos + rotated*sin in fp32, no FMA contraction, one bf16 cast).
-__device__ __forceinline__ uint4 rope8(const uint4 raw, const float* cr, const float* sr, int sub) {
-  const uint32_t d[4] = {raw.x, raw.y, raw.z, raw.w};
-  uint32_t pd[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) pd[i] = __builtin_amdgcn_update_dpp(0, d[i], 0x128, 0xF, 0xF, false);
-  const bool lo_half = sub < 8;
-  uint32_t out[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float r0 = bflo(pd[i]), r1 = bfhi(pd[i]);
-    if (lo_half) {
-      r0 = -r0;
-      r1 = -r1;
-    }
-    const float x0 = bflo(d[i]), x1 = bfhi(d[i]);
-    out[i] = pack2(add_rn(mul_rn(x0, cr[2 * i]), mul_rn(r0, sr[2 * i])),
-                   add_rn(mul_rn(x1, cr[2 * i + 1]), mul_rn(r1, sr[2 * i + 1])));
-  }
-  return make_uint4(out[0], out[1], out[2], out[3]);
 }
 
 // FUSED (decode, T = 1): q, k, v come straight from the qkv projection row; every workgroup ropes its group's

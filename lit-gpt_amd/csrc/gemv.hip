@@ -23,7 +23,7 @@
 //    log2(R) halving exchanges + DPP, instead of R separate wave reductions.
 //  * Epilogues: +bias, +residual (Block residual add, model.py:591-592), dual-weight SwiGLU
 //    (silu(fc_1 x) * fc_2 x, model.py:715) with the reference's bf16 rounding points.
-#include "common.h"
+#include "decode_ops.h"
 
 namespace lga {
 
@@ -50,67 +50,6 @@ __device__ unsigned long long g_gemv_trace[65536 * 8];
 #endif
 
 
-typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
-typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint4 ld_nt16(const void* p) {  // 16-B non-temporal load (weights are read once)
-  const u32x4_t v = __builtin_nontemporal_load((const u32x4_t*)p);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-__device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
-  return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c,
-                                         false);
-}
-
-#define LGA_DPP(v, ctrl) __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false))
-
-// DPP wave reduction -> uniform wave sum (used once per wave for the RMSNorm sum of squares)
-__device__ __forceinline__ float wave_sum_uniform(float v) {
-  v += LGA_DPP(v, 0xB1);   // quad [1,0,3,2]
-  v += LGA_DPP(v, 0x4E);   // quad [2,3,0,1]
-  v += LGA_DPP(v, 0x141);  // row half mirror
-  v += LGA_DPP(v, 0x140);  // row mirror
-  const int i = __float_as_int(v);
-  return (__int_as_float(__builtin_amdgcn_readlane(i, 0)) + __int_as_float(__builtin_amdgcn_readlane(i, 16))) +
-         (__int_as_float(__builtin_amdgcn_readlane(i, 32)) + __int_as_float(__builtin_amdgcn_readlane(i, 48)));
-}
-
-// Transposed butterfly over R in {2, 4, 8} per-lane partials a[0..R). Level with lane-distance D keeps one half
-// of the values and adds the partner's other half. Afterwards lanes whose low log2(64/R) bits are 0 hold the
-// full wave sum of value index  bfly_index<R>(lane).
-template <int R>
-__device__ __forceinline__ float butterfly(float* a, int lane) {
-  constexpr int L = R == 8 ? 3 : (R == 4 ? 2 : 1);
-#pragma unroll
-  for (int lev = 0; lev < L; ++lev) {
-    const int D = 32 >> lev;
-    const int n = R >> (lev + 1);
-    const bool h = lane & D;
-#pragma unroll
-    for (int i = 0; i < n; ++i) {
-      const float send = h ? a[i] : a[i + n], keep = h ? a[i + n] : a[i];
-      float recv;
-      if (D == 8) recv = LGA_DPP(send, 0x128);  // row_ror:8 == xor 8 inside a 16-lane row
-      else recv = __shfl_xor(send, D);
-      a[i] = keep + recv;
-    }
-  }
-  float d = a[0];
-  // reduce over the remaining 64/R lanes (bits below the last exchange distance)
-  d += LGA_DPP(d, 0xB1);
-  d += LGA_DPP(d, 0x4E);
-  d += LGA_DPP(d, 0x141);  // 8-lane groups done (R = 8)
-  if (R <= 4) d += LGA_DPP(d, 0x140);  // 16-lane groups (R = 4)
-  if (R <= 2) d += __shfl_xor(d, 16);  // 32-lane groups (R = 2)
-  return d;
-}
-template <int R>
-__device__ __forceinline__ int bfly_index(int lane) {
-  return R == 8 ? ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1)
-                : (R == 4 ? ((lane >> 5) & 1) * 2 + ((lane >> 4) & 1) : ((lane >> 5) & 1));
-}
-
 struct GemvArgs {
   const uint16_t* x;         // [K] bf16
   const uint8_t* qw;         // [N][K/2]
@@ -125,60 +64,6 @@ struct GemvArgs {
   float eps;
 };
 
-__constant__ float kNF4v[16] = {
-    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
-    -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
-    0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
-    0.7229568362236023f, 1.0f};
-
-// Scales stay raw bits until used: converting at load time makes the compiler wait for the scale load at once,
-// and vmcnt is in order, so that wait would also drain every weight load issued before it.
-template <int FMT>
-__device__ __forceinline__ uint32_t load_scale_bits(const void* sc, size_t i) {
-  return FMT == 0 ? (uint32_t)((const uint16_t*)sc)[i] : ((const uint32_t*)sc)[i];
-}
-template <int FMT>
-__device__ __forceinline__ float scale_of(uint32_t bits) {
-  return FMT == 0 ? __uint_as_float(bits << 16) : __uint_as_float(bits);
-}
-
-// (v & mask) | 0x43004300 in ONE VOP3 op: the compiler only emits the two-op VOP2 and/or pair (gfx9 VOP3 takes
-// no literal), which makes the nibble unpack 2 ops per bf16 pair instead of 1 (+1 shift for nibbles 1-3)
-__device__ __forceinline__ uint32_t and_or_magic(uint32_t v, uint32_t mask_vgpr) {
-  uint32_t r;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(mask_vgpr), "s"(0x43004300u));
-  return r;
-}
-__device__ __forceinline__ uint32_t nibble_mask() {  // 0x000F000F in a VGPR, materialised once per kernel
-  uint32_t m;
-  asm volatile("v_mov_b32 %0, 0x000F000F" : "=v"(m));
-  return m;
-}
-
-// dot of one 16-byte weight chunk (32 nibbles) with the LDS x chunk (4 uint4 of (x_i, x_i+4) pairs)
-template <int FMT>
-__device__ __forceinline__ float chunk_dot(const uint4 w, const uint4* xc, float xsum, const float* nf4,
-                                           uint32_t mask) {
-  const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
-  float d = 0.0f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint4 xv = xc[j];
-    const uint32_t xp[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      if (FMT == 0) {
-        d = dot2_bf16(xp[s], and_or_magic(s == 0 ? wd[j] : wd[j] >> (4 * s), mask), d);
-      } else {
-        d = fmaf(nf4[(wd[j] >> (4 * s)) & 0xF], bflo(xp[s]), d);
-        d = fmaf(nf4[(wd[j] >> (4 * s + 16)) & 0xF], bfhi(xp[s]), d);
-      }
-    }
-  }
-  return FMT == 0 ? d - 136.0f * xsum : d;  // int4: sum x*(128+q) - 136*sum x = sum x*(q-8)
-}
-
-// One workgroup = 4 independent waves (row slots); a wave handles RPR consecutive rows.
 template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES>
 __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

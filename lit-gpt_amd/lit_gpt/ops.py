@@ -13,6 +13,7 @@ kernels that ``lit_gpt/model.py`` issues (RMSNorm, RoPE, index_copy_, SDPA, embe
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 from pathlib import Path
 from typing import Optional
@@ -45,10 +46,13 @@ SIGNATURES = {
     "lga_swiglu": [_P, _P, _P, _L, _P],
     "lga_attention": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_attention_workspace_bytes": [_I, _I, _I, _I],
+    "lga_decode_layer": [_P] * 5 + [_F] + [_P] * 14 + [_I, _P, _P, _P, _P, _P, _P, _P] + [_I] * 6 + [_F, _I, _P],
+    "lga_decode_layer_counters": [_I],
     "lga_attention_decode_fused": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_argmax": [_P, _I, _P, _P, _P, _P],
 }
-_RESTYPES = {"lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t}
+_RESTYPES = {"lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
+             "lga_decode_layer_counters": ctypes.c_size_t}
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -231,6 +235,65 @@ def attention_decode_fused(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin,
         _dev(rope_pos, "rope_pos", torch.int64), _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32),
         cos.shape[0], _dev(y, "y", torch.bfloat16), ws, cnt, n_head, n_query_groups, head_size, rope_n_elem, max_seq,
         n_splits, float(scale), _stream()))
+    return y
+
+
+_N_CU = None
+
+
+def num_cus() -> int:
+    """Compute units of the current device (lga_device_info)."""
+    global _N_CU
+    if _N_CU is None:
+        n = ctypes.c_int(0)
+        arch = ctypes.create_string_buffer(64)
+        _check(load_library().lga_device_info(torch.cuda.current_device(), ctypes.byref(n), arch, 64))
+        _N_CU = int(n.value)
+    return _N_CU
+
+
+class DecodeLayerWorkspace:
+    """Per-block scratch of lga_decode_layer (allocate before graph capture): h_mid, qkv, y, act activations,
+    fp32 attention partials, zeroed hand-off counters (re-armed by the kernel) and the spin-timeout flag."""
+
+    def __init__(self, C: int, I: int, H: int, G: int, hs: int, device) -> None:
+        n_cu = num_cus()
+        bpg = n_cu // G
+        self.key = (C, I, H, G, hs, n_cu)
+        bf = dict(dtype=torch.bfloat16, device=device)
+        self.h_mid = torch.empty(C, **bf)
+        self.qkv = torch.empty((H + 2 * G) * hs, **bf)
+        self.y = torch.empty(H * hs, **bf)
+        self.act = torch.empty(I, **bf)
+        self.partials = torch.empty(H * bpg * (hs + 4), dtype=torch.float32, device=device)
+        self.counters = torch.zeros(int(load_library().lga_decode_layer_counters(G)), dtype=torch.int32, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+        self.n_cu = n_cu
+
+
+def decode_layer(x, blk, cos, sin, pos, kc, vc, ws: DecodeLayerWorkspace, out=None):
+    """One Llama decode block (T = 1) in a single persistent launch: x (C,) bf16 -> h_out (C,). blk is the Block
+    (its QuantLinear / RMSNorm parameters are read); raises RuntimeError when the geometry is unsupported."""
+    c = blk.config
+    at, mlp = blk.attn, blk.mlp
+    C, I, H, G, hs = c.n_embd, mlp.fc_1.out_features, c.n_head, c.n_query_groups, c.head_size
+    y = out if out is not None else torch.empty(C, dtype=torch.bfloat16, device=x.device)
+    q = at.attn
+    _check(load_library().lga_decode_layer(
+        _dev(x, "x", torch.bfloat16), _dev(ws.h_mid, "h_mid"), _dev(y, "h_out", torch.bfloat16),
+        _dev(blk.norm_1.weight, "norm_1", torch.bfloat16), _dev(blk.norm_2.weight, "norm_2", torch.bfloat16),
+        float(blk.norm_1.eps),
+        _dev(q.qweight, "qkv.qweight"), _dev(q.scales, "qkv.scales"),
+        _dev(at.proj.qweight, "proj.qweight"), _dev(at.proj.scales, "proj.scales"),
+        _dev(mlp.fc_1.qweight, "fc_1.qweight"), _dev(mlp.fc_1.scales, "fc_1.scales"),
+        _dev(mlp.fc_2.qweight, "fc_2.qweight"), _dev(mlp.fc_2.scales, "fc_2.scales"),
+        _dev(mlp.proj.qweight, "mlp.proj.qweight"), _dev(mlp.proj.scales, "mlp.proj.scales"),
+        _dev(kc, "k_cache", torch.bfloat16), _dev(vc, "v_cache", torch.bfloat16),
+        _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32), cos.shape[0],
+        _dev(pos, "pos", torch.int64), _dev(ws.qkv, "qkv"), _dev(ws.y, "y"), _dev(ws.act, "act"),
+        _dev(ws.partials, "partials", torch.float32), _dev(ws.counters, "counters", torch.int32),
+        _dev(ws.err, "err", torch.int32), C, I, H, G, hs, kc.shape[-2], 1.0 / math.sqrt(hs), ws.n_cu,
+        _stream()))
     return y
 
 
