@@ -48,7 +48,7 @@ __device__ __forceinline__ uint4 ld_kv(const uint16_t* p) {
 // q heads itself, and the workgroup whose split owns the new position p ropes k, appends k and v to the cache
 // at p (KVCache.forward, lit_gpt/model.py:788-795) and scores that key from registers — replacing the separate
 // lga_rope_kv_append launch of the decode step.
-template <int HS, int QPK, int UNR, int NW, bool FUSED>
+template <int HS, int QPK, int UNR, int NW, bool FUSED, bool PIPE>
 __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
                                                    uint16_t* __restrict__ vc, const int64_t* __restrict__ input_pos,
                                                    uint16_t* __restrict__ y, float* __restrict__ ws,
@@ -102,14 +102,8 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
   }
   const uint16_t* kbase = kc + (size_t)g * max_seq * HS + sub * 8;
   const uint16_t* vbase = vc + (size_t)g * max_seq * HS + sub * 8;
-  for (int j0 = k_lo + rg; j0 < k_end; j0 += RG * UNR) {
-    uint4 kv[UNR], vv[UNR];
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int j = min(j0 + u * RG, k_end - 1);  // clamped duplicate rows are masked below
-      kv[u] = ld_kv(kbase + (size_t)j * HS);
-      vv[u] = ld_kv(vbase + (size_t)j * HS);
-    }
+  // one step = UNR keys per row group: scores, online-softmax rescale, P.V (masked keys score -inf)
+  auto consume = [&](const uint4 (&kv)[UNR], const uint4 (&vv)[UNR], int j0) {
 #pragma unroll
     for (int h = 0; h < QPK; ++h) {
       float s[UNR];
@@ -139,6 +133,36 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
         for (int i = 0; i < 8; ++i) o[h][i] = fmaf(e, vf[i], o[h][i]);
       }
       m[h] = mx;
+    }
+  };
+  // clamped duplicate rows (past k_end) are masked in consume() and hit in cache
+  auto fetch = [&](uint4 (&kv)[UNR], uint4 (&vv)[UNR], int j0) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int j = max(min(j0 + u * RG, k_end - 1), 0);
+      kv[u] = ld_kv(kbase + (size_t)j * HS);
+      vv[u] = ld_kv(vbase + (size_t)j * HS);
+    }
+  };
+  const int j_first = k_lo + rg;
+  if (PIPE && k_lo < k_end) {
+    // software pipeline: the next step's 2*UNR loads are issued before this step's math, so every row group
+    // keeps 2-4 steps of K/V in flight and a split costs one load round trip plus its streaming time
+    uint4 ka[UNR], va[UNR], kb[UNR], vb[UNR];
+    fetch(ka, va, j_first);
+    int j0 = j_first;
+    for (; j0 + RG * UNR < k_end; j0 += 2 * RG * UNR) {
+      fetch(kb, vb, j0 + RG * UNR);
+      consume(ka, va, j0);
+      if (j0 + 2 * RG * UNR < k_end) fetch(ka, va, j0 + 2 * RG * UNR);
+      consume(kb, vb, j0 + RG * UNR);
+    }
+    if (j0 < k_end) consume(ka, va, j0);
+  } else {
+    for (int j0 = j_first; j0 < k_end; j0 += RG * UNR) {
+      uint4 kv[UNR], vv[UNR];
+      fetch(kv, vv, j0);
+      consume(kv, vv, j0);
     }
   }
   LGA_TRACE(3);
@@ -230,25 +254,39 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
   __syncthreads();
   LGA_TRACE(5);
   if (s_last != (unsigned)(n_splits - 1)) return;
-  // combine: split weights exp(m_s - max) staged in LDS, then one column per thread; empty splits carry
-  // m = -inf, l = 0, o = 0 (weight 0), so the split loop has no data-dependent branch and every load stays in flight
-  float* wm = &so[0][0][0];  // reuse LDS: [QPK][n_splits] (host caps n_splits at 256 <= NW * HS)
-  for (int it = threadIdx.x; it < QPK * n_splits; it += NT) {
-    const int h = it / n_splits, s = it % n_splits;
-    wm[it] = ld_sc1(ws + ((row0 + h) * n_splits + s) * (HS + 4));
-  }
-  __syncthreads();
+  // combine, one output column per thread, 8 splits per round with every (m, l, o) load of the round in flight
+  // at once (one load round trip for the usual <= 8 splits) and an online rescale across rounds. Split 0 always
+  // holds key 0, so the running max is finite after round 0; empty splits carry m = -inf, l = 0, o = 0 and
+  // clamped out-of-range slots are forced to m = -inf: both get weight exp(-inf) = 0.
   for (int it = threadIdx.x; it < QPK * HS; it += NT) {
     const int h = it / HS, d = it % HS;
-    float mx = -INFINITY;
-    for (int s = 0; s < n_splits; ++s) mx = fmaxf(mx, wm[h * n_splits + s]);
-    float lt = 0.0f, ot = 0.0f;
     const float* base = ws + (row0 + h) * n_splits * (HS + 4);
-#pragma unroll 8
-    for (int s = 0; s < n_splits; ++s) {
-      const float c = expf(wm[h * n_splits + s] - mx);
-      lt = fmaf(ld_sc1(base + s * (HS + 4) + 1), c, lt);
-      ot = fmaf(ld_sc1(base + s * (HS + 4) + 4 + d), c, ot);
+    float mx = -INFINITY, lt = 0.0f, ot = 0.0f;
+    for (int s0 = 0; s0 < n_splits; s0 += 8) {
+      float mv[8], lv[8], ov[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float* r = base + min(s0 + u, n_splits - 1) * (HS + 4);
+        mv[u] = ld_sc1(r);
+        lv[u] = ld_sc1(r + 1);
+        ov[u] = ld_sc1(r + 4 + d);
+      }
+      float nm = mx;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (s0 + u >= n_splits) mv[u] = -INFINITY;
+        nm = fmaxf(nm, mv[u]);
+      }
+      const float c = expf(mx - nm);  // round 0: exp(-inf) = 0
+      lt *= c;
+      ot *= c;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const float e = expf(mv[u] - nm);
+        lt = fmaf(lv[u], e, lt);
+        ot = fmaf(ov[u], e, ot);
+      }
+      mx = nm;
     }
     y[(row0 + h) * HS + d] = f2bf(ot / lt);
   }
@@ -426,12 +464,15 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const uint16_t* __res
 #ifndef LGA_ATTN_Q8
 #define LGA_ATTN_Q8 2, 4
 #endif
+#ifndef LGA_ATTN_PIPE
+#define LGA_ATTN_PIPE 1
+#endif
 
 template <int HS, int QPK, int UNR, int NW, bool FUSED>
 static void launch_one(dim3 grid, hipStream_t stream, const void* q, void* kc, void* vc, const int64_t* pos, void* y,
                        float* ws, unsigned* cnt, int H, int max_seq, float scale, const int64_t* rope_pos,
                        const float* cos, const float* sin, int rope_rows) {
-  attn_kernel<HS, QPK, UNR, NW, FUSED><<<grid, NW * 64, 0, stream>>>((const uint16_t*)q, (uint16_t*)kc, (uint16_t*)vc,
+  attn_kernel<HS, QPK, UNR, NW, FUSED, LGA_ATTN_PIPE != 0><<<grid, NW * 64, 0, stream>>>((const uint16_t*)q, (uint16_t*)kc, (uint16_t*)vc,
                                                                      pos, (uint16_t*)y, ws, cnt, H, max_seq, scale,
                                                                      rope_pos, cos, sin, rope_rows);
 }

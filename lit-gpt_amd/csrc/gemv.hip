@@ -86,28 +86,25 @@ __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
     xr[i] = ((const uint4*)a.x)[u];
     if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
   }
-  // 2. every weight / scale / residual load of this wave (rows past N re-read row N-1; never stored)
+  // 2. every weight / scale / residual load of this wave (rows past N re-read row N-1; never stored), issued in
+  //    the order step 4 consumes them (chunk-major, each scale right after its weights): vmcnt retires in order,
+  //    so the first dots start once their own chunk has landed instead of after the whole wave's stream
   uint4 w[RPR][CPT], w2[DUAL ? RPR : 1][DUAL ? CPT : 1];
   uint32_t s[RPR][CPT], s2[DUAL ? RPR : 1][DUAL ? CPT : 1];
   uint32_t res = 0;
 #pragma unroll
-  for (int i = 0; i < RPR; ++i) {
-    const size_t rb = (size_t)min(row0 + i, a.N - 1) * (a.K / 2);
+  for (int j = 0; j < CPT; ++j) {
+    const int c = min(lane + 64 * j, NC - 1);
+    const int g = (c * 32) / a.G;
 #pragma unroll
-    for (int j = 0; j < CPT; ++j) {
-      const int c = min(lane + 64 * j, NC - 1);
-      w[i][j] = ld_nt16(a.qw + rb + (size_t)c * 16);
-      if (DUAL) w2[i][j] = ld_nt16(a.qw2 + rb + (size_t)c * 16);
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < RPR; ++i) {
-    const size_t n = (size_t)min(row0 + i, a.N - 1);
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) {
-      const int g = (min(lane + 64 * j, NC - 1) * 32) / a.G;
+    for (int i = 0; i < RPR; ++i) {
+      const size_t n = (size_t)min(row0 + i, a.N - 1);
+      w[i][j] = ld_nt16(a.qw + n * (a.K / 2) + (size_t)c * 16);
       s[i][j] = load_scale_bits<FMT>(a.sc, n * groups + g);
-      if (DUAL) s2[i][j] = load_scale_bits<FMT>(a.sc2, n * groups + g);
+      if (DUAL) {
+        w2[i][j] = ld_nt16(a.qw2 + n * (a.K / 2) + (size_t)c * 16);
+        s2[i][j] = load_scale_bits<FMT>(a.sc2, n * groups + g);
+      }
     }
   }
   if (RES) res = a.residual[min(row0 + (lane & (RPR - 1)), a.N - 1)];
