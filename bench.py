@@ -42,12 +42,17 @@ PROMPT_LEN = 2048
 
 def algorithmic_bytes_per_token(cfg, pos: float, group: int = 128, tp: int = 1) -> float:
     """Weights (all Linears incl. lm_head, int4 + bf16 group scale) + norms + embedding row + KV read/write,
-    per rank (SURVEY §8d formula)."""
+    per rank (SURVEY §8d formula). Sparse MoE blocks count the router and the k routed experts only."""
     C, V, L = cfg.n_embd, cfg.padded_vocab_size, cfg.n_layer
     qkv = (cfg.n_head + 2 * cfg.n_query_groups) * cfg.head_size
-    per_layer = qkv * C + C * C + 3 * cfg.intermediate_size * C
+    mlp = 3 * cfg.intermediate_size * C
+    per_layer = (qkv * C + C * C) / tp
+    if cfg._mlp_class == "LLaMAMoE":
+        per_layer += cfg.n_expert * C + cfg.n_expert_per_token * mlp / tp  # gate replicated, experts sliced
+    else:
+        per_layer += mlp / tp
     bw = 0.5 + 2.0 / group
-    weights = (L * per_layer / tp + V * C) * bw
+    weights = (L * per_layer + V * C) * bw
     norms = (2 * L + 1) * C * 2
     kv = 2 * L * (cfg.n_query_groups / tp) * cfg.head_size * 2 * (pos + 1) + 2 * L * (cfg.n_query_groups / tp) * cfg.head_size * 2
     return weights + norms + C * 2 + kv
@@ -66,20 +71,29 @@ def _dual_gemv_bytes(f1, C: int) -> int:
 def time_dominant_kernel(model, replays: int = 5):
     """Average launch duration of the dominant kernel, measured with HIP events on the stream the launches run on:
     the fused RMSNorm + fc_1/fc_2 + SwiGLU GEMV of every block (32 distinct 46.5 MB weight sets, 1.5 GB, so every
-    launch streams from HBM as in the decode step), captured back to back in one HIP graph and replayed."""
+    launch streams from HBM as in the decode step), captured back to back in one HIP graph and replayed. Sparse
+    MoE blocks: the routed form (two experts, ids 0 and 1) of the same kernel."""
     from lit_gpt import ops
+    from lit_gpt.model import LLaMAMoE
 
     blocks = model.transformer.h
-    f1 = blocks[0].mlp.fc_1
+    moe = isinstance(blocks[0].mlp, LLaMAMoE)
+    f1 = blocks[0].mlp.experts[0].fc_1 if moe else blocks[0].mlp.fc_1
     C = f1.in_features
     x = torch.randn(C, device="cuda").to(torch.bfloat16)
-    out = torch.empty(f1.out_features, dtype=torch.bfloat16, device="cuda")
+    ids = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
+    out = torch.empty(2 if moe else 1, f1.out_features, dtype=torch.bfloat16, device="cuda")
 
     def launch_all():
         for blk in blocks:
+            if moe:
+                (q1, s1), (q2, s2), _ = blk.mlp._stack()
+                ops.q4_gemv_swiglu_experts(x, q1, s1, q2, s2, ids, f1.out_features, C, f1.group, f1.fmt,
+                                           norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps, out=out)
+                continue
             a, b = blk.mlp.fc_1, blk.mlp.fc_2
             ops.q4_gemv_swiglu(x, a.qweight, a.scales, b.qweight, b.scales, a.out_features, C, a.group, a.fmt,
-                               norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps, out=out)
+                               norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps, out=out.view(-1))
 
     launch_all()
     torch.cuda.synchronize()
@@ -96,7 +110,7 @@ def time_dominant_kernel(model, replays: int = 5):
     e.record(stream)
     e.synchronize()
     avg_ms = s.elapsed_time(e) / (replays * len(blocks))
-    return avg_ms, _dual_gemv_bytes(f1, C)
+    return avg_ms, _dual_gemv_bytes(f1, C) * (2 if moe else 1)
 
 
 def pmc_child() -> None:
@@ -211,6 +225,7 @@ def main():
     ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--warmup", type=int, default=14)
     ap.add_argument("--quantize", default="int4-g128")
+    ap.add_argument("--model", default=MODEL, help="lit_gpt Config name (default: the headline Llama-2-7B)")
     ap.add_argument("--prompt_len", type=int, default=PROMPT_LEN)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -222,7 +237,8 @@ def main():
         return pmc_child()
     traffic, traffic_note = None, "skipped"
     under_profiler = any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
-    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_traffic and not under_profiler:
+    headline = args.model == MODEL
+    if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_traffic and not under_profiler and headline:
         traffic, traffic_note = measure_traffic()  # before this process initialises the GPU
 
     import torch.distributed as dist
@@ -235,7 +251,7 @@ def main():
     fabric = gtp.init_distributed()
     world, rank = fabric.world_size, fabric.global_rank
     dev = torch.device("cuda", torch.cuda.current_device())
-    cfg = Config.from_name(MODEL)
+    cfg = Config.from_name(args.model)
     T = args.prompt_len
     max_seq = T + args.warmup + args.steps + 2
     t0 = time.perf_counter()
@@ -302,13 +318,14 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         avg_ms, kbytes = time_dominant_kernel(model)
 
-    cfg_full = Config.from_name(MODEL)
+    cfg_full = Config.from_name(args.model)
     mean_pos = T + args.warmup + 1 + (args.steps - 1) / 2
     step_bytes = algorithmic_bytes_per_token(cfg_full, mean_pos, tp=world)
     step_gbs = step_bytes * tok_s / 1e9
     kern_gbs = kbytes / (avg_ms * 1e-3) / 1e9
     result = {
-        "metric": "decode tokens/s/GPU (Llama-2-7B int4, seq=2048) + % HBM roofline",
+        "metric": ("decode tokens/s/GPU (Llama-2-7B int4, seq=2048) + % HBM roofline" if headline else
+                   f"decode tokens/s/GPU ({args.model} {args.quantize}, seq={T}) + % HBM roofline"),
         "value": round(tok_s, 2),
         "unit": "tokens/s",
         "n_gpus": world,
@@ -320,12 +337,13 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (random-init N(0,0.02) weights, uniform random prompt ids)",
-        "config": {"workload": "Llama-2-7B single-stream greedy decode after a 2048-token prefill",
+        "config": {"workload": f"{args.model} single-stream greedy decode after a {T}-token prefill",
                    "weights": args.quantize, "prompt_len": T, "decode_positions": [T + args.warmup + 1,
                                                                                    T + args.warmup + args.steps],
                    "global_batch": 1, "seq_len": T, "parallelism": f"tp{world}",
                    "graph": use_graph, **({"graph_note": graph_note} if graph_note else {})},
-        "roofline": {"bound": "hbm", "kernel": DOMINANT,
+        "roofline": {"bound": "hbm", "kernel": DOMINANT if not cfg._mlp_class == "LLaMAMoE" else
+                     "gemv_q4_kernel<.., DUAL> routed (RMSNorm + fc_1/fc_2 of 2 experts + SwiGLU of one block)",
                      "achieved": round(kern_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(kern_gbs / HBM_PEAK_GBS, 4),
                      "traffic": None if traffic is None else int(traffic),
@@ -339,7 +357,7 @@ def main():
             args.steps + args.warmup + 1) / args.steps), 2),
         "load_s": round(load_s, 2),
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
         try:
             result["cpu_baseline"] = cpu_baseline(cfg_full, threads, args.cpu_seconds)

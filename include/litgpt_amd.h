@@ -115,6 +115,29 @@ int lga_decode_layer(const void* h_in, void* h_mid, void* h_out, const void* nor
                      unsigned* counters, unsigned* err, int n_embd, int intermediate, int n_head,
                      int n_query_groups, int head_size, int max_seq, float scale, int n_cu, lga_stream_t stream);
 
+/* -- sparse MoE (LLaMAMoE.forward, lit_gpt/model.py:727-743; Mixtral) ------------------------------------------
+ * lga_moe_route: per token row of router logits [T][n_expert] bf16 -> expert_ids [T][k] int32 and probs [T][k]
+ * bf16 = topk(router, k) with the CPU torch.topk order on ties (model.py:737) and
+ * softmax(dim=1, dtype=float).to(bf16) (model.py:738). n_expert <= 8. */
+int lga_moe_route(const void* logits, int T, int n_expert, int k, int32_t* expert_ids, void* probs,
+                  lga_stream_t stream);
+/* Routed expert GEMVs (the per-expert `expert(x[token_idx])` calls, model.py:741-742, for one token): slot s
+ * (0..n_slots-1) uses expert e = expert_ids[s], whose packed weights / scales start at qweight + e * w_stride
+ * bytes / scales + e * s_stride bytes (experts stacked with a uniform stride). lga_q4_gemv_experts reads
+ * x + s * x_stride and writes y[s][N]; the SwiGLU form (fc_1 / fc_2 of LLaMAMLP, model.py:712-715) shares x and
+ * optionally fuses RMSNorm (norm_2) like lga_q4_gemv_swiglu. */
+int lga_q4_gemv_experts(const void* x, const uint8_t* qweight, const void* scales, const int32_t* expert_ids,
+                        int n_slots, int n_expert, long long w_stride, long long s_stride, int x_stride, void* y,
+                        int N, int K, int group, int fmt, int variant, lga_stream_t stream);
+int lga_q4_gemv_swiglu_experts(const void* x, const uint8_t* qweight1, const void* scales1, const uint8_t* qweight2,
+                               const void* scales2, const int32_t* expert_ids, int n_slots, int n_expert,
+                               long long w_stride, long long s_stride, const void* norm_weight, float norm_eps,
+                               void* y, int N, int K, int group, int fmt, int variant, lga_stream_t stream);
+/* y[t] = residual[t] (optional) + the bf16 sum, in ascending expert order, of bf16(probs[t][s] * expert_out[t][s])
+ * (the `y[token_idx] += probs * expert(...)` loop, model.py:739-742, then Block's residual add model.py:592). */
+int lga_moe_combine(const void* expert_out, const void* probs, const int32_t* expert_ids, const void* residual,
+                    void* y, int T, int k, int C, lga_stream_t stream);
+
 /* -- greedy sampling (generate/base.py:30-47 at temperature 0): lowest index among the maxima; optionally
  *    writes the token (int32) and advances *pos_inout by one (generate/base.py:92) -------------------------- */
 int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,

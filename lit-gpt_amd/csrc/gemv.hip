@@ -62,10 +62,26 @@ struct GemvArgs {
   uint16_t* y;               // [N]
   int N, K, G;
   float eps;
+  // sparse-MoE expert routing (lga_q4_gemv*_experts): grid.y = slots; slot s computes with the weights of expert
+  // eidx[s] (qw/qw2 + e * ew bytes, sc/sc2 + e * es bytes), reads x + s * xs and writes y + s * N
+  const int32_t* eidx;
+  long long ew, es;
+  int xs, n_expert, slots;
 };
 
 template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES>
 __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
+  if (a.eidx) {  // wave-uniform: one scalar load of the routed expert id, then plain pointer offsets
+    const long long e = min(max(a.eidx[blockIdx.y], 0), a.n_expert - 1);
+    a.qw += e * a.ew;
+    a.sc = (const unsigned char*)a.sc + e * a.es;
+    if (DUAL) {
+      a.qw2 += e * a.ew;
+      a.sc2 = (const unsigned char*)a.sc2 + e * a.es;
+    }
+    a.x += (size_t)blockIdx.y * a.xs;
+    a.y += (size_t)blockIdx.y * a.N;
+  }
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint4* xl = (uint4*)smem;                        // K/8 uint4 (bf16 pairs)
   float* xsum = (float*)(smem + (size_t)a.K * 2);  // K/32 chunk sums
@@ -213,7 +229,7 @@ __global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
 template <int RPR, int CPT, int FMT, bool DUAL>
 static void launch(const GemvArgs& a, hipStream_t stream) {
   const int waves = (a.N + RPR - 1) / RPR;
-  const int blocks = (waves + 3) / 4;
+  const dim3 blocks((waves + 3) / 4, a.eidx ? a.slots : 1);
   const size_t lds = (size_t)a.K * 2 + (a.K / 32) * 4 + 4 * 4 + 16 * 4;
   const bool norm = a.norm_w != nullptr, res = a.residual != nullptr;
   if (DUAL) {
@@ -291,6 +307,43 @@ extern "C" int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const 
   LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv_swiglu: fmt must be 0 or 1");
   lga::GemvArgs a{(const uint16_t*)x, qweight1, scales1, qweight2, scales2, nullptr, nullptr,
                   (const uint16_t*)norm_weight, (uint16_t*)y, N, K, group, norm_eps};
+  const int rc = fmt == 0 ? lga::dispatch<0, true>(a, variant, stream) : lga::dispatch<1, true>(a, variant, stream);
+  if (rc) return rc;
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_q4_gemv_experts(const void* x, const uint8_t* qweight, const void* scales, const int32_t* expert_ids,
+                                   int n_slots, int n_expert, long long w_stride, long long s_stride, int x_stride,
+                                   void* y, int N, int K, int group, int fmt, int variant, hipStream_t stream) {
+  LGA_CHECK_ARG(x && qweight && scales && expert_ids && y, "lga_q4_gemv_experts: null pointer");
+  LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0, "lga_q4_gemv_experts: K must be a positive multiple of 32");
+  LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv_experts: bad group");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv_experts: fmt must be 0 or 1");
+  LGA_CHECK_ARG(n_slots > 0 && n_slots <= 65535 && n_expert > 0 && w_stride >= (long long)N * K / 2 && s_stride > 0 &&
+                    x_stride >= 0, "lga_q4_gemv_experts: bad routing geometry");
+  lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, nullptr, nullptr, nullptr, (uint16_t*)y,
+                  N, K, group, 0.0f, expert_ids, w_stride, s_stride, x_stride, n_expert, n_slots};
+  const int rc = fmt == 0 ? lga::dispatch<0, false>(a, variant, stream) : lga::dispatch<1, false>(a, variant, stream);
+  if (rc) return rc;
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_q4_gemv_swiglu_experts(const void* x, const uint8_t* qweight1, const void* scales1,
+                                          const uint8_t* qweight2, const void* scales2, const int32_t* expert_ids,
+                                          int n_slots, int n_expert, long long w_stride, long long s_stride,
+                                          const void* norm_weight, float norm_eps, void* y, int N, int K, int group,
+                                          int fmt, int variant, hipStream_t stream) {
+  LGA_CHECK_ARG(x && qweight1 && scales1 && qweight2 && scales2 && expert_ids && y,
+                "lga_q4_gemv_swiglu_experts: null pointer");
+  LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0, "lga_q4_gemv_swiglu_experts: K must be a positive multiple of 32");
+  LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv_swiglu_experts: bad group");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv_swiglu_experts: fmt must be 0 or 1");
+  LGA_CHECK_ARG(n_slots > 0 && n_slots <= 65535 && n_expert > 0 && w_stride >= (long long)N * K / 2 && s_stride > 0,
+                "lga_q4_gemv_swiglu_experts: bad routing geometry");
+  LGA_CHECK_ARG(!norm_weight || K / 32 <= 128, "lga_q4_gemv_swiglu_experts: fused RMSNorm needs K <= 4096");
+  lga::GemvArgs a{(const uint16_t*)x, qweight1, scales1, qweight2, scales2, nullptr, nullptr,
+                  (const uint16_t*)norm_weight, (uint16_t*)y, N, K, group, norm_eps, expert_ids, w_stride, s_stride, 0,
+                  n_expert, n_slots};
   const int rc = fmt == 0 ? lga::dispatch<0, true>(a, variant, stream) : lga::dispatch<1, true>(a, variant, stream);
   if (rc) return rc;
   LGA_LAUNCH_RETURN();

@@ -1,0 +1,163 @@
+// Sparse-MoE routing and combine for LLaMAMoE (Mixtral), lit_gpt/model.py:727-743:
+//   router = gate(x); probs, indices = topk(router, k); probs = softmax(probs, fp32).to(bf16)
+//   y = 0; for expert e ascending: y[tok] += probs[tok, slot] * expert_e(x[tok])      (bf16 arithmetic)
+// The expert GEMVs themselves are lga_q4_gemv(_swiglu)_experts (gemv.hip): slot s of a token streams the weights of
+// expert ids[s] only, so a decode step reads k of the E experts and never leaves the device (no host-side
+// torch.where as in the reference loop; the step stays inside one HIP graph).
+#include "common.h"
+
+namespace lga {
+
+// ATen's CPU topk comparator for largest=True (aten/src/ATen/native/cpu/SortingKernel.cpp): NaN ranks first
+struct KV {
+  float v;
+  int i;
+};
+__device__ __forceinline__ bool before(const KV& a, const KV& b) {
+  return (a.v != a.v && !(b.v != b.v)) || (a.v > b.v);
+}
+__device__ __forceinline__ void swp(KV* q, int a, int b) {
+  const KV t = q[a];
+  q[a] = q[b];
+  q[b] = t;
+}
+
+// Tie order of torch.topk on the CPU = libstdc++ std::nth_element(begin, begin + k - 1, end) (introselect:
+// median-of-3 pivot moved to the front, unguarded Hoare partition while the range is longer than 3, then
+// insertion sort) followed by std::sort(begin, begin + k - 1) (insertion sort below 17 elements). For n <= 8 the
+// introselect depth limit 2*floor(log2 n) is never reached, so the heap-select fallback is not needed.
+// Mirrors the restatement checked against torch.topk in tests/test_host_logic.py.
+template <int NMAX>
+__device__ void topk_order(KV* q, int n, int k) {
+  int first = 0, last = n;
+  const int nth = k - 1;
+  while (last - first > 3) {
+    const int mid = first + (last - first) / 2;
+    const int a = first + 1, b = mid, c = last - 1;
+    int s;
+    if (before(q[a], q[b])) s = before(q[b], q[c]) ? b : (before(q[a], q[c]) ? c : a);
+    else s = before(q[a], q[c]) ? a : (before(q[b], q[c]) ? c : b);
+    swp(q, first, s);
+    int lo = first + 1, hi = last;
+    while (true) {
+      while (before(q[lo], q[first])) ++lo;
+      --hi;
+      while (before(q[first], q[hi])) --hi;
+      if (!(lo < hi)) break;
+      swp(q, lo, hi);
+      ++lo;
+    }
+    if (lo <= nth) first = lo;
+    else last = lo;
+  }
+  auto insertion = [&](int f, int l) {
+    for (int i = f + 1; i < l; ++i) {
+      const KV v = q[i];
+      if (before(v, q[f])) {
+        for (int j = i; j > f; --j) q[j] = q[j - 1];
+        q[f] = v;
+      } else {
+        int j = i;
+        while (before(v, q[j - 1])) {
+          q[j] = q[j - 1];
+          --j;
+        }
+        q[j] = v;
+      }
+    }
+  };
+  insertion(first, last);
+  insertion(0, k - 1);
+}
+
+// one thread per token row: top-k of E router logits, fp32 softmax over the k values (ATen's lastdim softmax:
+// exp(v - max), sum, multiply by the reciprocal), bf16 probabilities
+__global__ void moe_route_kernel(const uint16_t* __restrict__ logits, int T, int E, int k, int32_t* __restrict__ ids,
+                                 uint16_t* __restrict__ probs) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  KV q[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] = {i < E ? bf2f(logits[(size_t)t * E + i]) : -INFINITY, i};
+  topk_order<8>(q, E, k);
+  float mx = q[0].v;
+  for (int s = 1; s < k; ++s) mx = fmaxf(mx, q[s].v);
+  float e[8], sum = 0.0f;
+  for (int s = 0; s < k; ++s) {
+    e[s] = expf(q[s].v - mx);
+    sum += e[s];
+  }
+  const float r = 1.0f / sum;
+  for (int s = 0; s < k; ++s) {
+    ids[(size_t)t * k + s] = q[s].i;
+    probs[(size_t)t * k + s] = f2bf(e[s] * r);
+  }
+}
+
+// y[t] = residual[t] + sum over slots in ascending expert order of bf16(p * E_slot[t]), each add rounded to bf16
+// (the reference's `y[token_idx] += probs * expert(x)` loop); 8 channels per thread
+__global__ void moe_combine_kernel(const uint16_t* __restrict__ eout, const uint16_t* __restrict__ probs,
+                                   const int32_t* __restrict__ ids, const uint16_t* __restrict__ residual,
+                                   uint16_t* __restrict__ y, int k, int C) {
+  const int t = blockIdx.y;
+  const int c8 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c8 * 8 >= C) return;
+  int order[8];
+  for (int s = 0; s < k; ++s) order[s] = s;
+  for (int i = 1; i < k; ++i) {  // stable by expert id
+    const int v = order[i];
+    int j = i;
+    while (j > 0 && ids[(size_t)t * k + order[j - 1]] > ids[(size_t)t * k + v]) {
+      order[j] = order[j - 1];
+      --j;
+    }
+    order[j] = v;
+  }
+  float acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = 0.0f;
+  for (int j = 0; j < k; ++j) {
+    const int s = order[j];
+    const float p = bf2f(probs[(size_t)t * k + s]);
+    const uint4 ev = *(const uint4*)(eout + ((size_t)t * k + s) * C + c8 * 8);
+    const uint32_t d[4] = {ev.x, ev.y, ev.z, ev.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc[2 * q] = round_bf(acc[2 * q] + round_bf(p * bflo(d[q])));
+      acc[2 * q + 1] = round_bf(acc[2 * q + 1] + round_bf(p * bfhi(d[q])));
+    }
+  }
+  if (residual) {
+    const uint4 rv = *(const uint4*)(residual + (size_t)t * C + c8 * 8);
+    const uint32_t d[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc[2 * q] = bflo(d[q]) + acc[2 * q];
+      acc[2 * q + 1] = bfhi(d[q]) + acc[2 * q + 1];
+    }
+  }
+  *(uint4*)(y + (size_t)t * C + c8 * 8) =
+      make_uint4(pack2(acc[0], acc[1]), pack2(acc[2], acc[3]), pack2(acc[4], acc[5]), pack2(acc[6], acc[7]));
+}
+
+}  // namespace lga
+
+extern "C" int lga_moe_route(const void* logits, int T, int n_expert, int k, int32_t* expert_ids, void* probs,
+                             hipStream_t stream) {
+  LGA_CHECK_ARG(logits && expert_ids && probs, "lga_moe_route: null pointer");
+  LGA_CHECK_ARG(T > 0 && n_expert > 0 && n_expert <= 8 && k > 0 && k <= n_expert,
+                "lga_moe_route: needs 1 <= k <= n_expert <= 8");
+  lga::moe_route_kernel<<<(T + 63) / 64, 64, 0, stream>>>((const uint16_t*)logits, T, n_expert, k, expert_ids,
+                                                          (uint16_t*)probs);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_moe_combine(const void* expert_out, const void* probs, const int32_t* expert_ids,
+                               const void* residual, void* y, int T, int k, int C, hipStream_t stream) {
+  LGA_CHECK_ARG(expert_out && probs && expert_ids && y, "lga_moe_combine: null pointer");
+  LGA_CHECK_ARG(T > 0 && T <= 65535 && k > 0 && k <= 8 && C > 0 && C % 8 == 0, "lga_moe_combine: bad geometry");
+  const dim3 grid((C / 8 + 255) / 256, T);
+  lga::moe_combine_kernel<<<grid, 256, 0, stream>>>((const uint16_t*)expert_out, (const uint16_t*)probs, expert_ids,
+                                                    (const uint16_t*)residual, (uint16_t*)y, k, C);
+  LGA_LAUNCH_RETURN();
+}

@@ -162,7 +162,7 @@ class Block(nn.Module):
                                           " (non-parallel residual and shared attention norm).")
             raise NotImplementedError("parallel-residual (GPT-NeoX) blocks have no MI355X kernels in this build; "
                                       "config 1 (pythia) runs on the CPU oracle")
-        if not isinstance(self.norm_1, RMSNorm) or not isinstance(self.mlp, LLaMAMLP):
+        if not isinstance(self.norm_1, RMSNorm) or not isinstance(self.mlp, (LLaMAMLP, LLaMAMoE)):
             raise NotImplementedError(f"{type(self.mlp).__name__} / {type(self.norm_1).__name__} blocks have no "
                                       "MI355X kernels in this build")
         # decode token on a single GPU: the whole block is one persistent launch when the geometry allows
@@ -193,6 +193,9 @@ class Block(nn.Module):
             from lit_gpt.quantize import QuantLinear
 
             c = self.config
+            if not isinstance(self.mlp, LLaMAMLP):
+                self._layer_kernel = False
+                return False
             lins = (self.attn.attn, self.attn.proj, self.mlp.fc_1, self.mlp.fc_2, self.mlp.proj)
             self._layer_kernel = (
                 os.environ.get("LGA_DECODE_LAYER", "0") == "1" and x.is_cuda
@@ -365,16 +368,90 @@ class LLaMAMLP(nn.Module):
 
 
 class LLaMAMoE(nn.Module):
-    """Kept for the API / TP isinstance checks (model.py:719-743); the MoE kernels are a later milestone."""
+    """Sparse MoE (lit_gpt/model.py:719-743): router gate, top-k experts per token, prob-weighted bf16 sum.
+
+    Decode (one token) never leaves the device: ``lga_moe_route`` picks the experts, the routed GEMVs stream
+    only the k selected experts' weights (``lga_q4_gemv_swiglu_experts`` with the fused norm_2, then
+    ``lga_q4_gemv_experts``), ``lga_moe_combine`` adds them in ascending expert order plus the Block residual.
+    Prefill (T > 1) groups tokens per expert on the host (the reference's ``torch.where`` loop) and runs each
+    group through the MFMA GEMM. Forward hooks registered on the experts (``generate/tp.py`` registers the TP
+    all-reduce on each expert, tp.py:58-62) are applied to the stacked (T, k, C) expert outputs: a per-element
+    sum over ranks, identical to reducing every expert call separately.
+    """
 
     def __init__(self, config: Config) -> None:
         super().__init__()
         self.gate = nn.Linear(config.n_embd, config.n_expert, bias=False)
         self.experts = nn.ModuleList(LLaMAMLP(config) for _ in range(config.n_expert))
         self.config = config
+        self._stacks = None
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        raise NotImplementedError("LLaMAMoE has no MI355X kernels in this build yet")
+    def _stack(self):
+        """Stack the experts' packed weights per Linear ((E, N, K/2) / (E, N, K/group)) and re-point every
+        expert's buffers at its slice, so the routed GEMVs index experts with one stride (done once)."""
+        from lit_gpt.quantize import QuantLinear
+
+        if self._stacks is not None and self._stacks[0][0].data_ptr() == self.experts[0].fc_1.qweight.data_ptr():
+            return self._stacks
+        out = []
+        for name in ("fc_1", "fc_2", "proj"):
+            lins = [getattr(e, name) for e in self.experts]
+            l0 = lins[0]
+            if not all(isinstance(l, QuantLinear) and l.bias is None and (l.fmt, l.group, l.qweight.shape) ==
+                       (l0.fmt, l0.group, l0.qweight.shape) for l in lins):
+                raise NotImplementedError("LLaMAMoE on the MI355X needs bias-free QuantLinear experts of one format")
+            qw = torch.stack([l.qweight for l in lins])
+            sc = torch.stack([l.scales for l in lins])
+            for i, l in enumerate(lins):
+                l.qweight, l.scales = qw[i], sc[i]
+            out.append((qw, sc))
+        self._stacks = out
+        return out
+
+    def _expert_hooks(self, x: torch.Tensor, eout: torch.Tensor) -> torch.Tensor:
+        hooks = [list(e._forward_hooks.values()) for e in self.experts]
+        if any(len(h) != len(hooks[0]) for h in hooks):
+            raise NotImplementedError("LLaMAMoE: experts carry different forward hooks")
+        for hook in hooks[0]:
+            r = hook(self.experts[0], (x,), eout)
+            eout = eout if r is None else r
+        return eout
+
+    def forward(self, x: torch.Tensor, *, norm: Optional["RMSNorm"] = None,
+                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        c = self.config
+        lead, C = x.shape[:-1], x.shape[-1]
+        x2 = x.reshape(-1, C).contiguous()
+        T, k, E = x2.size(0), c.n_expert_per_token, c.n_expert
+        (q1, s1), (q2, s2), (qp, sp) = self._stack()
+        f1, pj = self.experts[0].fc_1, self.experts[0].proj
+        res = None if residual is None else residual.reshape(T, C).contiguous()
+        if T == 1:
+            fuse_norm = norm is not None and ops.gemv_fuses_norm(C, dual=True)
+            xin = x2 if (norm is None or fuse_norm) else norm(x2)
+            nw = norm.weight if fuse_norm else None
+            eps = norm.eps if fuse_norm else 1e-5
+            router = _lin(self.gate, xin, norm_weight=nw, norm_eps=eps).view(1, E)
+            ids, probs = ops.moe_route(router, k)
+            act = ops.q4_gemv_swiglu_experts(xin.view(-1), q1, s1, q2, s2, ids.view(-1), f1.out_features, C,
+                                             f1.group, f1.fmt, norm_weight=nw, eps=eps)
+            eout = ops.q4_gemv_experts(act, qp, sp, ids.view(-1), pj.out_features, pj.in_features, pj.group,
+                                       pj.fmt).view(1, k, C)
+        else:
+            n = x2 if norm is None else norm(x2)
+            router = _lin(self.gate, n)
+            ids, probs = ops.moe_route(router.contiguous(), k)
+            eout = torch.empty(T, k, C, dtype=torch.bfloat16, device=x2.device)
+            for e in range(E):  # the reference's per-expert token groups (model.py:740-742)
+                tok, slot = torch.where(ids == e)
+                if tok.numel() == 0:
+                    continue
+                xe = n.index_select(0, tok)
+                ex = self.experts[e]
+                g = ops.swiglu(_lin(ex.fc_1, xe).contiguous(), _lin(ex.fc_2, xe).contiguous())
+                eout[tok, slot] = _lin(ex.proj, g)
+        eout = self._expert_hooks(x2, eout)
+        return ops.moe_combine(eout.contiguous(), probs, ids, residual=res).view(*lead, C)
 
 
 LayerNorm = nn.LayerNorm  # config.norm_class for GPT-NeoX (reference config.py:137-144)

@@ -50,6 +50,12 @@ SIGNATURES = {
     "lga_decode_layer_counters": [_I],
     "lga_attention_decode_fused": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_argmax": [_P, _I, _P, _P, _P, _P],
+    "lga_moe_route": [_P, _I, _I, _I, _P, _P, _P],
+    "lga_q4_gemv_experts": [_P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _I, _P, _I, _I, _I, _I,
+                            _I, _P],
+    "lga_q4_gemv_swiglu_experts": [_P, _P, _P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _F,
+                                   _P, _I, _I, _I, _I, _I, _P],
+    "lga_moe_combine": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
 }
 _RESTYPES = {"lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
              "lga_decode_layer_counters": ctypes.c_size_t}
@@ -343,6 +349,63 @@ def argmax(logits, out_idx=None, token_out=None, pos_inout=None):
                                      _opt(token_out, "token_out", torch.int32),
                                      _opt(pos_inout, "pos_inout", torch.int64), _stream()))
     return idx
+
+
+# ------------------------------------------------------------------------------------------------ sparse MoE
+def moe_route(logits, k, ids=None, probs=None):
+    """(T, E) bf16 router logits -> (ids (T, k) int32, probs (T, k) bf16): torch.topk (CPU tie order) + fp32
+    softmax over the k values, cast to bf16 (lit_gpt/model.py:737-738)."""
+    T, E = logits.shape
+    ids = ids if ids is not None else torch.empty(T, k, dtype=torch.int32, device=logits.device)
+    probs = probs if probs is not None else torch.empty(T, k, dtype=torch.bfloat16, device=logits.device)
+    _check(load_library().lga_moe_route(_dev(logits, "logits", torch.bfloat16), T, E, k, _dev(ids, "ids", torch.int32),
+                                        _dev(probs, "probs", torch.bfloat16), _stream()))
+    return ids, probs
+
+
+def _expert_strides(qweight, scales):
+    if qweight.dim() != 3 or scales.dim() != 3:
+        raise ValueError("expert weights must be stacked as (E, N, K/2) / (E, N, K/group)")
+    return qweight.stride(0) * qweight.element_size(), scales.stride(0) * scales.element_size()
+
+
+def q4_gemv_experts(x, qweight, scales, ids, N, K, group, fmt, *, out=None, variant=-1):
+    """y (k, N): slot s = x[s] (k, K) . dequant(W[ids[s]])^T with W stacked (E, N, K/2)."""
+    k = ids.numel()
+    ws, ss = _expert_strides(qweight, scales)
+    y = out if out is not None else torch.empty(k, N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_q4_gemv_experts(_dev(x, "x", torch.bfloat16), _dev(qweight, "qweight", torch.uint8),
+                                              _dev(scales, "scales"), _dev(ids, "ids", torch.int32), k,
+                                              qweight.size(0), ws, ss, K, _dev(y, "y", torch.bfloat16), N, K, group,
+                                              fmt, variant, _stream()))
+    return y
+
+
+def q4_gemv_swiglu_experts(x, qw1, sc1, qw2, sc2, ids, N, K, group, fmt, *, norm_weight=None, eps=1e-5, out=None,
+                           variant=-1):
+    """y (k, N): slot s = bf16(silu(bf16(x W1[ids[s]]^T))) * bf16(x W2[ids[s]]^T), optional fused RMSNorm of x."""
+    k = ids.numel()
+    ws, ss = _expert_strides(qw1, sc1)
+    if _expert_strides(qw2, sc2) != (ws, ss):
+        raise ValueError("fc_1 and fc_2 expert stacks must share one stride")
+    y = out if out is not None else torch.empty(k, N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_q4_gemv_swiglu_experts(
+        _dev(x, "x", torch.bfloat16), _dev(qw1, "qw1", torch.uint8), _dev(sc1, "sc1"), _dev(qw2, "qw2", torch.uint8),
+        _dev(sc2, "sc2"), _dev(ids, "ids", torch.int32), k, qw1.size(0), ws, ss,
+        _opt(norm_weight, "norm_weight", torch.bfloat16), float(eps), _dev(y, "y", torch.bfloat16), N, K, group, fmt,
+        variant, _stream()))
+    return y
+
+
+def moe_combine(expert_out, probs, ids, residual=None, out=None):
+    """(T, k, C) expert outputs -> (T, C): [residual +] sum over slots in ascending expert id of bf16(p * E)."""
+    T, k, C = expert_out.shape
+    y = out if out is not None else torch.empty(T, C, dtype=torch.bfloat16, device=expert_out.device)
+    _check(load_library().lga_moe_combine(_dev(expert_out, "expert_out", torch.bfloat16),
+                                          _dev(probs, "probs", torch.bfloat16), _dev(ids, "ids", torch.int32),
+                                          _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16),
+                                          T, k, C, _stream()))
+    return y
 
 
 def gemv_fuses_norm(K: int, dual: bool) -> bool:

@@ -52,6 +52,62 @@ def layer_norm(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float) ->
     return F.layer_norm(x, (x.size(-1),), w, b, eps)
 
 
+def topk_order(values: List[float], k: int) -> List[int]:
+    """Indices of ``torch.topk(values, k)`` on the CPU (lit_gpt/model.py:737, the MoE router) including its tie
+    order, restated: ATen's CPU topk (k * 64 > n) runs libstdc++ std::nth_element(begin, begin + k - 1, end)
+    with the comparator "NaN first, then >" followed by std::sort(begin, begin + k - 1). nth_element is
+    introselect: median-of-3 pivot moved to the front, unguarded Hoare partition while the range is longer than
+    3, then insertion sort; for n <= 8 its depth limit is never reached. This is the specification of
+    lga_moe_route (csrc/moe.hip); tests/test_host_logic.py checks it against torch.topk on tie-heavy inputs."""
+    def gt(a, b):
+        return (math.isnan(a[0]) and not math.isnan(b[0])) or (a[0] > b[0])
+
+    def insertion(q, f, l):
+        for i in range(f + 1, l):
+            v = q[i]
+            if gt(v, q[f]):
+                q[f + 1:i + 1] = q[f:i]
+                q[f] = v
+            else:
+                j = i
+                while gt(v, q[j - 1]):
+                    q[j] = q[j - 1]
+                    j -= 1
+                q[j] = v
+
+    q = [(float(v), i) for i, v in enumerate(values)]
+    n = len(q)
+    if n > 8 or not 1 <= k <= n:
+        raise ValueError("topk_order restates the n <= 8 case")
+    first, last, nth = 0, n, k - 1
+    while last - first > 3:
+        mid = first + (last - first) // 2
+        a, b, c = first + 1, mid, last - 1
+        if gt(q[a], q[b]):
+            s = b if gt(q[b], q[c]) else (c if gt(q[a], q[c]) else a)
+        else:
+            s = a if gt(q[a], q[c]) else (c if gt(q[b], q[c]) else b)
+        q[first], q[s] = q[s], q[first]
+        lo, hi = first + 1, last
+        while True:
+            while gt(q[lo], q[first]):
+                lo += 1
+            hi -= 1
+            while gt(q[first], q[hi]):
+                hi -= 1
+            if not lo < hi:
+                break
+            q[lo], q[hi] = q[hi], q[lo]
+            lo += 1
+        if lo <= nth:
+            first = lo
+        else:
+            last = lo
+    insertion(q, first, last)
+    insertion(q, 0, k - 1)
+    return [i for _, i in q[:k]]
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
     return F.linear(x, w, b)
 

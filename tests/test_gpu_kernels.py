@@ -348,3 +348,74 @@ def test_errors_are_raised(ops):
         ops.q4_gemv(x, qw, sc, 10, 100, 100, 0)
     with pytest.raises(RuntimeError, match="GPU tensor"):
         ops.rmsnorm(torch.zeros(4, 8, dtype=torch.bfloat16), torch.ones(8, dtype=torch.bfloat16), 1e-5)
+
+
+# ------------------------------------------------------------------------------------------------ sparse MoE
+def test_moe_route_matches_cpu_topk_on_ties(ops):
+    """lga_moe_route == torch.topk on the CPU (the reference's tie order, model.py:737) + fp32 softmax cast to
+    bf16 (model.py:738): ids bit-exact; probs bit-exact except a 1-ulp fp32 exp difference may move a bf16
+    rounding (checked: <= 1 bf16 ulp)."""
+    g = torch.Generator().manual_seed(3)
+    rows = []
+    for E in (8, 4, 6):
+        pools = [torch.tensor([0.0, 1.0, 2.0]), torch.tensor([0.0, -0.0, 1.0, 1.5]), torch.arange(5.0), None]
+        for pool in pools:
+            if pool is None:
+                v = torch.randn(400, E, generator=g)
+            else:
+                v = pool[torch.randint(0, pool.numel(), (400, E), generator=g)]
+            rows.append((E, v.bfloat16()))
+    for E, logits in rows:
+        for k in (1, 2, 3):
+            ids, probs = ops.moe_route(logits.to(DEV), k)
+            pv, pi = torch.topk(logits, k)
+            ref_p = pv.softmax(dim=1, dtype=torch.float).to(torch.bfloat16)
+            assert torch.equal(ids.cpu().long(), pi), (E, k)
+            d = (probs.cpu().view(torch.int16).int() - ref_p.view(torch.int16).int()).abs()
+            assert int(d.max()) <= 1, (E, k)
+
+
+def test_moe_combine_matches_reference_loop(ops):
+    """y[tok] += probs * expert_out in ascending expert order, bf16 arithmetic (model.py:739-742) + residual."""
+    T, k, C = 9, 2, 4096
+    g = torch.Generator().manual_seed(5)
+    eout = torch.randn(T, k, C, generator=g).bfloat16()
+    probs = torch.rand(T, k, generator=g).bfloat16()
+    ids = torch.stack([torch.randperm(8, generator=g)[:k] for _ in range(T)]).int()
+    res = torch.randn(T, C, generator=g).bfloat16()
+    got = ops.moe_combine(eout.to(DEV), probs.to(DEV), ids.to(DEV), residual=res.to(DEV)).cpu()
+    y = torch.zeros(T, C, dtype=torch.bfloat16)
+    for e in range(8):
+        tok, slot = torch.where(ids == e)
+        y[tok] += probs[tok, slot, None] * eout[tok, slot]
+    assert torch.equal(got, res + y)
+    got_nores = ops.moe_combine(eout.to(DEV), probs.to(DEV), ids.to(DEV)).cpu()
+    assert torch.equal(got_nores, y)
+
+
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
+def test_routed_expert_gemvs_equal_per_expert_gemvs(ops, fmt, group):
+    """Slot s of the routed GEMVs == the plain GEMV on expert ids[s]'s own weights (same kernel, bit-exact)."""
+    E, N, K = 4, 1408, 512
+    ws = [_weights(N, K, f"e{e}") for e in range(E)]
+    qs = [ops.quantize(torch.from_numpy(w).to(DEV), fmt, group) for w in ws]
+    qw = torch.stack([q for q, _ in qs])
+    sc = torch.stack([s for _, s in qs])
+    ws2 = [_weights(N, K, f"f{e}") for e in range(E)]
+    qs2 = [ops.quantize(torch.from_numpy(w).to(DEV), fmt, group) for w in ws2]
+    qw2 = torch.stack([q for q, _ in qs2])
+    sc2 = torch.stack([s for _, s in qs2])
+    ids = torch.tensor([3, 1], dtype=torch.int32, device=DEV)
+    x = to_dev_bf16(synth.normal((K,), "xe", 5, 1.0))
+    nw = to_dev_bf16(1.0 + 0.1 * synth.normal((K,), "nwe", 5, 1.0))
+    act = ops.q4_gemv_swiglu_experts(x, qw, sc, qw2, sc2, ids, N, K, group, fmt, norm_weight=nw)
+    for s, e in enumerate((3, 1)):
+        ref = ops.q4_gemv_swiglu(x, qs[e][0], qs[e][1], qs2[e][0], qs2[e][1], N, K, group, fmt, norm_weight=nw)
+        assert torch.equal(act[s], ref)
+    # down projection: (K' = N) -> N' = K, each slot reading its own activation row
+    wd = [_weights(K, N, f"d{e}") for e in range(E)]
+    qd = [ops.quantize(torch.from_numpy(w).to(DEV), fmt, group) for w in wd]
+    out = ops.q4_gemv_experts(act, torch.stack([q for q, _ in qd]), torch.stack([s for _, s in qd]), ids, K, N,
+                              group, fmt)
+    for s, e in enumerate((3, 1)):
+        assert torch.equal(out[s], ops.q4_gemv(act[s].contiguous(), qd[e][0], qd[e][1], K, N, group, fmt))

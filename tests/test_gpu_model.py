@@ -25,6 +25,8 @@ CFGS = {
                                    vocab_size=1000, padding_multiple=64, block_size=256)),
     "hs64": ("Llama-2-7b-hf", dict(n_layer=2, n_embd=256, n_head=4, intermediate_size=640, vocab_size=1000,
                                     padding_multiple=64, block_size=256, rope_base=1000000)),
+    "moe": ("Mixtral-8x7B-v0.1", dict(n_layer=2, n_embd=512, n_head=4, n_query_groups=2, intermediate_size=384,
+                                       vocab_size=1000, padding_multiple=64, block_size=256)),
 }
 
 
@@ -60,6 +62,30 @@ def oracle_for(cfg, sd, mode):
     return om.OracleGPT(cfg, sd, dtype=torch.bfloat16, weight_override=deq)
 
 
+def _watch_router_margins(ref):
+    """Record, per oracle MoE router call, the gap between the k-th and (k+1)-th largest logit of every token."""
+    seen = []
+    orig = ref._lin
+
+    def lin(name, x, *a, **kw):
+        y = orig(name, x, *a, **kw)
+        if name.endswith("mlp.gate"):
+            v = torch.sort(y.float(), dim=-1, descending=True).values
+            k = ref.cfg.n_expert_per_token
+            seen.append(float((v[:, k - 1] - v[:, k]).min()))
+        return y
+
+    ref._lin = lin
+    return seen
+
+
+def _routing_ambiguous(margins, tol=2 ** -6):
+    """True when a router decision of the step just run was within ~2 bf16 ulps of flipping (then clear)."""
+    amb = any(m <= tol for m in margins)
+    margins.clear()
+    return amb
+
+
 @pytest.mark.parametrize("key", list(CFGS))
 @pytest.mark.parametrize("mode", ["int4-g128", "nf4"])
 @torch.inference_mode()
@@ -72,12 +98,18 @@ def test_teacher_forced_logits_match_oracle(key, mode):
     ref.set_kv_cache(T + N)
     prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=21))
     stream = torch.from_numpy(synth.token_ids(N, cfg.vocab_size, seed=22))  # forced continuation
+    margins = _watch_router_margins(ref)
     got = [model(prompt.view(1, -1).to(DEV), torch.arange(T, device=DEV))[0, -1].float().cpu()]
     exp = [ref.forward(prompt, torch.arange(T))[-1].float()]
+    ambiguous = [_routing_ambiguous(margins)]
     for i in range(N - 1):
         got.append(model(stream[i:i + 1].view(1, 1).to(DEV), torch.tensor([T + i], device=DEV))[0, -1].float().cpu())
         exp.append(ref.forward(stream[i:i + 1], torch.tensor([T + i]))[-1].float())
-    for g, e in zip(got, exp):
+        ambiguous.append(_routing_ambiguous(margins))
+    assert sum(ambiguous) <= N // 2, ambiguous
+    for g, e, amb in zip(got, exp, ambiguous):
+        if amb:  # a router near-tie the two sides may break differently: a different expert, not an error
+            continue
         err = (g - e).abs().max().item()
         assert err <= 0.04 * e.abs().max().item(), (err, e.abs().max().item())
         top2 = torch.topk(e, 2).values
@@ -85,7 +117,7 @@ def test_teacher_forced_logits_match_oracle(key, mode):
             assert int(torch.argmax(g)) == int(torch.argmax(e))
 
 
-@pytest.mark.parametrize("key", ["mha", "gqa"])
+@pytest.mark.parametrize("key", ["mha", "gqa", "moe"])
 @torch.inference_mode()
 def test_greedy_generate_graph_equals_eager_and_oracle(key):
     from generate.base import generate
@@ -105,9 +137,12 @@ def test_greedy_generate_graph_equals_eager_and_oracle(key):
     # oracle's top-2 margin is within the logit tolerance
     ref = oracle_for(cfg, sd, "int4-g128")
     ref.set_kv_cache(T + N)
+    margins = _watch_router_margins(ref)
     lg = ref.forward(prompt.cpu(), torch.arange(T))[-1].float()
     for i in range(N):
         top2 = torch.topk(lg, 2)
+        if _routing_ambiguous(margins):
+            continue
         if float(top2.values[0] - top2.values[1]) > 0.04 * lg.abs().max().item():
             assert int(y_graph[T + i]) == int(top2.indices[0]), f"step {i}"
         if i + 1 < N:
@@ -159,8 +194,8 @@ def test_sample_on_gpu():
     assert sample(logits, temperature=1.0, top_k=1).tolist() == [0]
 
 
-@pytest.mark.parametrize("mode", ["int4-g128", "nf4"])
-def test_tensor_parallel_2_ranks_one_gpu(mode, tmp_path):
+@pytest.mark.parametrize("family,mode", [("llama", "int4-g128"), ("llama", "nf4"), ("moe", "int4-g128")])
+def test_tensor_parallel_2_ranks_one_gpu(family, mode, tmp_path):
     """generate/tp.py sharding + all-reduce hooks + per-shard quantization on the HIP kernels: TP=2 (two ranks
     sharing cuda:0 over gloo) equals the unsharded model within bf16 reordering of the row-parallel sums."""
     import os
@@ -175,12 +210,14 @@ def test_tensor_parallel_2_ranks_one_gpu(mode, tmp_path):
     out = tmp_path / "tp.npz"
     worker = Path(__file__).parent / "workers" / "tp_gpu_worker.py"
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr=127.0.0.1", f"--master-port={port}", str(worker), str(out), mode]
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(worker), str(out), mode, family]
     env = dict(os.environ, OMP_NUM_THREADS="4")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     d = np.load(out)
-    tp, ref = d["tp"], d["ref"]
+    keep = d["gaps"] > 2 ** -6  # MoE: steps whose routing was within ~2 bf16 ulps of a tie may pick other experts
+    assert keep.sum() >= keep.size // 2, d["gaps"]
+    tp, ref = d["tp"][keep], d["ref"][keep]
     scale = np.abs(ref).max()
     # the row-parallel proj/down outputs are rounded to bf16 per rank before the sum: a few bf16 ulps of drift
     assert np.abs(tp - ref).max() <= 0.02 * scale, float(np.abs(tp - ref).max() / scale)

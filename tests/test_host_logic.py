@@ -210,3 +210,19 @@ def test_rope_cache_follows_reference_default_dtype(golden):
         np.testing.assert_array_equal(sin[2040:2050].numpy(), g[f"rope_sin_{tag}"])
     cos, _ = build_rope_cache(64, 16, base=1000000, condense_ratio=2)
     np.testing.assert_array_equal(cos.numpy(), g["rope_small_cos"])
+
+
+def test_topk_order_restatement_matches_cpu_torch_topk():
+    """oracle.model.topk_order (the spec of lga_moe_route) == torch.topk on the CPU, ties included."""
+    import random
+
+    from oracle.model import topk_order
+
+    rng = random.Random(7)
+    for _ in range(4000):
+        n = rng.choice([8, 8, 4, 6, 7, 5, 3, 2])
+        k = rng.randint(1, n)
+        pool = rng.choice([[0.0, 1.0, 2.0], [0.0, -0.0, 1.0, 1.5], [float(x) for x in range(5)], None])
+        vals = [rng.gauss(0, 1) if pool is None else rng.choice(pool) for _ in range(n)]
+        t = torch.tensor(vals, dtype=torch.bfloat16).view(1, -1)
+        assert topk_order(t[0].float().tolist(), k) == torch.topk(t, k).indices[0].tolist(), (vals, k)
