@@ -40,9 +40,10 @@ MODEL = "Llama-2-7b-hf"
 PROMPT_LEN = 2048
 
 
-def algorithmic_bytes_per_token(cfg, pos: float, group: int = 128, tp: int = 1) -> float:
-    """Weights (all Linears incl. lm_head, int4 + bf16 group scale) + norms + embedding row + KV read/write,
-    per rank (SURVEY §8d formula). Sparse MoE blocks count the router and the k routed experts only."""
+def algorithmic_bytes_per_token(cfg, pos: float, group: int = 128, tp: int = 1, dense: bool = False) -> float:
+    """Weights (all Linears incl. lm_head, int4 + bf16 group scale, or bf16 when ``dense``) + norms + embedding
+    row + KV read/write, per rank (SURVEY §8d formula). Sparse MoE blocks count the router and the k routed
+    experts only."""
     C, V, L = cfg.n_embd, cfg.padded_vocab_size, cfg.n_layer
     qkv = (cfg.n_head + 2 * cfg.n_query_groups) * cfg.head_size
     mlp = 3 * cfg.intermediate_size * C
@@ -51,7 +52,7 @@ def algorithmic_bytes_per_token(cfg, pos: float, group: int = 128, tp: int = 1) 
         per_layer += cfg.n_expert * C + cfg.n_expert_per_token * mlp / tp  # gate replicated, experts sliced
     else:
         per_layer += mlp / tp
-    bw = 0.5 + 2.0 / group
+    bw = 2.0 if dense else 0.5 + 2.0 / group
     weights = (L * per_layer + V * C) * bw
     norms = (2 * L + 1) * C * 2
     kv = 2 * L * (cfg.n_query_groups / tp) * cfg.head_size * 2 * (pos + 1) + 2 * L * (cfg.n_query_groups / tp) * cfg.head_size * 2
@@ -80,6 +81,7 @@ def time_dominant_kernel(model, replays: int = 5):
     moe = isinstance(blocks[0].mlp, LLaMAMoE)
     f1 = blocks[0].mlp.experts[0].fc_1 if moe else blocks[0].mlp.fc_1
     C = f1.in_features
+    dense = type(f1) is torch.nn.Linear
     x = torch.randn(C, device="cuda").to(torch.bfloat16)
     ids = torch.tensor([0, 1], dtype=torch.int32, device="cuda")
     out = torch.empty(2 if moe else 1, f1.out_features, dtype=torch.bfloat16, device="cuda")
@@ -92,6 +94,10 @@ def time_dominant_kernel(model, replays: int = 5):
                                            norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps, out=out)
                 continue
             a, b = blk.mlp.fc_1, blk.mlp.fc_2
+            if dense:
+                ops.bf16_gemv_swiglu(x, a.weight, b.weight, norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps,
+                                     out=out.view(-1))
+                continue
             ops.q4_gemv_swiglu(x, a.qweight, a.scales, b.qweight, b.scales, a.out_features, C, a.group, a.fmt,
                                norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps, out=out.view(-1))
 
@@ -110,6 +116,8 @@ def time_dominant_kernel(model, replays: int = 5):
     e.record(stream)
     e.synchronize()
     avg_ms = s.elapsed_time(e) / (replays * len(blocks))
+    if dense:
+        return avg_ms, 2 * f1.weight.numel() * 2 + 2 * C * 2 + f1.out_features * 2
     return avg_ms, _dual_gemv_bytes(f1, C) * (2 if moe else 1)
 
 
@@ -224,7 +232,8 @@ def main():
     # SURVEY §8d (p = 2048 ... 2302)
     ap.add_argument("--steps", type=int, default=240)
     ap.add_argument("--warmup", type=int, default=14)
-    ap.add_argument("--quantize", default="int4-g128")
+    ap.add_argument("--quantize", default="int4-g128",
+                    help="4-bit mode, or 'bf16' for unquantized weights (BASELINE config 2)")
     ap.add_argument("--model", default=MODEL, help="lit_gpt Config name (default: the headline Llama-2-7B)")
     ap.add_argument("--prompt_len", type=int, default=PROMPT_LEN)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -237,7 +246,8 @@ def main():
         return pmc_child()
     traffic, traffic_note = None, "skipped"
     under_profiler = any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
-    headline = args.model == MODEL
+    headline = args.model == MODEL and args.quantize == "int4-g128"
+    dense = args.quantize in ("bf16", "none")
     if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_traffic and not under_profiler and headline:
         traffic, traffic_note = measure_traffic()  # before this process initialises the GPU
 
@@ -257,7 +267,7 @@ def main():
     t0 = time.perf_counter()
     from functools import partial
 
-    model = build_model(cfg, quantize=args.quantize, device=dev, max_seq_length=max_seq,
+    model = build_model(cfg, quantize=None if dense else args.quantize, device=dev, max_seq_length=max_seq,
                         tp=partial(gtp.tensor_parallel, fabric) if world > 1 else None)
     load_s = time.perf_counter() - t0
     g = torch.Generator(device="cpu").manual_seed(1234)
@@ -320,7 +330,7 @@ def main():
 
     cfg_full = Config.from_name(args.model)
     mean_pos = T + args.warmup + 1 + (args.steps - 1) / 2
-    step_bytes = algorithmic_bytes_per_token(cfg_full, mean_pos, tp=world)
+    step_bytes = algorithmic_bytes_per_token(cfg_full, mean_pos, tp=world, dense=dense)
     step_gbs = step_bytes * tok_s / 1e9
     kern_gbs = kbytes / (avg_ms * 1e-3) / 1e9
     result = {
@@ -342,8 +352,10 @@ def main():
                                                                                    T + args.warmup + args.steps],
                    "global_batch": 1, "seq_len": T, "parallelism": f"tp{world}",
                    "graph": use_graph, **({"graph_note": graph_note} if graph_note else {})},
-        "roofline": {"bound": "hbm", "kernel": DOMINANT if not cfg._mlp_class == "LLaMAMoE" else
-                     "gemv_q4_kernel<.., DUAL> routed (RMSNorm + fc_1/fc_2 of 2 experts + SwiGLU of one block)",
+        "roofline": {"bound": "hbm", "kernel": (
+                     "gemv_bf16_kernel<.., DUAL> (RMSNorm + fc_1/fc_2 bf16 GEMV + SwiGLU of one block)" if dense else
+                     DOMINANT if not cfg._mlp_class == "LLaMAMoE" else
+                     "gemv_q4_kernel<.., DUAL> routed (RMSNorm + fc_1/fc_2 of 2 experts + SwiGLU of one block)"),
                      "achieved": round(kern_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(kern_gbs / HBM_PEAK_GBS, 4),
                      "traffic": None if traffic is None else int(traffic),

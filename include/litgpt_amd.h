@@ -57,6 +57,18 @@ int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const void* scale
 int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const void* bias, const void* residual,
                 void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
 
+/* -- unquantized bf16 Linears (BASELINE config 2: no --quantize, precision bf16-true; the reference runs
+ *    F.linear on the bf16 nn.Linear weight, lit_gpt/model.py:619, :656, :712-716, :519) ------------------- */
+/* decode GEMV y (N) = x (K) . W (N, K)^T [+bias] [+residual]; optional fused RMSNorm of x (as lga_q4_gemv) */
+int lga_bf16_gemv(const void* x, const void* weight, const void* bias, const void* residual, const void* norm_weight,
+                  float norm_eps, void* y, int N, int K, lga_stream_t stream);
+/* y = bf16(silu(bf16(x W1^T))) * bf16(x W2^T) (LLaMAMLP, model.py:715), optional fused RMSNorm of x */
+int lga_bf16_gemv_swiglu(const void* x, const void* weight1, const void* weight2, const void* norm_weight,
+                         float norm_eps, void* y, int N, int K, lga_stream_t stream);
+/* prefill GEMM Y (M, N) = X (M, K) . W (N, K)^T [+bias] [+residual] on MFMA; K % 32 == 0 */
+int lga_bf16_gemm(const void* x, const void* weight, const void* bias, const void* residual, void* y, int M, int N,
+                  int K, lga_stream_t stream);
+
 /* -- row / elementwise ops ---------------------------------------------------------------------------- */
 /* RMSNorm over rows of n (lit_gpt/rmsnorm.py:19-25) */
 int lga_rmsnorm(const void* x, const void* weight, void* y, int rows, int n, float eps, lga_stream_t stream);

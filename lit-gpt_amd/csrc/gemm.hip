@@ -47,13 +47,13 @@ __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int nk = (a.K + BK - 1) / BK, groups = a.K / a.G;
+  const int nk = (a.K + BK - 1) / BK, groups = FMT == 2 ? 1 : a.K / a.G;
   const size_t wrow_bytes = (size_t)a.K / 2;
-  if (tid < 16) wtab[tid] = FMT == 0 ? (float)(tid - 8) : kNF4g[tid];
+  if (tid < 16) wtab[tid] = FMT == 1 ? kNF4g[tid] : (float)(tid - 8);
 
   // global -> register staging: X 4 x 16 B per thread (row tid/8 + 32 i, chunk tid%8); W one row-half of 32 k
   uint4 xa[4];
-  uint4 wq;
+  uint4 wq, wbf[FMT == 2 ? 4 : 1];  // packed nibbles (4-bit formats) / 32 bf16 weights (FMT 2)
   float wscale = 0.0f;  // group scale (int4-g, bf16) / block absmax (nf4, fp32) of this thread's 32 weights
   const int a_row = tid >> 3, a_chunk = tid & 7;
   const int w_row = tid >> 1, w_half = tid & 1;
@@ -70,6 +70,12 @@ __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
       xa[i] = a_in ? v : make_uint4(0, 0, 0, 0);
     }
     const int wk = kt * BK + w_half * 32 < a.K ? kt * BK + w_half * 32 : 0;
+    if (FMT == 2) {
+      const uint4* src = (const uint4*)((const uint16_t*)a.qw + (size_t)w_n * a.K + wk);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) wbf[c] = src[c];
+      return;
+    }
     wq = *(const uint4*)(a.qw + (size_t)w_n * wrow_bytes + wk / 2);
     const size_t si = (size_t)w_n * groups + wk / a.G;
     wscale = FMT == 0 ? bf2f(((const uint16_t*)a.sc)[si]) : ((const float*)a.sc)[si];
@@ -79,6 +85,11 @@ __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
     unsigned char* B = A + TILE_BYTES;
 #pragma unroll
     for (int i = 0; i < 4; ++i) *(uint4*)(A + swz(a_row + 32 * i, a_chunk)) = xa[i];
+    if (FMT == 2) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) *(uint4*)(B + swz(w_row, w_half * 4 + c)) = wbf[c];
+      return;
+    }
     const uint32_t wd[4] = {wq.x, wq.y, wq.z, wq.w};  // 32 nibbles = 4 chunks of 8 k
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
@@ -144,6 +155,20 @@ __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
 }
 
 }  // namespace lga
+
+// bf16 weights [N][K] (BASELINE config 2, unquantized nn.Linear; reference F.linear in bf16-true): the same tiles
+// with W staged as stored.
+extern "C" int lga_bf16_gemm(const void* x, const void* weight, const void* bias, const void* residual, void* y,
+                             int M, int N, int K, hipStream_t stream) {
+  LGA_CHECK_ARG(x && weight && y, "lga_bf16_gemm: null pointer");
+  LGA_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 32 == 0, "lga_bf16_gemm: K must be a positive multiple of 32");
+  LGA_CHECK_ARG(((uintptr_t)x | (uintptr_t)weight) % 16 == 0, "lga_bf16_gemm: x and weight must be 16-B aligned");
+  lga::GemmArgs a{(const uint16_t*)x, (const uint8_t*)weight, nullptr, (const uint16_t*)bias,
+                  (const uint16_t*)residual, (uint16_t*)y, M, N, K, 32};
+  const dim3 grid((N + lga::BN - 1) / lga::BN, (M + lga::BM - 1) / lga::BM);
+  lga::gemm_q4_kernel<2><<<grid, 256, 0, stream>>>(a);
+  LGA_LAUNCH_RETURN();
+}
 
 extern "C" int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const void* bias,
                            const void* residual, void* y, int M, int N, int K, int group, int fmt,

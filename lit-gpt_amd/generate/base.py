@@ -6,7 +6,8 @@ steps at ``input_pos = T, T+1, ...``, stop on ``eos_id``, ``NotImplementedError`
 short) and ``main`` (:96-187) with the same flags and the same stderr timing line. Differences:
   * greedy decoding (``temperature == 0``) runs each step as one HIP graph replay (lit_gpt/runtime.py) with the
     argmax on the device — the role ``--compile`` (CUDA graphs) plays in the reference;
-  * ``--quantize`` takes this build's formats (int4-g128, nf4 / bnb.nf4 / bnb.nf4-dq);
+  * ``--quantize`` takes this build's formats (int4-g128, nf4 / bnb.nf4 / bnb.nf4-dq); without it the Linears
+    stay bf16 ``nn.Linear`` (BASELINE config 2) and run on the bf16 GEMV / GEMM kernels;
   * ``--synthetic NAME`` builds a random-init model of a registered config (no checkpoint, no tokenizer): the
     prompt is ``--prompt_len`` synthetic token ids.
 """
@@ -110,8 +111,10 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
         raise ValueError(f"rope_positions must be 'reference' or 'exact', got {rope_positions!r}")
     from lit_gpt.quantize import QuantizedPrecision
 
-    if quantize is None:
-        raise NotImplementedError("the MI355X path runs quantized weights: pass --quantize int4-g128 or nf4")
+    if quantize is not None:
+        from lit_gpt.quantize import parse_mode
+
+        parse_mode(quantize)  # unsupported modes fail before any weight is materialised
     with torch.device("meta"):
         model = GPT(config)
     state = None
@@ -135,7 +138,12 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
         setattr(mod, attr, torch.nn.Parameter(t, requires_grad=False))
     if tp is not None:
         tp(model)
-    QuantizedPrecision(quantize).convert_module(model, device)
+    if quantize is not None:
+        QuantizedPrecision(quantize).convert_module(model, device)
+    else:  # bf16-true: the Linears stay nn.Linear; TP row shards are strided views -> own contiguous storage
+        for mod in model.modules():
+            if isinstance(mod, torch.nn.Linear) and not mod.weight.is_contiguous():
+                mod.weight = torch.nn.Parameter(mod.weight.data.contiguous(), requires_grad=False)
     torch.cuda.empty_cache()
     prev = torch.get_default_dtype()
     torch.set_default_dtype(torch.bfloat16 if rope_positions == "reference" else torch.float32)
@@ -156,7 +164,7 @@ def main(prompt: str = "What food do llamas eat?", *, num_samples: int = 1, max_
          synthetic: Optional[str] = None, prompt_len: int = 16) -> None:
     precision = precision or "bf16-true"
     if precision != "bf16-true":
-        raise NotImplementedError("the MI355X 4-bit path computes in bf16 (precision bf16-true)")
+        raise NotImplementedError("the MI355X path computes in bf16 (precision bf16-true)")
     device = torch.device("cuda", torch.cuda.current_device())
     tokenizer = None
     if synthetic is not None:

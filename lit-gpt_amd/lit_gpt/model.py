@@ -37,13 +37,51 @@ def _gpu_only(what: str) -> None:
     raise RuntimeError(f"{what}: this build computes on the MI355X only (no CPU path); move the model to 'cuda'")
 
 
+def _dense_weight(linear: nn.Linear) -> torch.Tensor:
+    """The bf16 weight of an unquantized Linear, made contiguous once in place (a TP row shard from
+    ``generate/tp.py``'s ``tensor_split(dim=1)`` is a strided view)."""
+    w = linear.weight
+    if w.dtype != torch.bfloat16:
+        raise TypeError(f"unquantized Linear on the MI355X path expects bf16 weights (bf16-true), got {w.dtype}")
+    if not w.is_contiguous():
+        linear.weight.data = w.data.contiguous()
+        w = linear.weight
+    return w
+
+
+def _dense(linear: nn.Linear, x: torch.Tensor, *, residual: Optional[torch.Tensor] = None,
+           norm_weight: Optional[torch.Tensor] = None, norm_eps: float = 1e-5) -> torch.Tensor:
+    """F.linear with bf16 weights (BASELINE config 2): one token -> lga_bf16_gemv (RMSNorm / residual fused),
+    several -> lga_bf16_gemm (MFMA)."""
+    w = _dense_weight(linear)
+    N, K = w.shape
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, K)
+    if x2.dtype != torch.bfloat16:
+        raise TypeError(f"Linear expects bf16 activations (bf16-true), got {x2.dtype}")
+    x2 = x2.contiguous()
+    M = x2.shape[0]
+    b = None if linear.bias is None else linear.bias.to(torch.bfloat16)
+    res = None if residual is None else residual.reshape(M, N).contiguous()
+    if M == 1:
+        y = ops.bf16_gemv(x2.view(-1), w, bias=b, residual=None if res is None else res.view(-1),
+                          norm_weight=norm_weight, eps=norm_eps)
+    else:
+        if norm_weight is not None:
+            x2 = ops.rmsnorm(x2, norm_weight, norm_eps)
+        y = ops.bf16_gemm(x2, w, bias=b, residual=res)
+    return y.view(*lead, N)
+
+
 def _lin(linear: nn.Module, x: torch.Tensor, **kw) -> torch.Tensor:
     from lit_gpt.quantize import QuantLinear
 
     if isinstance(linear, QuantLinear):
         return linear(x, **kw)
+    if isinstance(linear, nn.Linear) and linear.weight.is_cuda:
+        return _dense(linear, x, **kw)
     raise NotImplementedError(
-        "unquantized nn.Linear on the MI355X path: convert the model with "
+        "Linear without MI355X weights: move the model to the GPU in bf16, or convert it with "
         "lit_gpt.quantize.QuantizedPrecision('int4-g128' | 'nf4').convert_module(model) (the --quantize flag)")
 
 
@@ -354,7 +392,13 @@ class LLaMAMLP(nn.Module):
         f1, f2 = self.fc_1, self.fc_2
         fusable = (M == 1 and isinstance(f1, QuantLinear) and isinstance(f2, QuantLinear) and f1.bias is None
                    and f2.bias is None and (f1.fmt, f1.group) == (f2.fmt, f2.group))
-        if fusable:
+        dense = (M == 1 and type(f1) is nn.Linear and type(f2) is nn.Linear and f1.bias is None and f2.bias is None
+                 and f1.weight.is_cuda and f1.weight.shape == f2.weight.shape)
+        if dense:  # bf16 weights: fc_1 || fc_2 + SwiGLU in one GEMV launch, norm_2 fused
+            g = ops.bf16_gemv_swiglu(x2.view(-1), _dense_weight(f1), _dense_weight(f2),
+                                     norm_weight=None if norm is None else norm.weight,
+                                     eps=1e-5 if norm is None else norm.eps).view(1, -1)
+        elif fusable:
             if norm is not None and not ops.gemv_fuses_norm(C, dual=True):
                 x2, norm = norm(x2), None
             g = ops.q4_gemv_swiglu(x2.view(-1), f1.qweight, f1.scales, f2.qweight, f2.scales, f1.out_features, C,

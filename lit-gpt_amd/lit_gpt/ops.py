@@ -39,6 +39,9 @@ SIGNATURES = {
     "lga_q4_gemv": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemv_swiglu": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemm": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lga_bf16_gemv": [_P, _P, _P, _P, _P, _F, _P, _I, _I, _P],
+    "lga_bf16_gemv_swiglu": [_P, _P, _P, _P, _F, _P, _I, _I, _P],
+    "lga_bf16_gemm": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lga_rmsnorm": [_P, _P, _P, _I, _I, _F, _P],
     "lga_rope_kv_append": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lga_embedding": [_P, _I, _P, _P, _I, _I, _I, _P],
@@ -157,6 +160,41 @@ def q4_gemm(x, qweight, scales, N, K, group, fmt, *, bias=None, residual=None, o
                                       _dev(scales, "scales"), _opt(bias, "bias", torch.bfloat16),
                                       _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16),
                                       M, N, K, group, fmt, _stream()))
+    return y
+
+
+def bf16_gemv(x, weight, *, bias=None, residual=None, norm_weight=None, eps=1e-5, out=None):
+    """y (N,) = x (K,) . W (N, K)^T [+bias] [+residual] with bf16 weights; optional fused RMSNorm of x."""
+    N, K = weight.shape
+    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_bf16_gemv(_dev(x, "x", torch.bfloat16), _dev(weight, "weight", torch.bfloat16),
+                                        _opt(bias, "bias", torch.bfloat16), _opt(residual, "residual", torch.bfloat16),
+                                        _opt(norm_weight, "norm_weight", torch.bfloat16), float(eps),
+                                        _dev(y, "y", torch.bfloat16), N, K, _stream()))
+    return y
+
+
+def bf16_gemv_swiglu(x, w1, w2, *, norm_weight=None, eps=1e-5, out=None):
+    """y (N,) = bf16(silu(bf16(x W1^T))) * bf16(x W2^T) with bf16 weights, optional fused RMSNorm of x."""
+    N, K = w1.shape
+    if tuple(w2.shape) != (N, K):
+        raise ValueError(f"bf16_gemv_swiglu: weight shapes differ {tuple(w1.shape)} vs {tuple(w2.shape)}")
+    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_bf16_gemv_swiglu(_dev(x, "x", torch.bfloat16), _dev(w1, "w1", torch.bfloat16),
+                                               _dev(w2, "w2", torch.bfloat16),
+                                               _opt(norm_weight, "norm_weight", torch.bfloat16), float(eps),
+                                               _dev(y, "y", torch.bfloat16), N, K, _stream()))
+    return y
+
+
+def bf16_gemm(x, weight, *, bias=None, residual=None, out=None):
+    """Y (M, N) = X (M, K) . W (N, K)^T [+bias] [+residual] with bf16 weights, MFMA tiles."""
+    M = x.shape[0]
+    N, K = weight.shape
+    y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_bf16_gemm(_dev(x, "x", torch.bfloat16), _dev(weight, "weight", torch.bfloat16),
+                                        _opt(bias, "bias", torch.bfloat16), _opt(residual, "residual", torch.bfloat16),
+                                        _dev(y, "y", torch.bfloat16), M, N, K, _stream()))
     return y
 
 

@@ -151,6 +151,75 @@ def test_gemm_matches_reference(ops, fmt, group, M, N, K):
     assert np.max(err) <= 2e-3, float(np.max(err))
 
 
+# ------------------------------------------------------------------------------------------------ bf16 weights
+# BASELINE config 2: unquantized nn.Linear in bf16-true. Reference: fp64 product of the same bf16 x and W.
+@pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 11008), (32000, 4096), (1000, 256), (77, 1376), (40, 8),
+                                 (640, 8192), (300, 28672)])
+def test_bf16_gemv_matches_reference(ops, N, K):
+    w = bf16_np(_weights(N, K, f"bgv{N}x{K}"))
+    x = bf16_np(synth.normal((K,), f"bx{K}", 5, 1.0))
+    y = ops.bf16_gemv(to_dev_bf16(x), to_dev_bf16(w)).float().cpu().numpy()
+    ref = _ref_linear(x, w)
+    # bf16 output rounding (2^-8 relative) + fp32 accumulation order
+    tol = np.abs(ref) * 2 ** -7 + 1e-3 * np.sqrt(K / 4096) * 0.02 * np.abs(x).mean() * 4
+    assert np.all(np.abs(y - ref) <= tol), float(np.max(np.abs(y - ref) - tol))
+
+
+@pytest.mark.parametrize("K", [1024, 11008])
+def test_bf16_gemv_fused_norm_residual_bias(ops, K):
+    N = 1536
+    w = bf16_np(_weights(N, K, "bgvf"))
+    x = bf16_np(synth.normal((K,), "bxf", 5, 2.0))
+    nw = bf16_np(1.0 + synth.normal((K,), "bnw", 5, 0.2))
+    res = bf16_np(synth.normal((N,), "bres", 5, 1.0))
+    bias = bf16_np(synth.normal((N,), "bbias", 5, 0.1))
+    y = ops.bf16_gemv(to_dev_bf16(x), to_dev_bf16(w), bias=to_dev_bf16(bias), residual=to_dev_bf16(res),
+                      norm_weight=to_dev_bf16(nw), eps=1e-5).float().cpu().numpy()
+    xn = om.rms_norm(torch.from_numpy(x).bfloat16(), torch.from_numpy(nw).bfloat16(), 1e-5).float().numpy()
+    h = bf16_np((_ref_linear(xn, w) + bias).astype(np.float32))
+    ref = h + res
+    assert np.max(np.abs(y - ref) - np.abs(ref) * 2 ** -7 - np.abs(h) * 2 ** -7) <= 2e-3
+
+
+@pytest.mark.parametrize("N,K", [(11008, 4096), (333, 8192)])
+def test_bf16_gemv_swiglu(ops, N, K):
+    w1, w2 = bf16_np(_weights(N, K, "bs1")), bf16_np(_weights(N, K, "bs2"))
+    x = bf16_np(synth.normal((K,), "bxs", 5, 1.0))
+    nw = bf16_np(1.0 + synth.normal((K,), "bnws", 5, 0.1))
+    y = ops.bf16_gemv_swiglu(to_dev_bf16(x), to_dev_bf16(w1), to_dev_bf16(w2), norm_weight=to_dev_bf16(nw)
+                             ).float().cpu().numpy()
+    xn = om.rms_norm(torch.from_numpy(x).bfloat16(), torch.from_numpy(nw).bfloat16(), 1e-5).float().numpy()
+    a, b = _ref_linear(xn, w1), _ref_linear(xn, w2)
+    ref = (a / (1 + np.exp(-a))) * b
+    assert np.max(np.abs(y - ref) - np.abs(ref) * 2 ** -6) <= 1e-3
+
+
+@pytest.mark.parametrize("M,N,K", [(200, 768, 256), (2048, 1024, 4096), (5, 640, 1376), (130, 4096, 11008),
+                                   (64, 96, 32)])
+def test_bf16_gemm_matches_reference(ops, M, N, K):
+    w = bf16_np(_weights(N, K, f"bgm{N}x{K}"))
+    x = bf16_np(synth.normal((M, K), f"bgx{M}x{K}", 5, 1.0))
+    res = bf16_np(synth.normal((M, N), "bgres", 5, 1.0))
+    bias = bf16_np(synth.normal((N,), "bgbias", 5, 0.1))
+    y = ops.bf16_gemm(to_dev_bf16(x), to_dev_bf16(w), bias=to_dev_bf16(bias), residual=to_dev_bf16(res)
+                      ).float().cpu().numpy()
+    h = _ref_linear(x, w) + bias
+    ref = bf16_np(h.astype(np.float32)) + res
+    err = np.abs(y - ref) - (np.abs(ref) + np.abs(h)) * 2 ** -7
+    assert np.max(err) <= 2e-3, float(np.max(err))
+
+
+def test_bf16_ops_reject_bad_arguments(ops):
+    w = torch.zeros(16, 12, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError, match="multiple of 8"):
+        ops.bf16_gemv(torch.zeros(12, dtype=torch.bfloat16, device=DEV), w)
+    with pytest.raises(TypeError):
+        ops.bf16_gemv(torch.zeros(16, device=DEV), torch.zeros(4, 16, device=DEV))
+    with pytest.raises(RuntimeError, match="multiple of 32"):
+        ops.bf16_gemm(torch.zeros(2, 16, dtype=torch.bfloat16, device=DEV),
+                      torch.zeros(4, 16, dtype=torch.bfloat16, device=DEV))
+
+
 # ------------------------------------------------------------------------------------------------ row ops
 def test_rmsnorm_matches_oracle(ops, golden):
     g = golden("g3_ops.npz")

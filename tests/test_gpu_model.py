@@ -44,7 +44,8 @@ def build_gpu_model(cfg, sd, mode, max_seq):
     model = GPT(cfg)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     model = model.to(device=DEV, dtype=torch.bfloat16)
-    QuantizedPrecision(mode).convert_module(model, DEV)
+    if mode != "bf16":  # "bf16": unquantized nn.Linear (BASELINE config 2) on the bf16 GEMV / GEMM kernels
+        QuantizedPrecision(mode).convert_module(model, DEV)
     model.max_seq_length = max_seq
     model.set_kv_cache(1, device=DEV)
     return model.eval()
@@ -54,6 +55,8 @@ def oracle_for(cfg, sd, mode):
     def deq(k, v):
         if k.endswith(".weight") and v.ndim == 2 and not k.startswith("transformer.wte"):
             vb = quant.bf16_bits_to_f32(quant.f32_to_bf16_bits(v))
+            if mode == "bf16":
+                return vb
             if mode == "int4-g128":
                 return quant.dequantize_q4g(*quant.quantize_q4g(vb, 128), 128)
             return quant.dequantize_nf4(*quant.quantize_nf4(vb, 64), 64)
@@ -87,9 +90,11 @@ def _routing_ambiguous(margins, tol=2 ** -6):
 
 
 @pytest.mark.parametrize("key", list(CFGS))
-@pytest.mark.parametrize("mode", ["int4-g128", "nf4"])
+@pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bf16"])
 @torch.inference_mode()
 def test_teacher_forced_logits_match_oracle(key, mode):
+    if mode == "bf16" and key == "moe":
+        pytest.skip("sparse-MoE experts run 4-bit weights only (BASELINE config 5 is int4)")
     cfg = _cfg(key)
     sd = synth.state_dict(cfg, seed=21)
     T, N = 20, 12
@@ -117,16 +122,17 @@ def test_teacher_forced_logits_match_oracle(key, mode):
             assert int(torch.argmax(g)) == int(torch.argmax(e))
 
 
-@pytest.mark.parametrize("key", ["mha", "gqa", "moe"])
+@pytest.mark.parametrize("key,mode", [("mha", "int4-g128"), ("gqa", "int4-g128"), ("moe", "int4-g128"),
+                                      ("gqa", "bf16")])
 @torch.inference_mode()
-def test_greedy_generate_graph_equals_eager_and_oracle(key):
+def test_greedy_generate_graph_equals_eager_and_oracle(key, mode):
     from generate.base import generate
 
     cfg = _cfg(key)
     sd = synth.state_dict(cfg, seed=31)
     T, N = 16, 24
     prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=31)).to(DEV)
-    model = build_gpu_model(cfg, sd, "int4-g128", T + N)
+    model = build_gpu_model(cfg, sd, mode, T + N)
     y_graph = generate(model, prompt, T + N, temperature=0.0, use_graph=True).cpu()
     for b in model.transformer.h:
         b.attn.kv_cache.reset_parameters()
@@ -135,7 +141,7 @@ def test_greedy_generate_graph_equals_eager_and_oracle(key):
     assert y_graph.shape == (T + N,) and torch.equal(y_graph[:T], prompt.cpu())
     # oracle, teacher-forced on the GPU's own tokens: each GPU token must be the oracle's argmax unless the
     # oracle's top-2 margin is within the logit tolerance
-    ref = oracle_for(cfg, sd, "int4-g128")
+    ref = oracle_for(cfg, sd, mode)
     ref.set_kv_cache(T + N)
     margins = _watch_router_margins(ref)
     lg = ref.forward(prompt.cpu(), torch.arange(T))[-1].float()
@@ -194,7 +200,8 @@ def test_sample_on_gpu():
     assert sample(logits, temperature=1.0, top_k=1).tolist() == [0]
 
 
-@pytest.mark.parametrize("family,mode", [("llama", "int4-g128"), ("llama", "nf4"), ("moe", "int4-g128")])
+@pytest.mark.parametrize("family,mode", [("llama", "int4-g128"), ("llama", "nf4"), ("moe", "int4-g128"),
+                                         ("llama", "bf16")])
 def test_tensor_parallel_2_ranks_one_gpu(family, mode, tmp_path):
     """generate/tp.py sharding + all-reduce hooks + per-shard quantization on the HIP kernels: TP=2 (two ranks
     sharing cuda:0 over gloo) equals the unsharded model within bf16 reordering of the row-parallel sums."""

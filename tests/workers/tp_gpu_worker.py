@@ -31,7 +31,8 @@ def build(cfg, sd, mode, fabric=None):
     if fabric is not None:
         gtp.tensor_parallel(fabric, model)
     model = model.to(device=DEV, dtype=torch.bfloat16)
-    QuantizedPrecision(mode).convert_module(model, DEV)
+    if mode != "bf16":  # "bf16": the shards stay nn.Linear (bf16 GEMV / GEMM kernels)
+        QuantizedPrecision(mode).convert_module(model, DEV)
     model.max_seq_length = 64
     model.set_kv_cache(1, device=DEV)
     return model.eval()
