@@ -57,6 +57,27 @@ int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const void* scale
 int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const void* bias, const void* residual,
                 void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
 
+/* -- chained decode GEMVs: attn.proj+residual -> RMSNorm+fc_1||fc_2+SwiGLU -> mlp.proj+residual -> RMSNorm+the
+ *    next GEMV (next block's fused qkv, or ln_f + lm_head) in ONE launch (lit_gpt/model.py:591-592, :656,
+ *    :712-716, :619 / :518-519; the GEMVs that bnb gemv_4bit runs one by one). Stages hand off inside the launch
+ *    (csrc/chain.hip); int4-g (fmt 0) weights only. ------------------------------------------------------------ */
+typedef struct lga_chain_stage {
+  const void* x;             /* (K) bf16 input: stage 0 = attention output; stage s > 0 = y of stage s-1 */
+  const uint8_t* qweight;    /* (N, K/2) */
+  const void* scales;        /* (N, K/group) bf16 */
+  const uint8_t* qweight2;   /* stage 1: fc_2 (fc_1 is qweight); else NULL */
+  const void* scales2;
+  const void* residual;      /* stage 0: block input; stage 2: y of stage 0; else NULL */
+  const void* norm_weight;   /* stage 1: norm_2; stage 3: next norm_1 / ln_f; else NULL */
+  float norm_eps;
+  void* y;                   /* (N) bf16 */
+  int N, K, group;
+} lga_chain_stage;
+/* stages: exactly 4, in the order above; counters: lga_decode_chain_counter_words() uint32, zeroed once before the
+ * first launch (every launch re-arms them); err: bit 0 set when an in-launch wait timed out (results invalid). */
+int lga_q4_decode_chain(const lga_chain_stage* stages, unsigned* counters, unsigned* err, lga_stream_t stream);
+size_t lga_decode_chain_counter_words(void);
+
 /* -- unquantized bf16 Linears (BASELINE config 2: no --quantize, precision bf16-true; the reference runs
  *    F.linear on the bf16 nn.Linear weight, lit_gpt/model.py:619, :656, :712-716, :519) ------------------- */
 /* decode GEMV y (N) = x (K) . W (N, K)^T [+bias] [+residual]; optional fused RMSNorm of x (as lga_q4_gemv) */

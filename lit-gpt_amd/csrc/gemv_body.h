@@ -1,0 +1,314 @@
+// Decode GEMV body over packed 4-bit weights, shared by the single-GEMV launches (gemv.hip) and the chained
+// out-projection + MLP + next-GEMV launch (chain.hip). Design notes: gemv.hip.
+#pragma once
+#include "decode_ops.h"
+
+namespace lga {
+
+#ifdef LGA_GEMV_TRACE  // lab builds only (tools/gemv_trace.py): per-wave phase timestamps, 100 MHz clock
+__device__ unsigned long long g_gemv_trace[65536 * 8];
+#define LGA_GTRACE(i)                                                                                        \
+  do {                                                                                                     \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");                                          \
+    if ((threadIdx.x & 63) == 0)                                                                         \
+      g_gemv_trace[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define LGA_GTRACE_NOWAIT(i)                                                                                 \
+  do {                                                                                                     \
+    if ((threadIdx.x & 63) == 0)                                                                         \
+      g_gemv_trace[((size_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LGA_GTRACE(i) \
+  do {                \
+  } while (0)
+#define LGA_GTRACE_NOWAIT(i) \
+  do {                       \
+  } while (0)
+#endif
+
+
+struct GemvArgs {
+  const uint16_t* x;         // [K] bf16
+  const uint8_t* qw;         // [N][K/2]
+  const void* sc;            // q4g: bf16 [N][K/G]; nf4: f32 [N][K/G]
+  const uint8_t* qw2;        // dual: second weight (fc_2)
+  const void* sc2;
+  const uint16_t* bias;      // [N] or null
+  const uint16_t* residual;  // [N] or null
+  const uint16_t* norm_w;    // [K] or null (fused RMSNorm)
+  uint16_t* y;               // [N]
+  int N, K, G;
+  float eps;
+  // sparse-MoE expert routing (lga_q4_gemv*_experts): grid.y = slots; slot s computes with the weights of expert
+  // eidx[s] (qw/qw2 + e * ew bytes, sc/sc2 + e * es bytes), reads x + s * xs and writes y + s * N
+  const int32_t* eidx;
+  long long ew, es;
+  int xs, n_expert, slots;
+};
+
+// In-launch hand-off between chained GEMV stages (lga_q4_decode_chain, chain.hip): every stage owns a contiguous
+// range of workgroups, dispatched in order, and counts its finished workgroups in kChainShards counters (256 B
+// apart; workgroup b of a stage adds to shard b % kChainShards). MI355X_MICROARCH.md "Valid forms", row 1: the
+// producer stores its outputs write-through (sc1, 4/8-B), every storing wave drains them (vmcnt(0)), then one
+// lane adds to its shard after a workgroup barrier; the consumer's wave 0 polls every shard with sc1 loads and
+// the other waves load after a workgroup barrier; all loads of handed-off bytes are sc1 loads.
+constexpr int kChainShards = 16;
+constexpr int kChainStride = 64;  // uint32 per counter
+
+struct ChainLink {
+  const unsigned* wait_cnt;  // shard counters of the producing stage (null: inputs predate the launch)
+  int wait_wgs;              // workgroups of the producing stage
+  unsigned* post_cnt;        // this stage's shard counters
+  unsigned* err;             // bit 0: a wait timed out (the launch's results are invalid)
+};
+
+__device__ __forceinline__ unsigned chain_ld(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load_dword sc1
+}
+
+// wave 0 polls until every shard of the producing stage has counted all its workgroups (bounded: ~20 ms, then the
+// error bit is set and the launch carries on so it always drains); then the workgroup barrier releases the rest
+__device__ __forceinline__ void chain_wait(const ChainLink& L) {
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const int sh = lane < kChainShards ? lane : 0;
+    const unsigned target = lane < kChainShards
+                                ? (unsigned)(L.wait_wgs / kChainShards + (sh < L.wait_wgs % kChainShards ? 1 : 0))
+                                : 0u;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (true) {
+      const unsigned v = chain_ld(L.wait_cnt + sh * kChainStride);
+      if (__all(v >= target)) break;
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {
+        if (lane == 0) __hip_atomic_fetch_or(L.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// 16-B activation chunk loaded as four sc1 dwords (written by another workgroup of this launch)
+__device__ __forceinline__ uint4 chain_ld16(const void* p) {
+  const unsigned* q = (const unsigned*)p;
+  return make_uint4(chain_ld(q), chain_ld(q + 1), chain_ld(q + 2), chain_ld(q + 3));
+}
+
+// Gather the wave's RPR row results (held after the butterfly by the first lane of each value group) into lane 0
+// and store them as one 4-B (RPR 2) or 8-B (RPR 4) sc1 store. DUAL: value index 2*row (+1 = fc_2 partner).
+template <int R>
+__device__ __forceinline__ int bfly_lane(int vi) {  // first lane of value index vi (inverse of bfly_index)
+  return R == 8 ? ((vi >> 2) & 1) * 32 + ((vi >> 1) & 1) * 16 + (vi & 1) * 8
+                : (R == 4 ? ((vi >> 1) & 1) * 32 + (vi & 1) * 16 : (vi & 1) * 32);
+}
+template <int RPR, int R>
+__device__ __forceinline__ void chain_store(uint16_t* y, uint16_t v, int lane, bool dual, bool in_range) {
+  static_assert(RPR == 2 || RPR == 4, "chained stages store 2 or 4 rows per wave");
+  uint32_t w[RPR / 2];
+#pragma unroll
+  for (int r = 0; r < RPR; r += 2) {
+    const int l0 = bfly_lane<R>(dual ? 2 * r : r), l1 = bfly_lane<R>(dual ? 2 * (r + 1) : r + 1);
+    const uint32_t a0 = (uint32_t)__shfl((int)v, l0) & 0xFFFFu, a1 = (uint32_t)__shfl((int)v, l1) & 0xFFFFu;
+    w[r / 2] = a0 | (a1 << 16);
+  }
+  if (lane == 0 && in_range) {
+    if (RPR == 4) {
+      const uint64_t q = (uint64_t)w[0] | ((uint64_t)w[RPR / 2 - 1] << 32);
+      __hip_atomic_store((uint64_t*)y, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store((uint32_t*)y, w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// One wave of a decode GEMV (see gemv.hip for the design). CHAIN: the workgroup is part of a chained launch —
+// weights are issued first, then the producing stage is awaited, activations / residual are read with sc1 loads,
+// the wave's RPR outputs leave as ONE 4/8-B sc1 store from lane 0, and the workgroup counts itself in its shard.
+// Returns (CHAIN, thread 0) the shard counter's value before this workgroup's add; 0 otherwise.
+template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, bool CHAIN>
+__device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned char* smem, const ChainLink* link) {
+  if (!CHAIN && a.eidx) {  // wave-uniform: one scalar load of the routed expert id, then plain pointer offsets
+    const long long e = min(max(a.eidx[blockIdx.y], 0), a.n_expert - 1);
+    a.qw += e * a.ew;
+    a.sc = (const unsigned char*)a.sc + e * a.es;
+    if (DUAL) {
+      a.qw2 += e * a.ew;
+      a.sc2 = (const unsigned char*)a.sc2 + e * a.es;
+    }
+    a.x += (size_t)blockIdx.y * a.xs;
+    a.y += (size_t)blockIdx.y * a.N;
+  }
+  uint4* xl = (uint4*)smem;                        // K/8 uint4 (bf16 pairs)
+  float* xsum = (float*)(smem + (size_t)a.K * 2);  // K/32 chunk sums
+  float* red = xsum + a.K / 32;                    // 4
+  float* nf4 = red + 4;                            // 16
+  constexpr int R = DUAL ? 2 * RPR : RPR;          // values per lane entering the butterfly
+  const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
+  const int NC = a.K / 32, n8 = a.K / 8, groups = a.K / a.G;
+  const int row0 = (blk * 4 + wave) * RPR;
+  if (FMT == 1 && t < 16) nf4[t] = kNF4v[t];
+  LGA_GTRACE_NOWAIT(0);
+
+  // 1. activation (and norm weight) share of this thread: uint4 t, t+256, ... (clamped, branch-free)
+  uint4 xr[CPT], nr[CPT];
+  if (!CHAIN) {
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int u = min(t + 256 * i, n8 - 1);
+      xr[i] = ((const uint4*)a.x)[u];
+      if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
+    }
+  }
+  // 2. every weight / scale / residual load of this wave (rows past N re-read row N-1; never stored), issued in
+  //    the order step 4 consumes them (chunk-major, each scale right after its weights): vmcnt retires in order,
+  //    so the first dots start once their own chunk has landed instead of after the whole wave's stream
+  uint4 w[RPR][CPT], w2[DUAL ? RPR : 1][DUAL ? CPT : 1];
+  uint32_t s[RPR][CPT], s2[DUAL ? RPR : 1][DUAL ? CPT : 1];
+  uint32_t res = 0;
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int c = min(lane + 64 * j, NC - 1);
+    const int g = (c * 32) / a.G;
+#pragma unroll
+    for (int i = 0; i < RPR; ++i) {
+      const size_t n = (size_t)min(row0 + i, a.N - 1);
+      w[i][j] = ld_nt16(a.qw + n * (a.K / 2) + (size_t)c * 16);
+      s[i][j] = load_scale_bits<FMT>(a.sc, n * groups + g);
+      if (DUAL) {
+        w2[i][j] = ld_nt16(a.qw2 + n * (a.K / 2) + (size_t)c * 16);
+        s2[i][j] = load_scale_bits<FMT>(a.sc2, n * groups + g);
+      }
+    }
+  }
+  if (!CHAIN && RES) res = a.residual[min(row0 + (lane & (RPR - 1)), a.N - 1)];
+  __builtin_amdgcn_sched_barrier(0);  // nothing that waits on x may move above the weight loads
+  if constexpr (CHAIN) {
+    if (link->wait_cnt) chain_wait(*link);
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const int u = min(t + 256 * i, n8 - 1);
+      xr[i] = chain_ld16(a.x + (size_t)u * 8);
+      if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
+    }
+    if (RES) {  // the wave's RPR residual values (N % RPR == 0, checked on the host), one sc1 load
+      const unsigned* rp = (const unsigned*)(a.residual + min(row0, a.N - RPR));
+      const unsigned w0 = chain_ld(rp + ((lane & (RPR - 1)) >> 1));
+      res = (lane & 1) ? (w0 >> 16) : (w0 & 0xFFFFu);
+    }
+  }
+  LGA_GTRACE_NOWAIT(1);
+
+  // 3. stage x into LDS (RMS-normalised when NORM) while the weights stream
+  float rs = 1.0f;
+  if (NORM) {
+    float ss = 0.0f;
+#pragma unroll
+    for (int i = 0; i < CPT; ++i) {
+      const bool ok = t + 256 * i < n8;
+      const uint32_t d[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float lo = ok ? bflo(d[q]) : 0.0f, hi = ok ? bfhi(d[q]) : 0.0f;
+        ss = fmaf(lo, lo, ss);
+        ss = fmaf(hi, hi, ss);
+      }
+    }
+    ss = wave_sum_uniform(ss);
+    if (lane == 0) red[wave] = ss;
+    LGA_GTRACE_NOWAIT(2);
+    __syncthreads();
+    rs = 1.0f / sqrtf(((red[0] + red[1]) + (red[2] + red[3])) / (float)a.K + a.eps);
+  }
+#pragma unroll
+  for (int i = 0; i < CPT; ++i) {
+    const int u = t + 256 * i;
+    uint32_t d[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};  // bf16 pairs (x0,x1) (x2,x3) (x4,x5) (x6,x7)
+    if (NORM) {  // bf16(w * (x * rs)), rounded in hardware, two elements per instruction
+      const uint32_t nw[4] = {nr[i].x, nr[i].y, nr[i].z, nr[i].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        d[q] = pack2(__fmul_rn(bflo(nw[q]), __fmul_rn(bflo(d[q]), rs)),
+                     __fmul_rn(bfhi(nw[q]), __fmul_rn(bfhi(d[q]), rs)));
+    }
+    float cs = ((bflo(d[0]) + bfhi(d[0])) + (bflo(d[1]) + bfhi(d[1]))) +
+               ((bflo(d[2]) + bfhi(d[2])) + (bflo(d[3]) + bfhi(d[3])));
+    cs += __shfl_xor(cs, 1);  // 4 consecutive threads hold one 32-element chunk
+    cs += __shfl_xor(cs, 2);
+    if (u < n8) {
+      // (x0,x4) (x1,x5) (x2,x6) (x3,x7): byte permutes of the bf16 pairs
+      xl[u] = make_uint4(__builtin_amdgcn_perm(d[2], d[0], 0x05040100u), __builtin_amdgcn_perm(d[2], d[0], 0x07060302u),
+                         __builtin_amdgcn_perm(d[3], d[1], 0x05040100u), __builtin_amdgcn_perm(d[3], d[1], 0x07060302u));
+      if ((u & 3) == 0) xsum[u >> 2] = cs;
+    }
+  }
+  __syncthreads();
+  LGA_GTRACE_NOWAIT(3);
+  LGA_GTRACE(4);
+
+  // 4. dequant-dot every row of this wave, then one butterfly for all of them
+  const uint32_t nmask = nibble_mask();
+  float part[R];
+#pragma unroll
+  for (int i = 0; i < R; ++i) part[i] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < CPT; ++j) {
+    const int c = lane + 64 * j;
+    const bool ok = c < NC;
+    const int cc = min(c, NC - 1);
+    const uint4* xc = xl + cc * 4;
+    const float xs = xsum[cc];
+#pragma unroll
+    for (int i = 0; i < RPR; ++i) {
+      const float d = chunk_dot<FMT>(w[i][j], xc, xs, nf4, nmask);
+      if (DUAL) {  // value index = 2*row + matrix (so the pair of one row lands in lanes l and l^8 / l^16 / l^32)
+        part[2 * i] = fmaf(ok ? scale_of<FMT>(s[i][j]) : 0.0f, d, part[2 * i]);
+        const float d2 = chunk_dot<FMT>(w2[i][j], xc, xs, nf4, nmask);
+        part[2 * i + 1] = fmaf(ok ? scale_of<FMT>(s2[i][j]) : 0.0f, d2, part[2 * i + 1]);
+      } else {
+        part[i] = fmaf(ok ? scale_of<FMT>(s[i][j]) : 0.0f, d, part[i]);
+      }
+    }
+  }
+  const float tot = butterfly<R>(part, lane);
+  const int vi = bfly_index<R>(lane);  // value index held by this lane
+  constexpr int GROUP = 64 / R;        // lanes per value after the butterfly
+  if (DUAL) {
+    // partner value (other matrix, same row) sits in the lane whose value index differs in bit 0
+    constexpr int PD = R == 8 ? 8 : (R == 4 ? 16 : 32);
+    const float other = PD == 8 ? LGA_DPP(tot, 0x128) : __shfl_xor(tot, PD);
+    const int row = row0 + (vi >> 1);
+    const float g = round_bf(silu_f(round_bf(tot)));  // silu(bf16(fc_1 x)) -> bf16
+    const uint16_t ob = f2bf(__fmul_rn(g, round_bf(other)));  // * bf16(fc_2 x)
+    if constexpr (CHAIN) {
+      chain_store<RPR, R>(a.y + row0, ob, lane, true, row0 < a.N);
+    } else if ((lane & (GROUP - 1)) == 0 && (vi & 1) == 0 && row < a.N) {
+      a.y[row] = ob;
+    }
+    LGA_GTRACE(5);
+  } else {
+    const int row = row0 + vi;
+    float o = tot;
+    if (RES) {
+      // residual of row vi sits in lane vi (loaded up front); fetch it into this lane
+      o = round_bf(a.bias ? o + bf2f(a.bias[min(row, a.N - 1)]) : o) +
+          __uint_as_float(((uint32_t)__shfl(res, vi)) << 16);
+    } else if (a.bias) {
+      o += bf2f(a.bias[min(row, a.N - 1)]);
+    }
+    if constexpr (CHAIN) chain_store<RPR, R>(a.y + row0, f2bf(o), lane, false, row0 < a.N);
+    else if ((lane & (GROUP - 1)) == 0 && row < a.N) a.y[row] = f2bf(o);
+    LGA_GTRACE(5);
+  }
+  if constexpr (CHAIN) {  // every storing wave has drained its sc1 store; one lane counts the workgroup
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0)
+      return __hip_atomic_fetch_add(link->post_cnt + (blk % kChainShards) * kChainStride, 1u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+  }
+  return 0u;
+}
+
+}  // namespace lga

@@ -60,7 +60,16 @@ SIGNATURES = {
                                    _P, _I, _I, _I, _I, _I, _P],
     "lga_moe_combine": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
 }
-_RESTYPES = {"lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
+class ChainStage(ctypes.Structure):
+    """``lga_chain_stage`` of include/litgpt_amd.h."""
+    _fields_ = [("x", _P), ("qweight", _P), ("scales", _P), ("qweight2", _P), ("scales2", _P), ("residual", _P),
+                ("norm_weight", _P), ("norm_eps", _F), ("y", _P), ("N", _I), ("K", _I), ("group", _I)]
+
+
+SIGNATURES["lga_q4_decode_chain"] = [ctypes.POINTER(ChainStage), _P, _P, _P]
+SIGNATURES["lga_decode_chain_counter_words"] = []
+
+_RESTYPES = {"lga_decode_chain_counter_words": ctypes.c_size_t, "lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
              "lga_decode_layer_counters": ctypes.c_size_t}
 
 _lib: Optional[ctypes.CDLL] = None
@@ -161,6 +170,42 @@ def q4_gemm(x, qweight, scales, N, K, group, fmt, *, bias=None, residual=None, o
                                       _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16),
                                       M, N, K, group, fmt, _stream()))
     return y
+
+
+class ChainWorkspace:
+    """Hand-off counters of lga_q4_decode_chain (zeroed once; every launch re-arms them, so they survive HIP-graph
+    replays) and its error word (bit 0: an in-launch wait timed out)."""
+
+    def __init__(self, device) -> None:
+        n = load_library().lga_decode_chain_counter_words()
+        self.counters = torch.zeros(n, dtype=torch.int32, device=device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=device)
+
+
+def q4_decode_chain(y_att, x_in, proj, fc_1, fc_2, norm_2, down, nxt, nxt_norm, ws: ChainWorkspace, out=None):
+    """One launch: h_mid = x_in + proj(y_att); act = silu(fc_1 n) * fc_2 n with n = norm_2(h_mid);
+    h_out = h_mid + down(act); out = nxt(nxt_norm(h_out)). The Linears are int4-g QuantLinear modules; the norms
+    RMSNorm modules. Returns (h_out, out)."""
+    dev = y_att.device
+    C, I = fc_1.in_features, fc_1.out_features
+    h_mid = torch.empty(C, dtype=torch.bfloat16, device=dev)
+    act = torch.empty(I, dtype=torch.bfloat16, device=dev)
+    h_out = torch.empty(C, dtype=torch.bfloat16, device=dev)
+    out = out if out is not None else torch.empty(nxt.out_features, dtype=torch.bfloat16, device=dev)
+
+    def st(x, lin, y, lin2=None, residual=None, norm=None):
+        return ChainStage(_dev(x, "x", torch.bfloat16), _dev(lin.qweight, "qweight", torch.uint8),
+                          _dev(lin.scales, "scales"), None if lin2 is None else _dev(lin2.qweight, "qweight2"),
+                          None if lin2 is None else _dev(lin2.scales, "scales2"),
+                          _opt(residual, "residual", torch.bfloat16),
+                          None if norm is None else _dev(norm.weight, "norm_weight", torch.bfloat16),
+                          float(norm.eps) if norm is not None else 0.0, _dev(y, "y", torch.bfloat16),
+                          lin.out_features, lin.in_features, lin.group)
+
+    stages = (ChainStage * 4)(st(y_att, proj, h_mid, residual=x_in), st(h_mid, fc_1, act, lin2=fc_2, norm=norm_2),
+                              st(act, down, h_out, residual=h_mid), st(h_out, nxt, out, norm=nxt_norm))
+    _check(load_library().lga_q4_decode_chain(stages, ws.counters.data_ptr(), ws.err.data_ptr(), _stream()))
+    return h_out, out
 
 
 def bf16_gemv(x, weight, *, bias=None, residual=None, norm_weight=None, eps=1e-5, out=None):
