@@ -129,7 +129,7 @@ extern "C" int lga_q4_decode_chain(const lga_chain_stage* stages, unsigned* coun
   }
   c.cnt = counters;
   c.err = err;
-  const size_t lds = (size_t)(C > I ? C : I) * 2 + ((C > I ? C : I) / 32) * 4 + 4 * 4 + 16 * 4;
+  const size_t lds = (size_t)(C > I ? C : I) * 2 + ((C > I ? C : I) / 32) * 4 + 16 * 4 + 16 * 4;
   if (cc == 1 && ci == 1) launch_chain<1, 1>(c, lds, stream);
   else if (cc == 1 && ci == 2) launch_chain<1, 2>(c, lds, stream);
   else if (cc == 2 && ci == 6) launch_chain<2, 6>(c, lds, stream);

@@ -27,27 +27,33 @@
 
 namespace lga {
 
+#ifndef LGA_GEMV_NW
+#define LGA_GEMV_NW 4  // waves per workgroup
+#endif
+constexpr int kGemvNW = LGA_GEMV_NW;
+
 template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES>
-__global__ void __launch_bounds__(256) gemv_q4_kernel(GemvArgs a) {
+__global__ void __launch_bounds__(kGemvNW * 64) gemv_q4_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  gemv_q4_body<RPR, CPT, FMT, DUAL, NORM, RES, false>(a, blockIdx.x, smem, nullptr);
+  gemv_q4_body<RPR, CPT, FMT, DUAL, NORM, RES, false, kGemvNW>(a, blockIdx.x, smem, nullptr);
 }
 
 template <int RPR, int CPT, int FMT, bool DUAL>
 static void launch(const GemvArgs& a, hipStream_t stream) {
   const int waves = (a.N + RPR - 1) / RPR;
-  const dim3 blocks((waves + 3) / 4, a.eidx ? a.slots : 1);
-  const size_t lds = (size_t)a.K * 2 + (a.K / 32) * 4 + 4 * 4 + 16 * 4;
+  const dim3 blocks((waves + kGemvNW - 1) / kGemvNW, a.eidx ? a.slots : 1);
+  const size_t lds = (size_t)a.K * 2 + (a.K / 32) * 4 + 16 * 4 + 16 * 4;
+  constexpr int NT = kGemvNW * 64;
   const bool norm = a.norm_w != nullptr, res = a.residual != nullptr;
   if (DUAL) {
-    if (norm) gemv_q4_kernel<RPR, CPT, FMT, DUAL, true, false><<<blocks, 256, lds, stream>>>(a);
-    else gemv_q4_kernel<RPR, CPT, FMT, DUAL, false, false><<<blocks, 256, lds, stream>>>(a);
+    if (norm) gemv_q4_kernel<RPR, CPT, FMT, DUAL, true, false><<<blocks, NT, lds, stream>>>(a);
+    else gemv_q4_kernel<RPR, CPT, FMT, DUAL, false, false><<<blocks, NT, lds, stream>>>(a);
   } else if (norm) {
-    if (res) gemv_q4_kernel<RPR, CPT, FMT, DUAL, true, true><<<blocks, 256, lds, stream>>>(a);
-    else gemv_q4_kernel<RPR, CPT, FMT, DUAL, true, false><<<blocks, 256, lds, stream>>>(a);
+    if (res) gemv_q4_kernel<RPR, CPT, FMT, DUAL, true, true><<<blocks, NT, lds, stream>>>(a);
+    else gemv_q4_kernel<RPR, CPT, FMT, DUAL, true, false><<<blocks, NT, lds, stream>>>(a);
   } else {
-    if (res) gemv_q4_kernel<RPR, CPT, FMT, DUAL, false, true><<<blocks, 256, lds, stream>>>(a);
-    else gemv_q4_kernel<RPR, CPT, FMT, DUAL, false, false><<<blocks, 256, lds, stream>>>(a);
+    if (res) gemv_q4_kernel<RPR, CPT, FMT, DUAL, false, true><<<blocks, NT, lds, stream>>>(a);
+    else gemv_q4_kernel<RPR, CPT, FMT, DUAL, false, false><<<blocks, NT, lds, stream>>>(a);
   }
 }
 

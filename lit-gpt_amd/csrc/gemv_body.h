@@ -127,7 +127,8 @@ __device__ __forceinline__ void chain_store(uint16_t* y, uint16_t v, int lane, b
 // weights are issued first, then the producing stage is awaited, activations / residual are read with sc1 loads,
 // the wave's RPR outputs leave as ONE 4/8-B sc1 store from lane 0, and the workgroup counts itself in its shard.
 // Returns (CHAIN, thread 0) the shard counter's value before this workgroup's add; 0 otherwise.
-template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, bool CHAIN>
+// NW waves per workgroup (each its own row slot); the workgroup stages x once for all of them.
+template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, bool CHAIN, int NW = 4>
 __device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned char* smem, const ChainLink* link) {
   if (!CHAIN && a.eidx) {  // wave-uniform: one scalar load of the routed expert id, then plain pointer offsets
     const long long e = min(max(a.eidx[blockIdx.y], 0), a.n_expert - 1);
@@ -142,21 +143,24 @@ __device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned c
   }
   uint4* xl = (uint4*)smem;                        // K/8 uint4 (bf16 pairs)
   float* xsum = (float*)(smem + (size_t)a.K * 2);  // K/32 chunk sums
-  float* red = xsum + a.K / 32;                    // 4
-  float* nf4 = red + 4;                            // 16
+  float* red = xsum + a.K / 32;                    // NW (<= 16)
+  float* nf4 = red + 16;                           // 16
+  constexpr int NT = NW * 64;
+  constexpr int XI = (CPT * 4 + NW - 1) / NW;      // x uint4 per thread (CPT * 256 >= K / 8)
+  static_assert(NW == 4 || NW == 8 || NW == 16, "4, 8 or 16 waves per workgroup");
   constexpr int R = DUAL ? 2 * RPR : RPR;          // values per lane entering the butterfly
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int NC = a.K / 32, n8 = a.K / 8, groups = a.K / a.G;
-  const int row0 = (blk * 4 + wave) * RPR;
+  const int row0 = (blk * NW + wave) * RPR;
   if (FMT == 1 && t < 16) nf4[t] = kNF4v[t];
   LGA_GTRACE_NOWAIT(0);
 
-  // 1. activation (and norm weight) share of this thread: uint4 t, t+256, ... (clamped, branch-free)
-  uint4 xr[CPT], nr[CPT];
+  // 1. activation (and norm weight) share of this thread: uint4 t, t+NT, ... (clamped, branch-free)
+  uint4 xr[XI], nr[XI];
   if (!CHAIN) {
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int u = min(t + 256 * i, n8 - 1);
+    for (int i = 0; i < XI; ++i) {
+      const int u = min(t + NT * i, n8 - 1);
       xr[i] = ((const uint4*)a.x)[u];
       if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
     }
@@ -187,8 +191,8 @@ __device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned c
   if constexpr (CHAIN) {
     if (link->wait_cnt) chain_wait(*link);
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const int u = min(t + 256 * i, n8 - 1);
+    for (int i = 0; i < XI; ++i) {
+      const int u = min(t + NT * i, n8 - 1);
       xr[i] = chain_ld16(a.x + (size_t)u * 8);
       if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
     }
@@ -205,8 +209,8 @@ __device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned c
   if (NORM) {
     float ss = 0.0f;
 #pragma unroll
-    for (int i = 0; i < CPT; ++i) {
-      const bool ok = t + 256 * i < n8;
+    for (int i = 0; i < XI; ++i) {
+      const bool ok = t + NT * i < n8;
       const uint32_t d[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
@@ -219,11 +223,17 @@ __device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned c
     if (lane == 0) red[wave] = ss;
     LGA_GTRACE_NOWAIT(2);
     __syncthreads();
-    rs = 1.0f / sqrtf(((red[0] + red[1]) + (red[2] + red[3])) / (float)a.K + a.eps);
+    float r4[NW / 4];  // pairwise tree over the waves (NW = 4: ((r0 + r1) + (r2 + r3)))
+#pragma unroll
+    for (int i = 0; i < NW / 4; ++i) r4[i] = (red[4 * i] + red[4 * i + 1]) + (red[4 * i + 2] + red[4 * i + 3]);
+    float tot = r4[0];
+    if (NW == 8) tot = r4[0] + r4[1];
+    if (NW == 16) tot = (r4[0] + r4[1]) + (r4[2] + r4[3]);
+    rs = 1.0f / sqrtf(tot / (float)a.K + a.eps);
   }
 #pragma unroll
-  for (int i = 0; i < CPT; ++i) {
-    const int u = t + 256 * i;
+  for (int i = 0; i < XI; ++i) {
+    const int u = t + NT * i;
     uint32_t d[4] = {xr[i].x, xr[i].y, xr[i].z, xr[i].w};  // bf16 pairs (x0,x1) (x2,x3) (x4,x5) (x6,x7)
     if (NORM) {  // bf16(w * (x * rs)), rounded in hardware, two elements per instruction
       const uint32_t nw[4] = {nr[i].x, nr[i].y, nr[i].z, nr[i].w};

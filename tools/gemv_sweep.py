@@ -15,6 +15,9 @@ sys.path[:0] = [str(REPO / "lit-gpt_amd"), str(REPO)]
 
 from lit_gpt import ops  # noqa: E402
 
+if os.environ.get("GEMV_LIB"):  # lab build of the library (e.g. -DLGA_GEMV_LAB variants)
+    ops.LIB_PATH = Path(os.environ["GEMV_LIB"])
+
 SHAPES = {  # name: (N, K, dual)
     "qkv": (12288, 4096, False),
     "o_proj": (4096, 4096, False),
