@@ -392,9 +392,11 @@ def decode_fusable(head_size: int, rope_n_elem: int) -> bool:
 
 
 def decode_splits(n_query_groups: int, q_per_kv: int, head_size: int, max_seq: int, n_cu: int = 256) -> int:
-    """Sequence splits for T = 1 attention: one workgroup per CU across all query groups (tools/attn_sweep.py:
-    8 splits beat 16 for Llama-2-7B at p = 128..4000 on MI355X — every extra split adds publish/combine work)."""
-    s = max(1, n_cu // max(1, n_query_groups))
+    """Sequence splits for T = 1 attention: one workgroup per CU across all query groups, at most 16 splits
+    (tools/attn_sweep.py on MI355X, p = 2048..4000: 8 splits beat 16 for Llama-2-7B's 32 groups; with the few
+    groups per rank of tensor parallelism 16 splits beat 32/64/128 — G = 4: 7.8 vs 10.9 us at 64 splits; G = 1,
+    8 heads per group: 21 vs 34 us at 64 — because the last-arriving split's combine grows with the split count)."""
+    s = max(1, min(n_cu // max(1, n_query_groups), 16))
     return min(s, max(1, max_seq // 16), 256)
 
 
