@@ -20,6 +20,12 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int BM = 128, BN = 128, BK = 64;
+#ifndef LGA_GEMM_GLDS
+#define LGA_GEMM_GLDS 1  // X (and bf16 W) tiles staged global -> LDS directly (global_load_lds_dwordx4)
+#endif
+#ifndef LGA_GEMM_XCD
+#define LGA_GEMM_XCD 0  // XCD-aware tile order (each XCD walks a contiguous run of tiles): measured 1-3 % slower
+#endif
 constexpr int TILE_BYTES = BM * BK * 2;  // one operand tile in LDS (128 rows x 128 B)
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
@@ -40,13 +46,32 @@ struct GemmArgs {
   int M, N, K, G;
 };
 
-template <int FMT>
+// X tile rows [r0, r0 + 8) of one 128-B-row tile, one wave instruction: lane L fills LDS bytes base + 16 L (row
+// r0 + L/8, physical chunk L%8), so it loads the logical chunk that swz() puts there: (L%8) ^ (row & 7)
+__device__ __forceinline__ void glds_rows8(const uint16_t* src, int ld, int row_lo, int row_max, int k0,
+                                           unsigned char* lds_rows, int lane) {
+  const int r = row_lo + (lane >> 3);
+  const int lc = (lane & 7) ^ (r & 7);
+  const uint16_t* g = src + (size_t)min(r, row_max) * ld + k0 + lc * 8;
+  __builtin_amdgcn_global_load_lds((const void*)g, (__attribute__((address_space(3))) void*)lds_rows, 16, 0, 0);
+}
+
+template <int FMT, bool GLDS>
 __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * 2 * TILE_BYTES];  // [buf][A|B]
   __shared__ float wtab[16];  // nibble -> value: nibble - 8 (int4-g) or the NF4 codebook
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave >> 1, wn = wave & 1;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+  int bx = blockIdx.x, by = blockIdx.y;
+  if (LGA_GEMM_XCD) {  // block b runs on XCD b % 8: give each XCD a contiguous run of tiles (x fastest)
+    const int nx = gridDim.x, T = nx * gridDim.y, b = by * nx + bx;
+    if (T % 8 == 0) {
+      const int t = (b % 8) * (T / 8) + b / 8;
+      bx = t % nx;
+      by = t / nx;
+    }
+  }
+  const int m0 = by * BM, n0 = bx * BN;
   const int nk = (a.K + BK - 1) / BK, groups = FMT == 2 ? 1 : a.K / a.G;
   const size_t wrow_bytes = (size_t)a.K / 2;
   if (tid < 16) wtab[tid] = FMT == 1 ? kNF4g[tid] : (float)(tid - 8);
@@ -60,6 +85,21 @@ __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
   const int w_n = min(n0 + w_row, a.N - 1);
 
   auto gload = [&](int kt) {
+    if (GLDS) {  // K % 64 == 0 here (host): X tile (and bf16 W tile) straight into LDS buffer kt & 1
+      unsigned char* A = lds + (kt & 1) * (2 * TILE_BYTES);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r0 = (wave * 4 + i) * 8;
+        glds_rows8(a.x, a.K, m0 + r0, a.M - 1, kt * BK, A + r0 * 128, lane);
+        if (FMT == 2) glds_rows8((const uint16_t*)a.qw, a.K, n0 + r0, a.N - 1, kt * BK, A + TILE_BYTES + r0 * 128, lane);
+      }
+      if (FMT == 2) return;
+      const int wk = kt * BK + w_half * 32;
+      wq = *(const uint4*)(a.qw + (size_t)w_n * wrow_bytes + wk / 2);
+      const size_t si = (size_t)w_n * groups + wk / a.G;
+      wscale = FMT == 0 ? bf2f(((const uint16_t*)a.sc)[si]) : ((const float*)a.sc)[si];
+      return;
+    }
     // K % 64 == 32 leaves a half tile at the end: its upper X half is zero-filled (so it adds nothing) and its W
     // half re-reads the row start (in bounds, multiplied by those zeros)
     const bool a_in = kt * BK + a_chunk * 8 < a.K;
@@ -83,9 +123,12 @@ __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
   auto lstore = [&](int buf) {
     unsigned char* A = lds + buf * (2 * TILE_BYTES);
     unsigned char* B = A + TILE_BYTES;
+    if (!GLDS) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) *(uint4*)(A + swz(a_row + 32 * i, a_chunk)) = xa[i];
+      for (int i = 0; i < 4; ++i) *(uint4*)(A + swz(a_row + 32 * i, a_chunk)) = xa[i];
+    }
     if (FMT == 2) {
+      if (GLDS) return;
 #pragma unroll
       for (int c = 0; c < 4; ++c) *(uint4*)(B + swz(w_row, w_half * 4 + c)) = wbf[c];
       return;
@@ -97,7 +140,11 @@ __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; e += 2) {
         const uint32_t lo = (wd[c] >> (4 * e)) & 0xF, hi = (wd[c] >> (4 * e + 4)) & 0xF;
-        o4[e / 2] = pack2(__fmul_rn(wtab[lo], wscale), __fmul_rn(wtab[hi], wscale));
+        if (FMT == 0) {  // int4-g: value = nibble - 8, exact in fp32 (no LDS table read on this path)
+          o4[e / 2] = pack2(__fmul_rn((float)((int)lo - 8), wscale), __fmul_rn((float)((int)hi - 8), wscale));
+        } else {
+          o4[e / 2] = pack2(__fmul_rn(wtab[lo], wscale), __fmul_rn(wtab[hi], wscale));
+        }
       }
       *(uint4*)(B + swz(w_row, w_half * 4 + c)) = make_uint4(o4[0], o4[1], o4[2], o4[3]);
     }
@@ -112,6 +159,7 @@ __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
   gload(0);
   __syncthreads();  // nf4 table
   lstore(0);
+  if (GLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   const int fr = lane & 15, fk = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
@@ -133,6 +181,7 @@ __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     if (kt + 1 < nk) lstore(cur ^ 1);
+    if (GLDS) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-direct loads have landed
     __syncthreads();
   }
 
@@ -166,7 +215,8 @@ extern "C" int lga_bf16_gemm(const void* x, const void* weight, const void* bias
   lga::GemmArgs a{(const uint16_t*)x, (const uint8_t*)weight, nullptr, (const uint16_t*)bias,
                   (const uint16_t*)residual, (uint16_t*)y, M, N, K, 32};
   const dim3 grid((N + lga::BN - 1) / lga::BN, (M + lga::BM - 1) / lga::BM);
-  lga::gemm_q4_kernel<2><<<grid, 256, 0, stream>>>(a);
+  if (LGA_GEMM_GLDS && K % lga::BK == 0) lga::gemm_q4_kernel<2, true><<<grid, 256, 0, stream>>>(a);
+  else lga::gemm_q4_kernel<2, false><<<grid, 256, 0, stream>>>(a);
   LGA_LAUNCH_RETURN();
 }
 
@@ -180,7 +230,13 @@ extern "C" int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* sc
   lga::GemmArgs a{(const uint16_t*)x, qweight, scales, (const uint16_t*)bias, (const uint16_t*)residual,
                   (uint16_t*)y, M, N, K, group};
   const dim3 grid((N + lga::BN - 1) / lga::BN, (M + lga::BM - 1) / lga::BM);
-  if (fmt == 0) lga::gemm_q4_kernel<0><<<grid, 256, 0, stream>>>(a);
-  else lga::gemm_q4_kernel<1><<<grid, 256, 0, stream>>>(a);
+  const bool glds = LGA_GEMM_GLDS && K % lga::BK == 0;
+  if (fmt == 0) {
+    if (glds) lga::gemm_q4_kernel<0, true><<<grid, 256, 0, stream>>>(a);
+    else lga::gemm_q4_kernel<0, false><<<grid, 256, 0, stream>>>(a);
+  } else {
+    if (glds) lga::gemm_q4_kernel<1, true><<<grid, 256, 0, stream>>>(a);
+    else lga::gemm_q4_kernel<1, false><<<grid, 256, 0, stream>>>(a);
+  }
   LGA_LAUNCH_RETURN();
 }

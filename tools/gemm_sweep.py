@@ -7,6 +7,10 @@ import torch
 REPO = Path(__file__).resolve().parent.parent
 sys.path[:0] = [str(REPO / "lit-gpt_amd"), str(REPO)]
 from lit_gpt import ops  # noqa: E402
+import os  # noqa: E402
+
+if os.environ.get("GEMM_LIB"):  # lab build of the library
+    ops.LIB_PATH = Path(os.environ["GEMM_LIB"])
 
 SHAPES = {"qkv": (12288, 4096), "o_proj": (4096, 4096), "fc": (11008, 4096), "down": (4096, 11008)}
 
@@ -15,17 +19,27 @@ def main(M=2048):
     dev = torch.device("cuda")
     tot_us, tot_fl = 0.0, 0.0
     for name, (N, K) in SHAPES.items():
-        for fmt, group in ((0, 128), (1, 64)):
-            q, s = ops.quantize(torch.randn(N, K, device=dev) * 0.02, fmt, group)
+        for fmt, group in ((0, 128), (1, 64), (2, 0)):
+            w = torch.randn(N, K, device=dev) * 0.02
+            if fmt == 2:
+                wb = w.bfloat16()
+            else:
+                q, s = ops.quantize(w, fmt, group)
             x = torch.randn(M, K, device=dev).bfloat16()
             y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+
+            def call():
+                if fmt == 2:
+                    ops.bf16_gemm(x, wb, out=y)
+                else:
+                    ops.q4_gemm(x, q, s, N, K, group, fmt, out=y)
             for _ in range(3):
-                ops.q4_gemm(x, q, s, N, K, group, fmt, out=y)
+                call()
             torch.cuda.synchronize()
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
                 for _ in range(10):
-                    ops.q4_gemm(x, q, s, N, K, group, fmt, out=y)
+                    call()
             g.replay()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
