@@ -363,29 +363,53 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const uint16_t* __res
   const uint16_t* vbase = vc + (size_t)g * max_seq * HS;
   constexpr int CPR = HS / 8;                // 16-B chunks per key row
   constexpr int LPT = KB * CPR / 256;        // chunks per thread per tile (K and V each)
-  for (int k0 = 0; k0 < kend; k0 += KB) {
-    // stage K (row-major, swizzled) and V^T
-    uint4 kr[LPT], vr[LPT];
+  constexpr bool VPAIR = LPT == 2;
+  // K / V tiles are register-staged one tile ahead: tile k0 + KB's global loads are in flight while tile k0 is
+  // multiplied, so each tile costs its MFMA + softmax time, not a global-load round trip
+  // scores in the log2 domain: exp(s * scale - m) = exp2(s * scale * log2(e) - m'), one v_exp_f32 per element
+  const float sl2 = scale * 1.4426950408889634f;
+  uint4 kr[LPT], vr[LPT];
+  auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i, row = c / CPR, ch = c % CPR;
       const int key = min(k0 + row, max_seq - 1);
       kr[i] = *(const uint4*)(kbase + (size_t)key * HS + ch * 8);
-      vr[i] = *(const uint4*)(vbase + (size_t)key * HS + ch * 8);
+      // V: with two chunks per thread, a thread takes keys 2kp, 2kp+1 of one hs chunk so V^T is written as
+      // (key pair) 32-bit words; otherwise the same chunks as K
+      const int vkey = VPAIR ? min(k0 + 2 * (tid / CPR) + i, max_seq - 1) : key;
+      const int vch = VPAIR ? tid % CPR : ch;
+      vr[i] = *(const uint4*)(vbase + (size_t)vkey * HS + vch * 8);
     }
+  };
+  gload(0);
+  for (int k0 = 0; k0 < kend; k0 += KB) {
+    // stage K (row-major, swizzled) and V^T
     __syncthreads();  // previous tile's LDS reads are done
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int c = tid + 256 * i, row = c / CPR, ch = c % CPR;
       *(uint4*)(k_lds + (HS == 128 ? swz256(row, ch) : row * HS * 2 + 16 * (ch ^ (row & 7)))) = kr[i];
-      const uint32_t d[4] = {vr[i].x, vr[i].y, vr[i].z, vr[i].w};
+      if (!VPAIR) {
+        const uint32_t d[4] = {vr[i].x, vr[i].y, vr[i].z, vr[i].w};
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int col = ch * 8 + e;  // hs index -> row of V^T
-        const uint16_t val = (uint16_t)(e & 1 ? d[e >> 1] >> 16 : d[e >> 1] & 0xFFFF);
-        *(uint16_t*)(vt_lds + swz64(col, row >> 3) + (row & 7) * 2) = val;
+        for (int e = 0; e < 8; ++e) {
+          const int col = ch * 8 + e;  // hs index -> row of V^T
+          const uint16_t val = (uint16_t)(e & 1 ? d[e >> 1] >> 16 : d[e >> 1] & 0xFFFF);
+          *(uint16_t*)(vt_lds + swz64(col, row >> 3) + (row & 7) * 2) = val;
+        }
       }
     }
+    if (VPAIR) {  // V^T row (hs col) <- 32-bit (key 2kp, key 2kp+1) words: 8 ds_write_b32 instead of 16 b16
+      const int key = 2 * (tid / CPR), ch = tid % CPR;
+      const uint32_t a[4] = {vr[0].x, vr[0].y, vr[0].z, vr[0].w}, b[4] = {vr[1].x, vr[1].y, vr[1].z, vr[1].w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t w = __builtin_amdgcn_perm(b[e >> 1], a[e >> 1], (e & 1) ? 0x07060302u : 0x05040100u);
+        *(uint32_t*)(vt_lds + swz64(ch * 8 + e, key >> 3) + (key & 7) * 2) = w;
+      }
+    }
+    if (k0 + KB < kend) gload(k0 + KB);
     __syncthreads();
     // S = Q K^T for this wave's 16 rows x 32 keys (2 column tiles)
     f32x4_t sacc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
@@ -402,15 +426,15 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const uint16_t* __res
     float pr[2][4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      float s0 = (k0 + fr <= rpos[r]) ? sacc[0][r] * scale : -INFINITY;
-      float s1 = (k0 + 16 + fr <= rpos[r]) ? sacc[1][r] * scale : -INFINITY;
+      float s0 = (k0 + fr <= rpos[r]) ? sacc[0][r] * sl2 : -INFINITY;
+      float s1 = (k0 + 16 + fr <= rpos[r]) ? sacc[1][r] * sl2 : -INFINITY;
       float mx = fmaxf(s0, s1);
 #pragma unroll
       for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
       const float mn = fmaxf(m[r], mx);
-      const float c = mn == -INFINITY ? 1.0f : expf(m[r] - mn);
-      const float e0 = mn == -INFINITY ? 0.0f : expf(s0 - mn);
-      const float e1 = mn == -INFINITY ? 0.0f : expf(s1 - mn);
+      const float c = mn == -INFINITY ? 1.0f : __builtin_amdgcn_exp2f(m[r] - mn);
+      const float e0 = mn == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(s0 - mn);
+      const float e1 = mn == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(s1 - mn);
       float rs = e0 + e1;
 #pragma unroll
       for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off);
