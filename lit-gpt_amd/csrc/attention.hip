@@ -308,7 +308,10 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + 16 * (chunk ^ ((row >> 2) & 3)); }
 __device__ __forceinline__ int swz256(int row, int chunk) { return row * 256 + 16 * (chunk ^ (row & 15)); }
 
-template <int HS>
+#ifndef LGA_PREFILL_MB
+#define LGA_PREFILL_MB 1  // 2 (128 rows per workgroup, K/V fragments shared) measured 365 vs 297 us: 212 VGPRs, 1 wave/SIMD
+#endif
+template <int HS, int MB>
 __global__ void __launch_bounds__(256) attn_prefill_kernel(const uint16_t* __restrict__ q,
                                                            const uint16_t* __restrict__ kc,
                                                            const uint16_t* __restrict__ vc,
@@ -320,44 +323,51 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const uint16_t* __res
   constexpr int NT = HS / 16;     // output column tiles
   __shared__ __attribute__((aligned(16))) unsigned char k_lds[KB * HS * 2];
   __shared__ __attribute__((aligned(16))) unsigned char vt_lds[HS * KB * 2];
-  __shared__ __attribute__((aligned(16))) unsigned char p_lds[4][16 * KB * 2];
+  __shared__ __attribute__((aligned(16))) unsigned char p_lds[4][MB][16 * KB * 2];
   __shared__ long s_kmax;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int fr = lane & 15, fk = lane >> 4;
   const int h = blockIdx.y, g = h / (n_head / G);
-  const int q0 = blockIdx.x * 64, qw = q0 + wave * 16;
+  const int q0 = blockIdx.x * (64 * MB), qw = q0 + wave * (16 * MB);  // wave rows qw + 16 mb + (0..15)
 
   // the block's key range: max position over its rows
   if (tid < 64) {
-    long pm = tid < T - q0 ? input_pos[q0 + tid] : -1;
+    long pm = -1;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) pm = max(pm, tid + 64 * i < T - q0 ? (long)input_pos[q0 + tid + 64 * i] : -1L);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) pm = max(pm, (long)__shfl_xor(pm, o));
     if (tid == 0) s_kmax = min(pm, (long)max_seq - 1);
   }
-  // Q fragments (A operand): row fr of this wave, k-slice ks*32 + fk*8
-  bf16x8_t qa[KS];
-  const int qrow = min(qw + fr, T - 1);
+  // Q fragments (A operand): row fr of each 16-row block, k-slice ks*32 + fk*8
+  bf16x8_t qa[MB][KS];
+  long rpos[MB][4];  // positions of the 4 accumulator rows this lane holds per block
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks)
-    qa[ks] = *(const bf16x8_t*)(q + ((size_t)qrow * n_head + h) * HS + ks * 32 + fk * 8);
-  // positions of the 4 accumulator rows this lane holds
-  long rpos[4];
+  for (int mb = 0; mb < MB; ++mb) {
+    const int qrow = min(qw + 16 * mb + fr, T - 1);
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int t = qw + fk * 4 + r;
-    rpos[r] = t < T ? input_pos[t] : -1;
+    for (int ks = 0; ks < KS; ++ks)
+      qa[mb][ks] = *(const bf16x8_t*)(q + ((size_t)qrow * n_head + h) * HS + ks * 32 + fk * 8);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int t = qw + 16 * mb + fk * 4 + r;
+      rpos[mb][r] = t < T ? input_pos[t] : -1;
+    }
   }
   __syncthreads();
   const int kend = (int)s_kmax + 1;
 
-  f32x4_t o[NT];
+  f32x4_t o[MB][NT];
+  float m[MB][4], l[MB][4];
 #pragma unroll
-  for (int j = 0; j < NT; ++j) o[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-  float m[4], l[4];
+  for (int mb = 0; mb < MB; ++mb) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    m[r] = -INFINITY;
-    l[r] = 0.f;
+    for (int j = 0; j < NT; ++j) o[mb][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      m[mb][r] = -INFINITY;
+      l[mb][r] = 0.f;
+    }
   }
   const uint16_t* kbase = kc + (size_t)g * max_seq * HS;
   const uint16_t* vbase = vc + (size_t)g * max_seq * HS;
@@ -411,8 +421,10 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const uint16_t* __res
     }
     if (k0 + KB < kend) gload(k0 + KB);
     __syncthreads();
-    // S = Q K^T for this wave's 16 rows x 32 keys (2 column tiles)
-    f32x4_t sacc[2] = {f32x4_t{0.f, 0.f, 0.f, 0.f}, f32x4_t{0.f, 0.f, 0.f, 0.f}};
+    // S = Q K^T for this wave's MB x 16 rows x 32 keys (2 column tiles); every K fragment feeds MB MFMAs
+    f32x4_t sacc[MB][2];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) sacc[mb][0] = sacc[mb][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -420,59 +432,69 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(const uint16_t* __res
         const int krow = j * 16 + fr, ch = ks * 4 + fk;
         const bf16x8_t kb =
             *(const bf16x8_t*)(k_lds + (HS == 128 ? swz256(krow, ch) : krow * HS * 2 + 16 * (ch ^ (krow & 7))));
-        sacc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[ks], kb, sacc[j], 0, 0, 0);
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          sacc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[mb][ks], kb, sacc[mb][j], 0, 0, 0);
       }
-    // online softmax per row (lane holds rows fk*4+r, key columns fr and 16+fr)
-    float pr[2][4];
+    // online softmax per row (lane holds rows fk*4+r of each block, key columns fr and 16+fr); P -> LDS (bf16,
+    // [16 rows][32 keys] per block) -> A fragments
+    bf16x8_t pa[MB];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float s0 = (k0 + fr <= rpos[r]) ? sacc[0][r] * sl2 : -INFINITY;
-      float s1 = (k0 + 16 + fr <= rpos[r]) ? sacc[1][r] * sl2 : -INFINITY;
-      float mx = fmaxf(s0, s1);
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-      const float mn = fmaxf(m[r], mx);
-      const float c = mn == -INFINITY ? 1.0f : __builtin_amdgcn_exp2f(m[r] - mn);
-      const float e0 = mn == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(s0 - mn);
-      const float e1 = mn == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(s1 - mn);
-      float rs = e0 + e1;
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off);
-      l[r] = l[r] * c + rs;
-      m[r] = mn;
-#pragma unroll
-      for (int j = 0; j < NT; ++j) o[j][r] *= c;
-      pr[0][r] = e0;
-      pr[1][r] = e1;
-    }
-    // P -> LDS (bf16, [16 rows][32 keys]) -> A fragments
-    unsigned char* pl = p_lds[wave];
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int mb = 0; mb < MB; ++mb) {
+      float pr[2][4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = fk * 4 + r, key = j * 16 + fr;
-        *(uint16_t*)(pl + swz64(row, key >> 3) + (key & 7) * 2) = f2bf(pr[j][r]);
+        float s0 = (k0 + fr <= rpos[mb][r]) ? sacc[mb][0][r] * sl2 : -INFINITY;
+        float s1 = (k0 + 16 + fr <= rpos[mb][r]) ? sacc[mb][1][r] * sl2 : -INFINITY;
+        float mx = fmaxf(s0, s1);
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+        const float mn = fmaxf(m[mb][r], mx);
+        const float c = mn == -INFINITY ? 1.0f : __builtin_amdgcn_exp2f(m[mb][r] - mn);
+        const float e0 = mn == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(s0 - mn);
+        const float e1 = mn == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(s1 - mn);
+        float rs = e0 + e1;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off);
+        l[mb][r] = l[mb][r] * c + rs;
+        m[mb][r] = mn;
+#pragma unroll
+        for (int j = 0; j < NT; ++j) o[mb][j][r] *= c;
+        pr[0][r] = e0;
+        pr[1][r] = e1;
       }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed (the tile is wave-private)
+      unsigned char* pl = p_lds[wave][mb];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = fk * 4 + r, key = j * 16 + fr;
+          *(uint16_t*)(pl + swz64(row, key >> 3) + (key & 7) * 2) = f2bf(pr[j][r]);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed (the tiles are wave-private)
     __builtin_amdgcn_wave_barrier();
-    const bf16x8_t pa = *(const bf16x8_t*)(pl + swz64(fr, fk));
-    // O += P V
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) pa[mb] = *(const bf16x8_t*)(p_lds[wave][mb] + swz64(fr, fk));
+    // O += P V; every V fragment feeds MB MFMAs
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const bf16x8_t vb = *(const bf16x8_t*)(vt_lds + swz64(j * 16 + fr, fk));
-      o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[j], 0, 0, 0);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) o[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[mb], vb, o[mb][j], 0, 0, 0);
     }
   }
   // y[t][h*HS + col] = O / l
 #pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const int t = qw + fk * 4 + r;
-    if (t >= T) continue;
-    const float inv = 1.0f / l[r];
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
-    for (int j = 0; j < NT; ++j) y[((size_t)t * n_head + h) * HS + j * 16 + fr] = f2bf(o[j][r] * inv);
-  }
+    for (int r = 0; r < 4; ++r) {
+      const int t = qw + 16 * mb + fk * 4 + r;
+      if (t >= T) continue;
+      const float inv = 1.0f / l[mb][r];
+#pragma unroll
+      for (int j = 0; j < NT; ++j) y[((size_t)t * n_head + h) * HS + j * 16 + fr] = f2bf(o[mb][j][r] * inv);
+    }
 }
 
 // (keys in flight per row group, waves per workgroup) by q_per_kv; -D overrides are for tools/attn_sweep.py
@@ -529,13 +551,14 @@ extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_c
   LGA_CHECK_ARG(n_splits >= 1 && n_splits <= 256, "lga_attention: n_splits must be in [1, 256]");
   LGA_CHECK_ARG(n_splits == 1 || (workspace && counters), "lga_attention: split attention needs workspace + counters");
   if (T >= 16 && n_splits == 1 && (head_size == 128 || head_size == 64)) {  // prefill: flash attention on MFMA
-    const dim3 grid((T + 63) / 64, n_head);
+    constexpr int MB = LGA_PREFILL_MB;  // 16-row query blocks per wave (64 * MB rows per workgroup)
+    const dim3 grid((T + 64 * MB - 1) / (64 * MB), n_head);
     if (head_size == 128)
-      lga::attn_prefill_kernel<128><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+      lga::attn_prefill_kernel<128, MB><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
                                                               (const uint16_t*)v_cache, input_pos, (uint16_t*)y, T,
                                                               n_head, n_query_groups, max_seq, scale);
     else
-      lga::attn_prefill_kernel<64><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+      lga::attn_prefill_kernel<64, MB><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
                                                              (const uint16_t*)v_cache, input_pos, (uint16_t*)y, T,
                                                              n_head, n_query_groups, max_seq, scale);
     LGA_LAUNCH_RETURN();
