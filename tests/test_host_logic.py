@@ -226,3 +226,16 @@ def test_topk_order_restatement_matches_cpu_torch_topk():
         vals = [rng.gauss(0, 1) if pool is None else rng.choice(pool) for _ in range(n)]
         t = torch.tensor(vals, dtype=torch.bfloat16).view(1, -1)
         assert topk_order(t[0].float().tolist(), k) == torch.topk(t, k).indices[0].tolist(), (vals, k)
+
+
+def test_decode_attention_split_heuristic_per_tp_rank():
+    """Sequence splits chosen for T = 1 attention (ops.decode_splits): 8 for Llama-2-7B's 32 groups, at most 16 for
+    the few groups a tensor-parallel rank keeps (measured on MI355X, tools/attn_sweep.py)."""
+    from lit_gpt import ops
+
+    assert ops.decode_splits(32, 1, 128, 2304) == 8  # 7B TP=1
+    assert ops.decode_splits(16, 1, 128, 2304) == 16  # 7B TP=2
+    assert ops.decode_splits(4, 1, 128, 2304) == 16  # 7B TP=8 (was 64: 10.9 vs 7.8 us)
+    assert ops.decode_splits(1, 8, 128, 2304) == 16  # 70B TP=8: one KV group, 8 heads per group
+    assert ops.decode_splits(4, 4, 128, 32768) == 16  # Mixtral TP=2 at 32k context
+    assert ops.decode_splits(4, 1, 128, 64) == 4  # short caches: >= 16 keys per split
