@@ -77,3 +77,40 @@ def _reference_schedule(produced, stop_tokens):
             out += toks[yield_i:t]
             yield_i = t
     return out
+
+
+@torch.inference_mode()
+def test_converted_hf_checkpoint_generates_same_tokens(tmp_path, monkeypatch):
+    """HF-layout shards -> scripts/convert_hf_checkpoint.py -> generate/base.py's loader: the same greedy tokens
+    as the model built straight from the lit-layout weights."""
+    from safetensors.torch import save_file
+
+    import scripts.convert_hf_checkpoint as cth
+    from generate.base import build_model, generate
+    from lit_gpt import Config
+    from test_convert_hf_checkpoint import _hf_state
+
+    cfg = _cfg("gqa")
+    sd = synth.state_dict(cfg, seed=47)
+    lit = {k: torch.from_numpy(v) for k, v in sd.items()}
+    save_file({k: v.contiguous() for k, v in _hf_state(cfg, lit).items()}, str(tmp_path / "model.safetensors"))
+    name, kw = "Llama-2-70b-hf", dict(n_layer=2, n_embd=1024, n_head=8, n_query_groups=2, intermediate_size=512,
+                                      vocab_size=1000, padding_multiple=64, block_size=256)
+
+    class TinyConfig(Config):
+        @classmethod
+        def from_name(cls, n, **k):
+            return Config.from_name(n, **kw)
+
+    monkeypatch.setattr(cth, "Config", TinyConfig)
+    cth.convert_hf_checkpoint(checkpoint_dir=tmp_path, model_name=name)
+    T, N = 16, 12
+    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=47)).to(DEV)
+    ref_model = build_gpu_model(cfg, sd, "int4-g128", T + N)
+    y_ref = generate(ref_model, prompt, T + N, temperature=0.0).cpu()
+    del ref_model
+    loaded_cfg = Config.from_json(tmp_path / "lit_config.json")
+    model = build_model(loaded_cfg, quantize="int4-g128", device=DEV, checkpoint_path=tmp_path / "lit_model.pth",
+                        max_seq_length=T + N, rope_positions="exact")
+    y = generate(model, prompt, T + N, temperature=0.0).cpu()
+    assert torch.equal(y, y_ref)
