@@ -57,27 +57,6 @@ int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const void* scale
 int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const void* bias, const void* residual,
                 void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
 
-/* -- chained decode GEMVs: attn.proj+residual -> RMSNorm+fc_1||fc_2+SwiGLU -> mlp.proj+residual -> RMSNorm+the
- *    next GEMV (next block's fused qkv, or ln_f + lm_head) in ONE launch (lit_gpt/model.py:591-592, :656,
- *    :712-716, :619 / :518-519; the GEMVs that bnb gemv_4bit runs one by one). Stages hand off inside the launch
- *    (csrc/chain.hip); int4-g (fmt 0) weights only. ------------------------------------------------------------ */
-typedef struct lga_chain_stage {
-  const void* x;             /* (K) bf16 input: stage 0 = attention output; stage s > 0 = y of stage s-1 */
-  const uint8_t* qweight;    /* (N, K/2) */
-  const void* scales;        /* (N, K/group) bf16 */
-  const uint8_t* qweight2;   /* stage 1: fc_2 (fc_1 is qweight); else NULL */
-  const void* scales2;
-  const void* residual;      /* stage 0: block input; stage 2: y of stage 0; else NULL */
-  const void* norm_weight;   /* stage 1: norm_2; stage 3: next norm_1 / ln_f; else NULL */
-  float norm_eps;
-  void* y;                   /* (N) bf16 */
-  int N, K, group;
-} lga_chain_stage;
-/* stages: exactly 4, in the order above; counters: lga_decode_chain_counter_words() uint32, zeroed once before the
- * first launch (every launch re-arms them); err: bit 0 set when an in-launch wait timed out (results invalid). */
-int lga_q4_decode_chain(const lga_chain_stage* stages, unsigned* counters, unsigned* err, lga_stream_t stream);
-size_t lga_decode_chain_counter_words(void);
-
 /* -- unquantized bf16 Linears (BASELINE config 2: no --quantize, precision bf16-true; the reference runs
  *    F.linear on the bf16 nn.Linear weight, lit_gpt/model.py:619, :656, :712-716, :519) ------------------- */
 /* decode GEMV y (N) = x (K) . W (N, K)^T [+bias] [+residual]; optional fused RMSNorm of x (as lga_q4_gemv) */
@@ -129,24 +108,6 @@ int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, co
                                const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, void* y,
                                float* workspace, unsigned* counters, int n_head, int n_query_groups, int head_size,
                                int rope_n_elem, int max_seq, int n_splits, float scale, lga_stream_t stream);
-
-/* -- one Llama decode block (Block.forward, lit_gpt/model.py:572-593, T = 1) in ONE persistent launch --------
- * h_out = h_mid + mlp(norm_2(h_mid)), h_mid = h_in + attn(norm_1(h_in)) with RoPE + KV append of position *pos
- * (model.py:609-665, 712-716, 767-795). Weights int4-g128 (LGA_FMT_Q4G, group 128): wq (qkv), wo (attn.proj),
- * w1/w2 (fc_1/fc_2), wd (mlp.proj) with their bf16 scales. Scratch: qkv ((H+2G)*hs), y (H*hs), act (I) bf16,
- * attn_ws (H * (n_cu/G) * (hs+4) fp32), counters (lga_decode_layer_counters(G) uint32, zeroed once; re-armed
- * by the kernel), err (1 uint32: bit 0 = a hand-off wait timed out, results invalid). Grid = one workgroup per CU
- * (n_cu = compute units of the device). Geometry limits (checked, error otherwise): head_size 128, q_per_kv 1,
- * n_cu a multiple of n_query_groups dividing the qkv rows and n_embd, the qkv rows of one group = that group's
- * attention workgroups, n_embd 4096, intermediate <= 12288. */
-size_t lga_decode_layer_counters(int n_query_groups);
-int lga_decode_layer(const void* h_in, void* h_mid, void* h_out, const void* norm1, const void* norm2, float eps,
-                     const uint8_t* wq, const void* sq, const uint8_t* wo, const void* so, const uint8_t* w1,
-                     const void* s1, const uint8_t* w2, const void* s2, const uint8_t* wd, const void* sd,
-                     void* k_cache, void* v_cache, const float* cos, const float* sin, int rope_rows,
-                     const int64_t* pos, void* qkv_scratch, void* y_scratch, void* act_scratch, float* attn_ws,
-                     unsigned* counters, unsigned* err, int n_embd, int intermediate, int n_head,
-                     int n_query_groups, int head_size, int max_seq, float scale, int n_cu, lga_stream_t stream);
 
 /* -- sparse MoE (LLaMAMoE.forward, lit_gpt/model.py:727-743; Mixtral) ------------------------------------------
  * lga_moe_route: per token row of router logits [T][n_expert] bf16 -> expert_ids [T][k] int32 and probs [T][k]

@@ -35,7 +35,7 @@ constexpr int kGemvNW = LGA_GEMV_NW;
 template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES>
 __global__ void __launch_bounds__(kGemvNW * 64) gemv_q4_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  gemv_q4_body<RPR, CPT, FMT, DUAL, NORM, RES, false, kGemvNW>(a, blockIdx.x, smem, nullptr);
+  gemv_q4_body<RPR, CPT, FMT, DUAL, NORM, RES, kGemvNW>(a, blockIdx.x, smem);
 }
 
 template <int RPR, int CPT, int FMT, bool DUAL>

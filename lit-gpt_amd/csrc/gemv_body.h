@@ -1,5 +1,4 @@
-// Decode GEMV body over packed 4-bit weights, shared by the single-GEMV launches (gemv.hip) and the chained
-// out-projection + MLP + next-GEMV launch (chain.hip). Design notes: gemv.hip.
+// Decode GEMV body over packed 4-bit weights (gemv.hip launches it; design notes there).
 #pragma once
 #include "decode_ops.h"
 
@@ -47,90 +46,11 @@ struct GemvArgs {
   int xs, n_expert, slots;
 };
 
-// In-launch hand-off between chained GEMV stages (lga_q4_decode_chain, chain.hip): every stage owns a contiguous
-// range of workgroups, dispatched in order, and counts its finished workgroups in kChainShards counters (256 B
-// apart; workgroup b of a stage adds to shard b % kChainShards). MI355X_MICROARCH.md "Valid forms", row 1: the
-// producer stores its outputs write-through (sc1, 4/8-B), every storing wave drains them (vmcnt(0)), then one
-// lane adds to its shard after a workgroup barrier; the consumer's wave 0 polls every shard with sc1 loads and
-// the other waves load after a workgroup barrier; all loads of handed-off bytes are sc1 loads.
-constexpr int kChainShards = 16;
-constexpr int kChainStride = 64;  // uint32 per counter
-
-struct ChainLink {
-  const unsigned* wait_cnt;  // shard counters of the producing stage (null: inputs predate the launch)
-  int wait_wgs;              // workgroups of the producing stage
-  unsigned* post_cnt;        // this stage's shard counters
-  unsigned* err;             // bit 0: a wait timed out (the launch's results are invalid)
-};
-
-__device__ __forceinline__ unsigned chain_ld(const unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // global_load_dword sc1
-}
-
-// wave 0 polls until every shard of the producing stage has counted all its workgroups (bounded: ~20 ms, then the
-// error bit is set and the launch carries on so it always drains); then the workgroup barrier releases the rest
-__device__ __forceinline__ void chain_wait(const ChainLink& L) {
-  if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const int sh = lane < kChainShards ? lane : 0;
-    const unsigned target = lane < kChainShards
-                                ? (unsigned)(L.wait_wgs / kChainShards + (sh < L.wait_wgs % kChainShards ? 1 : 0))
-                                : 0u;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (true) {
-      const unsigned v = chain_ld(L.wait_cnt + sh * kChainStride);
-      if (__all(v >= target)) break;
-      __builtin_amdgcn_s_sleep(2);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {
-        if (lane == 0) __hip_atomic_fetch_or(L.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-}
-
-// 16-B activation chunk loaded as four sc1 dwords (written by another workgroup of this launch)
-__device__ __forceinline__ uint4 chain_ld16(const void* p) {
-  const unsigned* q = (const unsigned*)p;
-  return make_uint4(chain_ld(q), chain_ld(q + 1), chain_ld(q + 2), chain_ld(q + 3));
-}
-
-// Gather the wave's RPR row results (held after the butterfly by the first lane of each value group) into lane 0
-// and store them as one 4-B (RPR 2) or 8-B (RPR 4) sc1 store. DUAL: value index 2*row (+1 = fc_2 partner).
-template <int R>
-__device__ __forceinline__ int bfly_lane(int vi) {  // first lane of value index vi (inverse of bfly_index)
-  return R == 8 ? ((vi >> 2) & 1) * 32 + ((vi >> 1) & 1) * 16 + (vi & 1) * 8
-                : (R == 4 ? ((vi >> 1) & 1) * 32 + (vi & 1) * 16 : (vi & 1) * 32);
-}
-template <int RPR, int R>
-__device__ __forceinline__ void chain_store(uint16_t* y, uint16_t v, int lane, bool dual, bool in_range) {
-  static_assert(RPR == 2 || RPR == 4, "chained stages store 2 or 4 rows per wave");
-  uint32_t w[RPR / 2];
-#pragma unroll
-  for (int r = 0; r < RPR; r += 2) {
-    const int l0 = bfly_lane<R>(dual ? 2 * r : r), l1 = bfly_lane<R>(dual ? 2 * (r + 1) : r + 1);
-    const uint32_t a0 = (uint32_t)__shfl((int)v, l0) & 0xFFFFu, a1 = (uint32_t)__shfl((int)v, l1) & 0xFFFFu;
-    w[r / 2] = a0 | (a1 << 16);
-  }
-  if (lane == 0 && in_range) {
-    if (RPR == 4) {
-      const uint64_t q = (uint64_t)w[0] | ((uint64_t)w[RPR / 2 - 1] << 32);
-      __hip_atomic_store((uint64_t*)y, q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store((uint32_t*)y, w[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// One wave of a decode GEMV (see gemv.hip for the design). CHAIN: the workgroup is part of a chained launch —
-// weights are issued first, then the producing stage is awaited, activations / residual are read with sc1 loads,
-// the wave's RPR outputs leave as ONE 4/8-B sc1 store from lane 0, and the workgroup counts itself in its shard.
-// Returns (CHAIN, thread 0) the shard counter's value before this workgroup's add; 0 otherwise.
-// NW waves per workgroup (each its own row slot); the workgroup stages x once for all of them.
-template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, bool CHAIN, int NW = 4>
-__device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned char* smem, const ChainLink* link) {
-  if (!CHAIN && a.eidx) {  // wave-uniform: one scalar load of the routed expert id, then plain pointer offsets
+// One wave of a decode GEMV (see gemv.hip for the design). NW waves per workgroup (each its own row slot); the
+// workgroup stages x once for all of them.
+template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, int NW = 4>
+__device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char* smem) {
+  if (a.eidx) {  // wave-uniform: one scalar load of the routed expert id, then plain pointer offsets
     const long long e = min(max(a.eidx[blockIdx.y], 0), a.n_expert - 1);
     a.qw += e * a.ew;
     a.sc = (const unsigned char*)a.sc + e * a.es;
@@ -157,13 +77,11 @@ __device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned c
 
   // 1. activation (and norm weight) share of this thread: uint4 t, t+NT, ... (clamped, branch-free)
   uint4 xr[XI], nr[XI];
-  if (!CHAIN) {
 #pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int u = min(t + NT * i, n8 - 1);
-      xr[i] = ((const uint4*)a.x)[u];
-      if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
-    }
+  for (int i = 0; i < XI; ++i) {
+    const int u = min(t + NT * i, n8 - 1);
+    xr[i] = ((const uint4*)a.x)[u];
+    if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
   }
   // 2. every weight / scale / residual load of this wave (rows past N re-read row N-1; never stored), issued in
   //    the order step 4 consumes them (chunk-major, each scale right after its weights): vmcnt retires in order,
@@ -186,22 +104,8 @@ __device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned c
       }
     }
   }
-  if (!CHAIN && RES) res = a.residual[min(row0 + (lane & (RPR - 1)), a.N - 1)];
+  if (RES) res = a.residual[min(row0 + (lane & (RPR - 1)), a.N - 1)];
   __builtin_amdgcn_sched_barrier(0);  // nothing that waits on x may move above the weight loads
-  if constexpr (CHAIN) {
-    if (link->wait_cnt) chain_wait(*link);
-#pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int u = min(t + NT * i, n8 - 1);
-      xr[i] = chain_ld16(a.x + (size_t)u * 8);
-      if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
-    }
-    if (RES) {  // the wave's RPR residual values (N % RPR == 0, checked on the host), one sc1 load
-      const unsigned* rp = (const unsigned*)(a.residual + min(row0, a.N - RPR));
-      const unsigned w0 = chain_ld(rp + ((lane & (RPR - 1)) >> 1));
-      res = (lane & 1) ? (w0 >> 16) : (w0 & 0xFFFFu);
-    }
-  }
   LGA_GTRACE_NOWAIT(1);
 
   // 3. stage x into LDS (RMS-normalised when NORM) while the weights stream
@@ -291,9 +195,7 @@ __device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned c
     const int row = row0 + (vi >> 1);
     const float g = round_bf(silu_f(round_bf(tot)));  // silu(bf16(fc_1 x)) -> bf16
     const uint16_t ob = f2bf(__fmul_rn(g, round_bf(other)));  // * bf16(fc_2 x)
-    if constexpr (CHAIN) {
-      chain_store<RPR, R>(a.y + row0, ob, lane, true, row0 < a.N);
-    } else if ((lane & (GROUP - 1)) == 0 && (vi & 1) == 0 && row < a.N) {
+    if ((lane & (GROUP - 1)) == 0 && (vi & 1) == 0 && row < a.N) {
       a.y[row] = ob;
     }
     LGA_GTRACE(5);
@@ -307,18 +209,9 @@ __device__ __forceinline__ unsigned gemv_q4_body(GemvArgs a, int blk, unsigned c
     } else if (a.bias) {
       o += bf2f(a.bias[min(row, a.N - 1)]);
     }
-    if constexpr (CHAIN) chain_store<RPR, R>(a.y + row0, f2bf(o), lane, false, row0 < a.N);
-    else if ((lane & (GROUP - 1)) == 0 && row < a.N) a.y[row] = f2bf(o);
+    if ((lane & (GROUP - 1)) == 0 && row < a.N) a.y[row] = f2bf(o);
     LGA_GTRACE(5);
   }
-  if constexpr (CHAIN) {  // every storing wave has drained its sc1 store; one lane counts the workgroup
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0)
-      return __hip_atomic_fetch_add(link->post_cnt + (blk % kChainShards) * kChainStride, 1u, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-  }
-  return 0u;
 }
 
 }  // namespace lga

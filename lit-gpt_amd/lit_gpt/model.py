@@ -203,13 +203,6 @@ class Block(nn.Module):
         if not isinstance(self.norm_1, RMSNorm) or not isinstance(self.mlp, (LLaMAMLP, LLaMAMoE)):
             raise NotImplementedError(f"{type(self.mlp).__name__} / {type(self.norm_1).__name__} blocks have no "
                                       "MI355X kernels in this build")
-        # decode token on a single GPU: the whole block is one persistent launch when the geometry allows
-        if (x.size(1) == 1 and input_pos is not None and self._layer_kernel_ok(x)
-                and isinstance(self.attn.kv_cache, KVCache) and cos.size(0) == self.attn.kv_cache.k.size(-2)):
-            try:
-                return self._decode_layer(x, cos, sin, input_pos)
-            except RuntimeError:
-                self._layer_kernel = False  # geometry the kernel does not cover: per-op path from now on
         # residual adds ride the out-projection epilogues unless a hook (TP all-reduce) must see the bare output
         if not self.attn._forward_hooks and not self.mlp._forward_hooks:
             x = self.attn(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x)
@@ -218,62 +211,6 @@ class Block(nn.Module):
         x = ops.add(h.contiguous(), x.contiguous())
         return ops.add(self.mlp(self.norm_2(x)).contiguous(), x)
 
-
-    # lga_decode_layer for T = 1 (None = not decided yet). Opt-in (LGA_DECODE_LAYER=1): measured 72 us per
-    # Llama-2-7B block vs 45 us for the per-op path on MI355X — in-launch hand-offs under a saturated weight
-    # stream cost 5-7 us each (DESIGN.md "Persistent block kernel"); tests force it on explicitly.
-    _layer_kernel: Optional[bool] = None
-
-    def _layer_kernel_ok(self, x: torch.Tensor) -> bool:
-        if self._layer_kernel is None:
-            import os
-
-            from lit_gpt.quantize import QuantLinear
-
-            c = self.config
-            if not isinstance(self.mlp, LLaMAMLP):
-                self._layer_kernel = False
-                return False
-            lins = (self.attn.attn, self.attn.proj, self.mlp.fc_1, self.mlp.fc_2, self.mlp.proj)
-            self._layer_kernel = (
-                os.environ.get("LGA_DECODE_LAYER", "0") == "1" and x.is_cuda
-                and all(isinstance(m, QuantLinear) and m.fmt == 0 and m.group == 128 and m.bias is None for m in lins)
-                and not self.attn._forward_hooks and not self.mlp._forward_hooks
-                and c.head_size == 128 and c.rope_n_elem == 128 and c.n_head == c.n_query_groups
-                and isinstance(self.norm_2, RMSNorm) and self.norm_1.eps == self.norm_2.eps)
-        return bool(self._layer_kernel)
-
-    def _decode_layer(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor,
-                      input_pos: torch.Tensor) -> torch.Tensor:
-        c = self.config
-        kv = self.attn.kv_cache
-        if not isinstance(kv, KVCache):
-            raise TypeError("You need to call `gpt.set_kv_cache()`")
-        if kv.k.dtype != torch.bfloat16:
-            kv.k, kv.v = kv.k.to(torch.bfloat16), kv.v.to(torch.bfloat16)
-        I = self.mlp.fc_1.out_features
-        ws = getattr(self, "_layer_ws", None)
-        if ws is None or ws.key[:5] != (c.n_embd, I, c.n_head, c.n_query_groups, c.head_size) or ws.err.device != x.device:
-            ws = self._layer_ws = ops.DecodeLayerWorkspace(c.n_embd, I, c.n_head, c.n_query_groups, c.head_size,
-                                                           x.device)
-        cos = cos.to(device=x.device, dtype=torch.float32).contiguous()
-        sin = sin.to(device=x.device, dtype=torch.float32).contiguous()
-        y = ops.decode_layer(x.reshape(-1).contiguous(), self, cos, sin, input_pos.reshape(-1)[:1].contiguous(),
-                             kv.k, kv.v, ws)
-        return y.view(1, 1, -1)
-
-
-def decode_layer_errors(model: nn.Module) -> int:
-    """Number of blocks whose lga_decode_layer flagged a timed-out hand-off since the last call (device sync);
-    the flags are cleared. Any non-zero count means those launches produced invalid results."""
-    n = 0
-    with torch.inference_mode():
-        for m in model.modules():
-            ws = getattr(m, "_layer_ws", None)
-            if ws is not None:
-                n += int(ws.err.item() != 0)
-                ws.err.zero_()
-    return n
 
 
 class CausalSelfAttention(nn.Module):

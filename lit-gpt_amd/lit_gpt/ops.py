@@ -49,8 +49,6 @@ SIGNATURES = {
     "lga_swiglu": [_P, _P, _P, _L, _P],
     "lga_attention": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_attention_workspace_bytes": [_I, _I, _I, _I],
-    "lga_decode_layer": [_P] * 5 + [_F] + [_P] * 14 + [_I, _P, _P, _P, _P, _P, _P, _P] + [_I] * 6 + [_F, _I, _P],
-    "lga_decode_layer_counters": [_I],
     "lga_attention_decode_fused": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_argmax": [_P, _I, _P, _P, _P, _P],
     "lga_moe_route": [_P, _I, _I, _I, _P, _P, _P],
@@ -60,17 +58,7 @@ SIGNATURES = {
                                    _P, _I, _I, _I, _I, _I, _P],
     "lga_moe_combine": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
 }
-class ChainStage(ctypes.Structure):
-    """``lga_chain_stage`` of include/litgpt_amd.h."""
-    _fields_ = [("x", _P), ("qweight", _P), ("scales", _P), ("qweight2", _P), ("scales2", _P), ("residual", _P),
-                ("norm_weight", _P), ("norm_eps", _F), ("y", _P), ("N", _I), ("K", _I), ("group", _I)]
-
-
-SIGNATURES["lga_q4_decode_chain"] = [ctypes.POINTER(ChainStage), _P, _P, _P]
-SIGNATURES["lga_decode_chain_counter_words"] = []
-
-_RESTYPES = {"lga_decode_chain_counter_words": ctypes.c_size_t, "lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
-             "lga_decode_layer_counters": ctypes.c_size_t}
+_RESTYPES = {"lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t}
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -170,42 +158,6 @@ def q4_gemm(x, qweight, scales, N, K, group, fmt, *, bias=None, residual=None, o
                                       _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16),
                                       M, N, K, group, fmt, _stream()))
     return y
-
-
-class ChainWorkspace:
-    """Hand-off counters of lga_q4_decode_chain (zeroed once; every launch re-arms them, so they survive HIP-graph
-    replays) and its error word (bit 0: an in-launch wait timed out)."""
-
-    def __init__(self, device) -> None:
-        n = load_library().lga_decode_chain_counter_words()
-        self.counters = torch.zeros(n, dtype=torch.int32, device=device)
-        self.err = torch.zeros(1, dtype=torch.int32, device=device)
-
-
-def q4_decode_chain(y_att, x_in, proj, fc_1, fc_2, norm_2, down, nxt, nxt_norm, ws: ChainWorkspace, out=None):
-    """One launch: h_mid = x_in + proj(y_att); act = silu(fc_1 n) * fc_2 n with n = norm_2(h_mid);
-    h_out = h_mid + down(act); out = nxt(nxt_norm(h_out)). The Linears are int4-g QuantLinear modules; the norms
-    RMSNorm modules. Returns (h_out, out)."""
-    dev = y_att.device
-    C, I = fc_1.in_features, fc_1.out_features
-    h_mid = torch.empty(C, dtype=torch.bfloat16, device=dev)
-    act = torch.empty(I, dtype=torch.bfloat16, device=dev)
-    h_out = torch.empty(C, dtype=torch.bfloat16, device=dev)
-    out = out if out is not None else torch.empty(nxt.out_features, dtype=torch.bfloat16, device=dev)
-
-    def st(x, lin, y, lin2=None, residual=None, norm=None):
-        return ChainStage(_dev(x, "x", torch.bfloat16), _dev(lin.qweight, "qweight", torch.uint8),
-                          _dev(lin.scales, "scales"), None if lin2 is None else _dev(lin2.qweight, "qweight2"),
-                          None if lin2 is None else _dev(lin2.scales, "scales2"),
-                          _opt(residual, "residual", torch.bfloat16),
-                          None if norm is None else _dev(norm.weight, "norm_weight", torch.bfloat16),
-                          float(norm.eps) if norm is not None else 0.0, _dev(y, "y", torch.bfloat16),
-                          lin.out_features, lin.in_features, lin.group)
-
-    stages = (ChainStage * 4)(st(y_att, proj, h_mid, residual=x_in), st(h_mid, fc_1, act, lin2=fc_2, norm=norm_2),
-                              st(act, down, h_out, residual=h_mid), st(h_out, nxt, out, norm=nxt_norm))
-    _check(load_library().lga_q4_decode_chain(stages, ws.counters.data_ptr(), ws.err.data_ptr(), _stream()))
-    return h_out, out
 
 
 def bf16_gemv(x, weight, *, bias=None, residual=None, norm_weight=None, eps=1e-5, out=None):
@@ -339,51 +291,6 @@ def num_cus() -> int:
         _check(load_library().lga_device_info(torch.cuda.current_device(), ctypes.byref(n), arch, 64))
         _N_CU = int(n.value)
     return _N_CU
-
-
-class DecodeLayerWorkspace:
-    """Per-block scratch of lga_decode_layer (allocate before graph capture): h_mid, qkv, y, act activations,
-    fp32 attention partials, zeroed hand-off counters (re-armed by the kernel) and the spin-timeout flag."""
-
-    def __init__(self, C: int, I: int, H: int, G: int, hs: int, device) -> None:
-        n_cu = num_cus()
-        bpg = n_cu // G
-        self.key = (C, I, H, G, hs, n_cu)
-        bf = dict(dtype=torch.bfloat16, device=device)
-        self.h_mid = torch.empty(C, **bf)
-        self.qkv = torch.empty((H + 2 * G) * hs, **bf)
-        self.y = torch.empty(H * hs, **bf)
-        self.act = torch.empty(I, **bf)
-        self.partials = torch.empty(H * bpg * (hs + 4), dtype=torch.float32, device=device)
-        self.counters = torch.zeros(int(load_library().lga_decode_layer_counters(G)), dtype=torch.int32, device=device)
-        self.err = torch.zeros(1, dtype=torch.int32, device=device)
-        self.n_cu = n_cu
-
-
-def decode_layer(x, blk, cos, sin, pos, kc, vc, ws: DecodeLayerWorkspace, out=None):
-    """One Llama decode block (T = 1) in a single persistent launch: x (C,) bf16 -> h_out (C,). blk is the Block
-    (its QuantLinear / RMSNorm parameters are read); raises RuntimeError when the geometry is unsupported."""
-    c = blk.config
-    at, mlp = blk.attn, blk.mlp
-    C, I, H, G, hs = c.n_embd, mlp.fc_1.out_features, c.n_head, c.n_query_groups, c.head_size
-    y = out if out is not None else torch.empty(C, dtype=torch.bfloat16, device=x.device)
-    q = at.attn
-    _check(load_library().lga_decode_layer(
-        _dev(x, "x", torch.bfloat16), _dev(ws.h_mid, "h_mid"), _dev(y, "h_out", torch.bfloat16),
-        _dev(blk.norm_1.weight, "norm_1", torch.bfloat16), _dev(blk.norm_2.weight, "norm_2", torch.bfloat16),
-        float(blk.norm_1.eps),
-        _dev(q.qweight, "qkv.qweight"), _dev(q.scales, "qkv.scales"),
-        _dev(at.proj.qweight, "proj.qweight"), _dev(at.proj.scales, "proj.scales"),
-        _dev(mlp.fc_1.qweight, "fc_1.qweight"), _dev(mlp.fc_1.scales, "fc_1.scales"),
-        _dev(mlp.fc_2.qweight, "fc_2.qweight"), _dev(mlp.fc_2.scales, "fc_2.scales"),
-        _dev(mlp.proj.qweight, "mlp.proj.qweight"), _dev(mlp.proj.scales, "mlp.proj.scales"),
-        _dev(kc, "k_cache", torch.bfloat16), _dev(vc, "v_cache", torch.bfloat16),
-        _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32), cos.shape[0],
-        _dev(pos, "pos", torch.int64), _dev(ws.qkv, "qkv"), _dev(ws.y, "y"), _dev(ws.act, "act"),
-        _dev(ws.partials, "partials", torch.float32), _dev(ws.counters, "counters", torch.int32),
-        _dev(ws.err, "err", torch.int32), C, I, H, G, hs, kc.shape[-2], 1.0 / math.sqrt(hs), ws.n_cu,
-        _stream()))
-    return y
 
 
 def decode_fusable(head_size: int, rope_n_elem: int) -> bool:

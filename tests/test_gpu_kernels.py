@@ -488,56 +488,3 @@ def test_routed_expert_gemvs_equal_per_expert_gemvs(ops, fmt, group):
                               group, fmt)
     for s, e in enumerate((3, 1)):
         assert torch.equal(out[s], ops.q4_gemv(act[s].contiguous(), qd[e][0], qd[e][1], K, N, group, fmt))
-
-
-# ------------------------------------------------------------------------------------------------ chained decode GEMVs
-def _qlin(ops, N, K, name, group=128):
-    from lit_gpt.quantize import QuantLinear
-
-    return QuantLinear.from_float(torch.from_numpy(_weights(N, K, name)).to(DEV), None, f"int4-g{group}",
-                                  torch.device(DEV))
-
-
-def _norm(C, name):
-    from lit_gpt.rmsnorm import RMSNorm
-
-    n = RMSNorm(C).to(DEV)
-    with torch.no_grad():
-        n.weight.copy_(torch.from_numpy(1.0 + 0.1 * synth.normal((C,), name, 5, 1.0)))
-    return n.to(torch.bfloat16)
-
-
-@pytest.mark.parametrize("C,I,Nn", [(4096, 11008, 12288), (4096, 11008, 32000), (1024, 2816, 3072), (512, 1376, 768)])
-def test_decode_chain_equals_per_op_gemvs(ops, C, I, Nn):
-    """lga_q4_decode_chain (4 GEMVs handing off inside one launch) == the four per-op launches, bit for bit, on every
-    one of 12 back-to-back launches (in-launch hand-offs must never read stale activations); error word stays 0."""
-    proj, f1, f2, down, nxt = (_qlin(ops, C, C, "cp"), _qlin(ops, I, C, "c1"), _qlin(ops, I, C, "c2"),
-                               _qlin(ops, C, I, "cd"), _qlin(ops, Nn, C, "cn"))
-    n2, nn_ = _norm(C, "cn2"), _norm(C, "cnn")
-    ws = ops.ChainWorkspace(DEV)
-    for it in range(12):
-        y_att = to_dev_bf16(synth.normal((C,), f"ya{it}", 5, 1.0))
-        x_in = to_dev_bf16(synth.normal((C,), f"xi{it}", 5, 1.0))
-        h_out, out = ops.q4_decode_chain(y_att, x_in, proj, f1, f2, n2, down, nxt, nn_, ws)
-        h_mid = ops.q4_gemv(y_att, proj.qweight, proj.scales, C, C, proj.group, 0, residual=x_in)
-        act = ops.q4_gemv_swiglu(h_mid, f1.qweight, f1.scales, f2.qweight, f2.scales, I, C, f1.group, 0,
-                                 norm_weight=n2.weight, eps=n2.eps)
-        h_ref = ops.q4_gemv(act, down.qweight, down.scales, C, I, down.group, 0, residual=h_mid)
-        # the standalone GEMV picks its rows-per-wave by height; the chain's last stage always uses 4 -> the
-        # lm_head-sized case compares through variant 0 (same rows per wave, same reduction order)
-        o_ref = ops.q4_gemv(h_ref, nxt.qweight, nxt.scales, Nn, C, nxt.group, 0, norm_weight=nn_.weight,
-                            eps=nn_.eps, variant=0)
-        torch.cuda.synchronize()
-        assert int(ws.err.item()) == 0
-        assert torch.equal(h_out, h_ref), it
-        assert torch.equal(out, o_ref), it
-
-
-def test_decode_chain_rejects_unchained_stages(ops):
-    C, I = 512, 1376
-    proj, f1, f2, down, nxt = (_qlin(ops, C, C, "cp"), _qlin(ops, I, C, "c1"), _qlin(ops, I, C, "c2"),
-                               _qlin(ops, C, I, "cd"), _qlin(ops, 768, C, "cn"))
-    ws = ops.ChainWorkspace(DEV)
-    y = to_dev_bf16(synth.normal((C,), "ya", 5, 1.0))
-    with pytest.raises(RuntimeError):  # down/fc swapped: shapes do not chain
-        ops.q4_decode_chain(y, y, proj, f1, f2, _norm(C, "a"), f1, nxt, _norm(C, "b"), ws)
