@@ -215,8 +215,9 @@ def cpu_baseline(cfg, threads: int, seconds: float = 15.0):
     S = PROMPT_LEN + 64
     m.set_kv_cache(S)
     for i in range(2):  # fill a 2048-long context cheaply (random K/V; attention cost is what matters)
-        m.cache.k[i][:, :PROMPT_LEN] = torch.randn(small.n_query_groups, PROMPT_LEN, small.head_size).bfloat16()
-        m.cache.v[i][:, :PROMPT_LEN] = torch.randn(small.n_query_groups, PROMPT_LEN, small.head_size).bfloat16()
+        m.cache.write(i, torch.arange(PROMPT_LEN),
+                      torch.randn(small.n_query_groups, PROMPT_LEN, small.head_size).bfloat16(),
+                      torch.randn(small.n_query_groups, PROMPT_LEN, small.head_size).bfloat16())
     tok = torch.tensor([1])
     with torch.inference_mode():
         m.forward(tok, torch.tensor([PROMPT_LEN]))  # warm-up
@@ -403,7 +404,8 @@ def main():
         "load_s": round(load_s, 2),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        # the reference's CPU path on all the host cores this process may run on
+        threads = len(os.sched_getaffinity(0)) or os.cpu_count() or 1
         try:
             result["cpu_baseline"] = cpu_baseline(cfg_full, threads, args.cpu_seconds)
         except Exception as e:  # the baseline is reported, never the target: do not lose the GPU number

@@ -114,9 +114,22 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
 
 @dataclass
 class Cache:
-    """Per-layer K/V for positions written so far (lit_gpt/model.py:776-799); stored un-expanded (G heads)."""
+    """Per-layer K/V for positions written so far (lit_gpt/model.py:776-799); stored un-expanded (G heads).
+
+    ``k`` / ``v`` hold the values in the activation dtype (the reference's cache dtype); ``kf`` / ``vf`` hold the
+    same values widened to fp32 once at append time, so a decode step's attention reads the cache without
+    re-casting (or re-expanding) the whole context every step."""
     k: List[torch.Tensor] = field(default_factory=list)  # (G, S, hs) per layer
     v: List[torch.Tensor] = field(default_factory=list)
+    kf: List[torch.Tensor] = field(default_factory=list)
+    vf: List[torch.Tensor] = field(default_factory=list)
+
+    def write(self, i: int, pos, k: torch.Tensor, v: torch.Tensor) -> None:
+        """KVCache.forward's index_copy_ (model.py:788-795) at positions ``pos`` of layer i; k, v (G, T, hs)."""
+        self.k[i][:, pos] = k
+        self.v[i][:, pos] = v
+        self.kf[i][:, pos] = self.k[i][:, pos].float()
+        self.vf[i][:, pos] = self.v[i][:, pos].float()
 
 
 class OracleGPT:
@@ -145,9 +158,12 @@ class OracleGPT:
                                               self.cfg.rope_condense_ratio, self.rope_pos_dtype)
         c = self.cfg
         S = max_seq_length
+        shape = (c.n_query_groups, S, c.head_size)
         self.cache = Cache(
-            k=[torch.zeros(c.n_query_groups, S, c.head_size, dtype=self.dtype) for _ in range(c.n_layer)],
-            v=[torch.zeros(c.n_query_groups, S, c.head_size, dtype=self.dtype) for _ in range(c.n_layer)])
+            k=[torch.zeros(shape, dtype=self.dtype) for _ in range(c.n_layer)],
+            v=[torch.zeros(shape, dtype=self.dtype) for _ in range(c.n_layer)],
+            kf=[torch.zeros(shape, dtype=torch.float32) for _ in range(c.n_layer)],
+            vf=[torch.zeros(shape, dtype=torch.float32) for _ in range(c.n_layer)])
 
     def _norm(self, prefix: str, x: torch.Tensor) -> torch.Tensor:
         c = self.cfg
@@ -174,21 +190,22 @@ class OracleGPT:
         if input_pos is not None:
             if self.cache is None:
                 raise TypeError("You need to call `gpt.set_kv_cache()`")
-            self.cache.k[i][:, input_pos] = k
-            self.cache.v[i][:, input_pos] = v
+            self.cache.write(i, input_pos, k, v)
             L = int(input_pos.max()) + 1  # keys beyond the last written position are masked out
-            kk, vv = self.cache.k[i][:, :L], self.cache.v[i][:, :L]
+            kk, vv = self.cache.kf[i][:, :L], self.cache.vf[i][:, :L]  # fp32 views, no per-step copy
             allowed = torch.arange(L)[None, :] <= input_pos[:, None]  # (T, L) = mask_cache rows
         else:
-            kk, vv = k, v
+            kk, vv = k.float(), v.float()
+            L = T
             allowed = torch.ones(T, T, dtype=torch.bool).tril()
-        kk = kk.repeat_interleave(qpk, dim=0)  # expand groups to heads (model.py:633-635)
-        vv = vv.repeat_interleave(qpk, dim=0)
+        # the reference expands k/v from G groups to H heads (model.py:633-635); the same math without the copy:
+        # the qpk heads of group g attend g's keys, so fold them into the row dimension of one (G, qpk*T, L) matmul
         scale = 1.0 / math.sqrt(hs)
-        att = (q.float() @ kk.float().transpose(-1, -2)) * scale
-        att = att.masked_fill(~allowed, float("-inf"))
+        qg = q.float().reshape(G, qpk * T, hs)
+        att = torch.matmul(qg, kk.transpose(-1, -2)) * scale
+        att = att.masked_fill(~allowed.repeat(qpk, 1), float("-inf"))
         att = torch.softmax(att, dim=-1)
-        y = (att @ vv.float()).to(self.dtype)  # (H, T, hs)
+        y = torch.matmul(att, vv).to(self.dtype).reshape(H, T, hs)
         y = y.transpose(0, 1).reshape(T, H * hs)
         return self._lin(f"transformer.h.{i}.attn.proj", y)
 
@@ -215,8 +232,10 @@ class OracleGPT:
             return y
         raise NotImplementedError(c._mlp_class)
 
-    def forward(self, idx: torch.Tensor, input_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """GPT.forward (model.py:499-519) for B=1: idx (T,) int -> logits (T, V) in ``dtype``."""
+    def forward(self, idx: torch.Tensor, input_pos: Optional[torch.Tensor] = None,
+                last_only: bool = False) -> torch.Tensor:
+        """GPT.forward (model.py:499-519) for B=1: idx (T,) int -> logits (T, V) in ``dtype`` (``last_only``: the
+        last row only, (1, V) — all that generate samples from, generate/base.py:31)."""
         c = self.cfg
         T = idx.numel()
         if self.max_seq_length < T:
@@ -240,6 +259,8 @@ class OracleGPT:
                     raise NotImplementedError("non-parallel residual and shared attention norm")
                 x = h + x
                 x = self._mlp(i, self._norm(f"{pre}.norm_2", x)) + x
+        if last_only:
+            x = x[-1:]
         x = self._norm("transformer.ln_f", x)
         return self._lin("lm_head", x)
 
