@@ -132,6 +132,23 @@ int lga_q4_gemv_swiglu_experts(const void* x, const uint8_t* qweight1, const voi
 int lga_moe_combine(const void* expert_out, const void* probs, const int32_t* expert_ids, const void* residual,
                     void* y, int T, int k, int C, lga_stream_t stream);
 
+/* -- tensor-parallel all-reduce of decode activations (generate/tp.py:73-74 `all_reduce(outs, "sum", ranks)`,
+ *    the forward hook after every attention / MLP, :53,57,70) over xGMI peer memory -----------------------------
+ * Each rank owns one mailbox of lga_comm_mailbox_bytes(cap) bytes from lga_comm_alloc (uncached device memory,
+ * zeroed; its 64-byte IPC handle goes to the peers, which map it with lga_comm_open). lga_allreduce_bf16:
+ * y[n] = bf16(sum over ranks 0..world-1, in that order, of x_r) (+ residual[n]: y = bf16(bf16(sum) + residual),
+ * the Block residual add, lit_gpt/model.py:591-592), identical bits on every rank. mailboxes: host array of world
+ * device pointers (index rank = this rank's own mailbox); seq_counter: 1 uint32 zeroed once, advanced by every
+ * call (the same call sequence on every rank); err: bit 0 set when a peer's flag did not arrive within ~0.2 s
+ * (results invalid). n % 8 == 0, n <= cap, world <= 8. One workgroup; graph-capturable. */
+size_t lga_comm_mailbox_bytes(int cap);
+int lga_comm_alloc(size_t bytes, void** ptr, void* ipc_handle);
+int lga_comm_open(const void* ipc_handle, void** ptr);
+int lga_comm_close(void* ptr);
+int lga_comm_free(void* ptr);
+int lga_allreduce_bf16(const void* x, const void* residual, void* y, int n, void* const* mailboxes, int rank,
+                       int world, int cap, unsigned* seq_counter, unsigned* err, lga_stream_t stream);
+
 /* -- greedy sampling (generate/base.py:30-47 at temperature 0): lowest index among the maxima; optionally
  *    writes the token (int32) and advances *pos_inout by one (generate/base.py:92) -------------------------- */
 int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,

@@ -99,10 +99,13 @@ def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temp
 
 def build_model(config: Config, *, quantize: Optional[str], device: torch.device, seed: int = 1234,
                 checkpoint_path: Optional[Path] = None, max_seq_length: Optional[int] = None,
-                tp=None, rope_positions: str = "reference") -> GPT:
-    """Instantiate on the meta device, load (or random-init, as GPT._init_weights) the float weights layer by
-    layer on the GPU, optionally shard them (``tp(model)``), quantize every Linear on the device, then build the
-    rope tables and the KV cache. Mirrors generate/base.py:151-171 / generate/tp.py:157-190.
+                fabric=None, rope_positions: str = "reference") -> GPT:
+    """Instantiate on the meta device, then materialise (load, or random-init as GPT._init_weights) the float
+    weights on the GPU in the model's parameter order; with ``fabric`` (world_size / global_rank, generate/tp.py)
+    every block is sharded (``tensor_parallel_block``) and quantized as soon as its weights exist, so a rank holds
+    at most one unsharded block (70B TP=8: ~1.7 GB, not the whole 138 GB model). Then the rope tables and the KV
+    cache. Mirrors generate/base.py:151-171 / generate/tp.py:157-190 (convert_module -> tensor_parallel ->
+    to_device: the values each rank quantizes are its float shard, as there).
 
     ``rope_positions="reference"`` builds the rope tables under a bf16 default dtype, as the reference's
     ``with fabric.init_tensor(): model.max_seq_length = ...`` does under bf16-true / bnb precision
@@ -115,6 +118,14 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
         from lit_gpt.quantize import parse_mode
 
         parse_mode(quantize)  # unsupported modes fail before any weight is materialised
+    tp = None
+    if fabric is not None and fabric.world_size > 1:
+        from generate import tp
+
+        for attr in ("n_head", "n_embd", "n_query_groups"):  # fail before materialising (generate/tp.py:87-90)
+            if getattr(config, attr) % fabric.world_size:
+                raise ValueError(f"This {attr} value ({getattr(config, attr)}) is not evenly divisible by the world "
+                                 f"size ({fabric.world_size})")
     with torch.device("meta"):
         model = GPT(config)
     state = None
@@ -123,8 +134,27 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
         state = state.get("model", state)
     gen = torch.Generator(device=device)
     gen.manual_seed(seed)
+    precision = QuantizedPrecision(quantize) if quantize is not None else None
+
+    def finish(module: torch.nn.Module) -> None:
+        """Shard (TP) and quantize one fully materialised block (or the top-level Linears)."""
+        if tp is not None and hasattr(module, "attn"):
+            tp.tensor_parallel_block(fabric, module)
+        if precision is not None:
+            precision.convert_module(module, device)
+        else:  # bf16-true: the Linears stay nn.Linear; TP row shards are strided views -> own contiguous storage
+            for mod in module.modules():
+                if isinstance(mod, torch.nn.Linear) and not mod.weight.is_contiguous():
+                    mod.weight = torch.nn.Parameter(mod.weight.data.contiguous(), requires_grad=False)
+
+    open_block = None
     for name, p in list(model.named_parameters()):
         mod_name, _, attr = name.rpartition(".")
+        parts = name.split(".")
+        blk = int(parts[2]) if parts[:2] == ["transformer", "h"] else None
+        if open_block is not None and blk != open_block:
+            finish(model.transformer.h[open_block])
+        open_block = blk
         mod = model.get_submodule(mod_name)
         if state is not None:
             t = state[name].to(device=device, dtype=torch.bfloat16)
@@ -136,14 +166,12 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
         else:  # norm weights
             t = torch.ones(p.shape, dtype=torch.bfloat16, device=device)
         setattr(mod, attr, torch.nn.Parameter(t, requires_grad=False))
+    if open_block is not None:
+        finish(model.transformer.h[open_block])
+    if precision is not None:  # lm_head (replicated under TP, as the reference leaves it unsharded)
+        precision.convert_module(model, device)
     if tp is not None:
-        tp(model)
-    if quantize is not None:
-        QuantizedPrecision(quantize).convert_module(model, device)
-    else:  # bf16-true: the Linears stay nn.Linear; TP row shards are strided views -> own contiguous storage
-        for mod in model.modules():
-            if isinstance(mod, torch.nn.Linear) and not mod.weight.is_contiguous():
-                mod.weight = torch.nn.Parameter(mod.weight.data.contiguous(), requires_grad=False)
+        tp.shard_config(fabric, model)
     torch.cuda.empty_cache()
     prev = torch.get_default_dtype()
     torch.set_default_dtype(torch.bfloat16 if rope_positions == "reference" else torch.float32)

@@ -5,7 +5,9 @@ attn.proj / mlp.proj row-parallel (dim 1), bias split only for colwise (the refe
 kept), one all-reduce(sum) forward hook after attention and after the MLP, ``n_head``, ``n_embd``,
 ``n_query_groups`` divided by the world size (``ValueError`` when not divisible). Weights are sharded while
 still float and quantized per shard afterwards (convert_module -> tensor_parallel -> to_device order,
-generate/tp.py:171-190). The collective is ``torch.distributed`` (backend "nccl" = RCCL over xGMI).
+generate/tp.py:171-190), block by block so a rank never holds the whole unsharded model. The collective for a
+decode token is the xGMI one-shot all-reduce of lit_gpt/comm.py (graph-captured, fused with the Block residual
+add); prefill messages use ``torch.distributed`` (backend "nccl" = RCCL over xGMI).
 
 One process per GPU; launch with ``python -m torch.distributed.run --nproc-per-node N generate/tp.py ...``.
 """
@@ -28,7 +30,8 @@ if str(wd) not in sys.path:
     sys.path.append(str(wd))
 
 import generate.base as generate_base  # noqa: E402
-from lit_gpt import GPT, Config  # noqa: E402
+from lit_gpt import GPT, Config, comm  # noqa: E402
+from lit_gpt.comm import all_reduce_output  # noqa: E402,F401  (the hook, reference generate/tp.py:73-74)
 from lit_gpt.model import CausalSelfAttention, GptNeoxMLP, LLaMAMLP, LLaMAMoE  # noqa: E402
 
 
@@ -77,17 +80,22 @@ def tensor_parallel_attn(fabric, attn: CausalSelfAttention) -> None:
     attn.register_forward_hook(partial(all_reduce_output, fabric.world_size))
 
 
-def all_reduce_output(world_size: int, module: torch.nn.Module, ins, outs) -> torch.Tensor:
-    """Sum the row-parallel partial outputs over the TP group (RCCL all-reduce, in place)."""
-    if world_size > 1:
-        dist.all_reduce(outs, op=dist.ReduceOp.SUM)
-    return outs
 
 
 def tensor_parallel(fabric, model: GPT) -> GPT:
     for block in model.transformer.h:
-        tensor_parallel_mlp(fabric, block.mlp)
-        tensor_parallel_attn(fabric, block.attn)
+        tensor_parallel_block(fabric, block)
+    return shard_config(fabric, model)
+
+
+def tensor_parallel_block(fabric, block) -> None:
+    """One block's share of ``tensor_parallel`` (build_model shards block by block, before quantizing)."""
+    tensor_parallel_mlp(fabric, block.mlp)
+    tensor_parallel_attn(fabric, block.attn)
+
+
+def shard_config(fabric, model: GPT) -> GPT:
+    """The config update at the end of the reference's ``tensor_parallel`` (generate/tp.py:84-91)."""
     world_size = fabric.world_size
     for attr in ("n_head", "n_embd", "n_query_groups"):
         size = getattr(model.config, attr)
@@ -97,14 +105,21 @@ def tensor_parallel(fabric, model: GPT) -> GPT:
     return model
 
 
-def init_distributed() -> Fabric:
-    """One process per GPU from the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*)."""
+def init_distributed(allreduce: Optional[str] = None) -> Fabric:
+    """One process per GPU from the torchrun environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*). With more
+    than one rank the decode all-reduces go through the xGMI one-shot kernel (lit_gpt/comm.py) unless
+    ``allreduce`` (or ``LGA_TP_ALLREDUCE``) is "rccl"; prefill messages always use RCCL."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     if world > 1 and not dist.is_initialized():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    mode = allreduce or os.environ.get("LGA_TP_ALLREDUCE", "xgmi")
+    if mode not in ("xgmi", "rccl"):
+        raise ValueError(f"allreduce must be 'xgmi' or 'rccl', got {mode!r}")
+    if world > 1 and mode == "xgmi" and comm.get_default() is None:
+        comm.set_default(comm.XgmiAllReduce(device=torch.device("cuda", local)))
     return Fabric(world, rank)
 
 
@@ -131,7 +146,7 @@ def main(prompt: str = "What food do llamas eat?", *, num_samples: int = 1, max_
     max_returned = encoded.size(0) + max_new_tokens
     t0 = time.perf_counter()
     model = generate_base.build_model(config, quantize=quantize, device=device, checkpoint_path=checkpoint_path,
-                                      max_seq_length=max_returned, tp=partial(tensor_parallel, fabric))
+                                      max_seq_length=max_returned, fabric=fabric)
     if fabric.world_size > 1:
         dist.barrier()
     if fabric.global_rank == 0:

@@ -1,0 +1,145 @@
+"""Tensor-parallel all-reduce for decode activations over xGMI peer memory (``lga_allreduce_bf16``).
+
+The reference sums the row-parallel partial outputs with a collective in a forward hook
+(/root/reference/generate/tp.py:73-74, ``all_reduce(outs, "sum", list(range(world_size)))``), 64 times per
+Llama-2-7B token. ``XgmiAllReduce`` is the MI355X replacement for those one-token messages: every rank owns a
+mailbox (uncached HBM, IPC-exported), the handles are exchanged once over the process group, and each call is
+ONE single-workgroup kernel that pushes the partial into every peer's mailbox, waits for the peers' flags and
+sums the ranks in order 0..W-1 (bit-identical on every rank), optionally adding the Block residual. The launch
+is graph-capturable. Prefill-sized messages (more than ``cap`` elements) stay on ``torch.distributed``
+(RCCL over xGMI with the ``nccl`` backend).
+
+One process per GPU, all ranks of the group on this node (xGMI / same-device IPC). Ranks may also share one GPU
+(tests run two ranks on cuda:0 with a gloo group for the handle exchange).
+"""
+
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from lit_gpt import ops
+
+DEFAULT_CAP = 32768  # bf16 elements per message (64 KB): decode activations of every config (k * C for MoE)
+
+_default: Optional["XgmiAllReduce"] = None
+
+
+class XgmiAllReduce:
+    def __init__(self, group=None, device: Optional[torch.device] = None, cap: int = DEFAULT_CAP) -> None:
+        lib = ops.load_library()
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        if not 1 <= self.world <= 8:
+            raise ValueError(f"XgmiAllReduce supports 1..8 ranks, got {self.world}")
+        self.cap = cap
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        nbytes = lib.lga_comm_mailbox_bytes(cap)
+        handle = ctypes.create_string_buffer(64)
+        own = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            ops._check(lib.lga_comm_alloc(nbytes, ctypes.byref(own), handle))
+        self._own = own
+        handles: List[Optional[bytes]] = [None] * self.world
+        dist.all_gather_object(handles, bytes(handle.raw), group=group)
+        ptrs = []
+        self._opened = []
+        with torch.cuda.device(self.device):
+            for r, h in enumerate(handles):
+                if r == self.rank:
+                    ptrs.append(own.value)
+                    continue
+                p = ctypes.c_void_p()
+                ops._check(lib.lga_comm_open(h, ctypes.byref(p)))
+                self._opened.append(p)
+                ptrs.append(p.value)
+        self._mailboxes = (ctypes.c_void_p * self.world)(*ptrs)
+        self.seq = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        dist.barrier(group=group)
+
+    def supports(self, t: torch.Tensor) -> bool:
+        return (t.is_cuda and t.dtype == torch.bfloat16 and t.numel() <= self.cap and t.numel() % 8 == 0
+                and t.is_contiguous())
+
+    def all_reduce(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """bf16(sum over ranks of x) (+ residual, rounded as the Block's ``x + h``); a new tensor unless ``out``."""
+        if not self.supports(x):
+            raise ValueError(f"XgmiAllReduce: needs a contiguous bf16 GPU tensor of <= {self.cap} elements "
+                             f"(multiple of 8), got {tuple(x.shape)} {x.dtype}")
+        y = out if out is not None else torch.empty_like(x)
+        res = None
+        if residual is not None:
+            if residual.numel() != x.numel():
+                raise ValueError("XgmiAllReduce: residual shape differs from x")
+            res = ops._dev(residual.contiguous(), "residual", torch.bfloat16)
+        ops._check(ops.load_library().lga_allreduce_bf16(
+            ops._dev(x, "x", torch.bfloat16), res, ops._dev(y, "y", torch.bfloat16), x.numel(), self._mailboxes,
+            self.rank, self.world, self.cap, self.seq.data_ptr(), self.err.data_ptr(), ops._stream()))
+        return y
+
+    def errors(self) -> int:
+        """Non-zero when a call timed out waiting for a peer since the last check (syncs; clears the word)."""
+        e = int(self.err.item())
+        self.err.zero_()
+        return e
+
+    def close(self) -> None:
+        lib = ops.load_library()
+        torch.cuda.synchronize(self.device)
+        for p in self._opened:
+            lib.lga_comm_close(p)
+        self._opened = []
+        if self._own is not None:
+            lib.lga_comm_free(self._own)
+            self._own = None
+
+
+def set_default(comm: Optional[XgmiAllReduce]) -> None:
+    """Install the communicator the TP hooks (generate/tp.py all_reduce_output) use for small messages."""
+    global _default
+    _default = comm
+
+
+def get_default() -> Optional[XgmiAllReduce]:
+    return _default
+
+
+def all_reduce_output(world_size: int, module: torch.nn.Module, ins, outs) -> torch.Tensor:
+    """The TP forward hook (reference generate/tp.py:73-74): sum the row-parallel partial outputs over the ranks.
+    One-token messages go through the xGMI one-shot kernel when a communicator is installed; everything else
+    (prefill, CPU / gloo groups) through ``torch.distributed.all_reduce`` (RCCL with the ``nccl`` backend)."""
+    if world_size <= 1:
+        return outs
+    comm = _default
+    if comm is not None and comm.world == world_size and comm.supports(outs):
+        return comm.all_reduce(outs)
+    dist.all_reduce(outs, op=dist.ReduceOp.SUM)
+    return outs
+
+
+def tp_hook(module: torch.nn.Module):
+    """The ``all_reduce_output`` hook when it is the module's only forward hook (then Block may run the module
+    without hooks and fuse the reduction with the residual add); None otherwise."""
+    import functools
+
+    hooks = list(module._forward_hooks.values())
+    if len(hooks) == 1 and isinstance(hooks[0], functools.partial) and hooks[0].func is all_reduce_output:
+        return hooks[0]
+    return None
+
+
+def reduce_add(hook, module: torch.nn.Module, h: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:
+    """residual + all_reduce(h), the Block's ``x + attn(...)`` / ``x + mlp(...)`` under TP: one fused kernel for
+    decode messages, else the hook's collective followed by the bf16 add."""
+    comm = _default
+    world = hook.args[0]
+    if comm is not None and comm.world == world and comm.supports(h) and residual.numel() == h.numel():
+        return comm.all_reduce(h, residual=residual.contiguous()).view_as(residual)
+    h = hook(module, (), h)
+    return ops.add(h.contiguous(), residual.contiguous()).view_as(residual)

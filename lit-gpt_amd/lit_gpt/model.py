@@ -203,12 +203,24 @@ class Block(nn.Module):
         if not isinstance(self.norm_1, RMSNorm) or not isinstance(self.mlp, (LLaMAMLP, LLaMAMoE)):
             raise NotImplementedError(f"{type(self.mlp).__name__} / {type(self.norm_1).__name__} blocks have no "
                                       "MI355X kernels in this build")
-        # residual adds ride the out-projection epilogues unless a hook (TP all-reduce) must see the bare output
-        if not self.attn._forward_hooks and not self.mlp._forward_hooks:
+        # The norms ride the qkv / fc GEMV prologues and the residual adds the out-projection epilogues. Under
+        # tensor parallelism (generate/tp.py's all_reduce_output hook on attn / mlp) the projections yield partial
+        # sums: the module then runs without its hook and the reduction + residual add is one fused kernel
+        # (lit_gpt/comm.py); any other forward hook keeps the reference's call-the-module semantics.
+        from lit_gpt import comm
+
+        ha = comm.tp_hook(self.attn)
+        if ha is not None:
+            x = comm.reduce_add(ha, self.attn, self.attn.forward(x, cos, sin, mask, input_pos, norm=self.norm_1), x)
+        elif not self.attn._forward_hooks:
             x = self.attn(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x)
+        else:
+            x = ops.add(self.attn(self.norm_1(x), cos, sin, mask, input_pos).contiguous(), x.contiguous())
+        hm = comm.tp_hook(self.mlp)
+        if hm is not None:
+            return comm.reduce_add(hm, self.mlp, self.mlp.forward(x, norm=self.norm_2), x)
+        if not self.mlp._forward_hooks:  # (a sparse-MoE block applies its experts' TP hooks itself)
             return self.mlp(x, norm=self.norm_2, residual=x)
-        h = self.attn(self.norm_1(x), cos, sin, mask, input_pos)
-        x = ops.add(h.contiguous(), x.contiguous())
         return ops.add(self.mlp(self.norm_2(x)).contiguous(), x)
 
 

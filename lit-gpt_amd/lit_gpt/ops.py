@@ -57,8 +57,15 @@ SIGNATURES = {
     "lga_q4_gemv_swiglu_experts": [_P, _P, _P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _F,
                                    _P, _I, _I, _I, _I, _I, _P],
     "lga_moe_combine": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lga_comm_mailbox_bytes": [_I],
+    "lga_comm_alloc": [ctypes.c_size_t, ctypes.POINTER(_P), _P],
+    "lga_comm_open": [_P, ctypes.POINTER(_P)],
+    "lga_comm_close": [_P],
+    "lga_comm_free": [_P],
+    "lga_allreduce_bf16": [_P, _P, _P, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P, _P],
 }
-_RESTYPES = {"lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t}
+_RESTYPES = {"lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
+             "lga_comm_mailbox_bytes": ctypes.c_size_t}
 
 _lib: Optional[ctypes.CDLL] = None
 

