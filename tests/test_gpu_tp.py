@@ -123,3 +123,26 @@ def test_tp2_mixtral_32k_context(tmp_path):
     _launch("tp_geometry_worker.py", 2, [out, "--model", "Mixtral-8x7B-v0.1", "--layers", "1", "--cache", "32000",
                                          "--steps", "8", "--tmp", tmp_path], timeout=580)
     print(f"worst {_check_logits(np.load(out)):.3%}")
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("fam", ["llama", "mixtral"])
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("mode", ["bf16", "int4-g128"])
+def test_tp_matches_reference_tp_fixture(fam, world, mode, tmp_path):
+    """The product's TP decode (generate/tp.py sharding, per-shard quantization, xGMI all-reduce) against the
+    REFERENCE's own tensor_parallel run under gloo (tests/golden/g4_tp_logits.npz, made by
+    tests/golden/make_golden_tp.py), bf16 activations on both sides, teacher-forced on the reference's tokens."""
+    out = tmp_path / "r.npz"
+    _launch("tp_golden_worker.py", world, [out, fam, mode], timeout=280)
+    d = np.load(out)
+    assert int(d["comm_err"]) == 0
+    for s, (g, e) in enumerate(zip(d["logits"], d["ref"])):
+        err = np.abs(g - e)
+        rel_max = err.max() / np.abs(e).max()
+        rel_rms = math.sqrt(float((err ** 2).mean())) / math.sqrt(float((e ** 2).mean()))
+        print(f"{fam} w{world} {mode} step {s}: max {rel_max:.3%} rms {rel_rms:.3%}")
+        assert rel_max <= MAX_REL and rel_rms <= RMS_REL, (s, rel_max, rel_rms)
+        top = np.sort(e)
+        if top[-1] - top[-2] > MARGIN:
+            assert int(np.argmax(g)) == int(np.argmax(e)), f"step {s}: greedy token differs from the reference"

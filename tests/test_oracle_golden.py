@@ -187,3 +187,52 @@ def test_synth_is_deterministic():
     np.testing.assert_array_equal(a, b)
     assert abs(a.std() - 0.02) < 0.002 and abs(a.mean()) < 0.002
     assert not np.array_equal(a, synth.normal((1000,), "y", 1))
+
+
+@pytest.mark.parametrize("fam", ["llama", "mixtral"])
+@pytest.mark.parametrize("world", [2, 4])
+def test_reference_tp_logits_equal_unsharded_oracle(fam, world, golden):
+    """G4: the reference's own tensor_parallel under gloo TP=2/4 (tests/golden/make_golden_tp.py)
+    computes what the unsharded oracle computes: same greedy tokens, logits within fp32 reordering of the
+    row-parallel sums; and with per-shard int4 weights, what the oracle computes on those assembled shards."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).parent / "golden"))
+    from make_golden_tp import FAMILIES, STEPS, T, fit_group
+
+    g = golden("g4_tp_logits.npz")
+    name, kw = FAMILIES[fam]
+    cfg = _cfg(name, **kw)
+    sd = synth.state_dict(cfg, seed=17)
+    prompt = torch.from_numpy(g[f"{fam}_prompt"])
+    ref = g[f"{fam}_w{world}_fp32_float32_logits"]
+    toks = g[f"{fam}_w{world}_fp32_float32_tokens"]
+    m = om.OracleGPT(cfg, sd)
+    m.set_kv_cache(T + STEPS + 1)
+    got = [m.forward(prompt, torch.arange(T))[-1]]
+    for s in range(STEPS):
+        got.append(m.forward(torch.tensor([int(toks[s])]), torch.tensor([T + s]))[-1])
+    got = torch.stack(got).float().numpy()
+    assert np.abs(got - ref).max() <= 1e-4 * np.abs(ref).max()
+    assert np.array_equal(got.argmax(-1), toks)
+
+    # int4 per shard: colwise shards (dim 0) keep the unsharded groups; rowwise shards (dim 1) are quantized with
+    # the group that fits the shard's width, i.e. the unsharded matrix quantized with that group
+    def deq(k, v):
+        if not (k.endswith(".weight") and v.ndim == 2) or k.startswith("transformer.wte"):
+            return v
+        rowwise = k.endswith("attn.proj.weight") or (k.endswith("proj.weight") and ".mlp" in k)
+        gsz = fit_group(v.shape[1] // world if rowwise else v.shape[1])
+        return quant.dequantize_q4g(*quant.quantize_q4g(v, gsz), gsz)
+
+    mq = om.OracleGPT(cfg, sd, weight_override=deq)
+    mq.set_kv_cache(T + STEPS + 1)
+    ref_q = g[f"{fam}_w{world}_q4g_bfloat16_logits"]
+    toks_q = g[f"{fam}_w{world}_q4g_bfloat16_tokens"]
+    got_q = [mq.forward(prompt, torch.arange(T))[-1]]
+    for s in range(STEPS):
+        got_q.append(mq.forward(torch.tensor([int(toks_q[s])]), torch.tensor([T + s]))[-1])
+    got_q = torch.stack(got_q).float().numpy()
+    # reference side ran in bf16: bf16 activation rounding vs the fp32 oracle
+    assert np.abs(got_q - ref_q).max() <= 0.03 * np.abs(ref_q).max()
