@@ -6,7 +6,8 @@ Run once here (never on the GPU box; /root/reference does not exist there):
     python tests/golden/make_golden_tp.py
 Writes ``g4_tp_logits.npz``: per (family, world, weights, dtype) the logits of a 12-token prefill and 8 greedy
 decode steps (teacher-forced on the reference's own greedy tokens, identical on every rank), the tokens, and the
-prompt. Weights come from ``oracle.synth`` (regenerable anywhere). ``weights = "q4g"``: after sharding, every
+prompt; for every bf16 run also ``{key}_logits_f32``: the same weights in fp32, teacher-forced on the bf16 run's
+tokens (the exact-arithmetic side of the GPU tests' accuracy bound, tests/parity.py). Weights come from ``oracle.synth`` (regenerable anywhere). ``weights = "q4g"``: after sharding, every
 Linear (lm_head included, unsharded) holds dequant(quant_int4(shard)) with the product's group rule (128, or the
 largest of 64 / 32 dividing the shard's in_features) — the order of the reference's BitsandbytesPrecision
 convert -> tensor_parallel -> quantize-on-device (generate/tp.py:171-190).
@@ -31,9 +32,11 @@ sys.path.insert(0, str(REPO))
 sys.path.insert(0, str(HERE))
 
 FAMILIES = {
-    "llama": ("Llama-2-70b-hf", dict(n_layer=2, n_embd=256, n_head=8, n_query_groups=4, intermediate_size=512,
+    # head_size 64 (n_embd 512 / 8 heads): a head size the MI355X attention kernels run, so the product's TP decode
+    # can be compared with these logits on the GPU
+    "llama": ("Llama-2-70b-hf", dict(n_layer=2, n_embd=512, n_head=8, n_query_groups=4, intermediate_size=1024,
                                      vocab_size=1000, padding_multiple=64, block_size=64)),
-    "mixtral": ("Mixtral-8x7B-v0.1", dict(n_layer=2, n_embd=256, n_head=8, n_query_groups=4, intermediate_size=512,
+    "mixtral": ("Mixtral-8x7B-v0.1", dict(n_layer=2, n_embd=512, n_head=8, n_query_groups=4, intermediate_size=1024,
                                           n_expert=4, n_expert_per_token=2, padded_vocab_size=1024, vocab_size=1024,
                                           block_size=64)),
 }
@@ -72,26 +75,34 @@ def worker(rank, world, tmp, port):
         sd = synth.state_dict(cfg, seed=17)
         prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=17)).long()
         for wname, dtype in VARIANTS:
-            m = model_mod.GPT(config.Config.from_name(name, **kw))  # tensor_parallel divides the config in place
-            m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-            fab = Mock()
-            fab.world_size, fab.global_rank = world, rank
-            gtp.tensor_parallel(fab, m)
-            if wname == "q4g":
-                q4g_shards(m)
-            m = m.to(dtype).eval()
-            m.max_seq_length = T + STEPS + 1
-            m.set_kv_cache(batch_size=1)
-            with torch.inference_mode():
-                lg = m(prompt.view(1, -1), torch.arange(T))[0, -1].float()
-                logits, toks = [lg], [int(torch.argmax(lg))]
-                for s in range(STEPS):
-                    lg = m(torch.tensor([[toks[-1]]]), torch.tensor([T + s]))[0, -1].float()
-                    logits.append(lg)
-                    toks.append(int(torch.argmax(lg)))
+            def build(dt):
+                m = model_mod.GPT(config.Config.from_name(name, **kw))  # tensor_parallel divides the config in place
+                m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+                fab = Mock()
+                fab.world_size, fab.global_rank = world, rank
+                gtp.tensor_parallel(fab, m)
+                if wname == "q4g":
+                    q4g_shards(m)
+                m = m.to(dt).eval()
+                m.max_seq_length = T + STEPS + 1
+                m.set_kv_cache(batch_size=1)
+                return m
+
+            def run(m, forced=None):
+                with torch.inference_mode():
+                    lg = m(prompt.view(1, -1), torch.arange(T))[0, -1].float()
+                    logits, toks = [lg], [int(torch.argmax(lg))]
+                    for s in range(STEPS):
+                        tok = toks[-1] if forced is None else int(forced[s])
+                        lg = m(torch.tensor([[tok]]), torch.tensor([T + s]))[0, -1].float()
+                        logits.append(lg)
+                        toks.append(int(torch.argmax(lg)))
+                return torch.stack(logits).numpy(), np.array(toks, dtype=np.int64)
+
             key = f"{fam}_w{world}_{wname}_{str(dtype).split('.')[-1]}"
-            out[f"{key}_logits"] = torch.stack(logits).numpy()
-            out[f"{key}_tokens"] = np.array(toks, dtype=np.int64)
+            out[f"{key}_logits"], out[f"{key}_tokens"] = run(build(dtype))
+            if dtype == torch.bfloat16:
+                out[f"{key}_logits_f32"], _ = run(build(torch.float32), forced=out[f"{key}_tokens"])
         out[f"{fam}_prompt"] = prompt.numpy()
     if rank == 0:
         np.savez(Path(tmp) / f"w{world}.npz", **out)

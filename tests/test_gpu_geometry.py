@@ -6,12 +6,11 @@ reference math, oracle/model.py) is then built from EXACTLY the weights the GPU 
 packed bytes are dequantized by oracle/quant.py (the packing itself is pinned bit-exact by
 tests/test_gpu_kernels.py::test_quantizer_bit_exact), bf16 Linears / embeddings / norms are copied.
 
-Tolerance (written per test, derived from bf16 rounding): every activation the reference rounds to bf16 carries a
-relative error of at most 2^-9; the GPU and the CPU restatement accumulate in different orders, so an element may
-land one bf16 ulp (2^-8 relative) apart and that difference propagates linearly through the following layers.
-For a two-block model that bounds the logit error at a few ulps of the logit scale: we require
-max |logit - oracle| <= 1.5 % of max |oracle logit| (round 1 used 4 %) and an RMS error <= 1.5 % of the RMS logit
-(the logits themselves are bf16: one output ulp is 0.4-0.8 % of a logit of magnitude 1-2), per step. Greedy tokens must equal the oracle's argmax at every step whose oracle top-1/top-2 margin exceeds 0.1.
+Tolerance (tests/parity.py): the oracle runs twice on the GPU's own weights, in float64 (exact-arithmetic
+stand-in) and in bf16 (the reference's ``--precision bf16-true`` rounding points). At this geometry the bf16
+reference itself sits 1.4-1.9 % (max) / 1.6-1.7 % (rms) of the logit scale from float64 (tools/bf16_noise_floor.py),
+so the product must be as accurate as that (<= 1.25 x its distance + 0.25 %), within 3 % of the bf16 oracle, and
+give the float64 greedy token wherever the margin exceeds 4 x its own error.
 """
 
 from __future__ import annotations
@@ -24,13 +23,10 @@ import torch
 
 from oracle import model as om
 from oracle import quant, synth
+from parity import check_step
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
-
-MAX_REL = 0.015   # max |d logit| / max |logit|
-RMS_REL = 0.015   # rms(d logit) / rms(logit)
-MARGIN = 0.1      # oracle top-1 / top-2 gap above which the greedy token must match
 
 
 def oracle_state_from_model(model) -> dict:
@@ -53,21 +49,6 @@ def oracle_state_from_model(model) -> dict:
         if name not in sd:
             sd[name] = p.detach().float().cpu().numpy()
     return sd
-
-
-def check_step(got: torch.Tensor, exp: torch.Tensor, tag: str) -> float:
-    err = (got - exp).abs()
-    scale = exp.abs().max().item()
-    rms = math.sqrt(float((exp ** 2).mean()))
-    rel_max, rel_rms = err.max().item() / scale, math.sqrt(float((err ** 2).mean())) / rms
-    top2 = torch.topk(exp, 2)
-    margin = float(top2.values[0] - top2.values[1])
-    print(f"{tag}: max|d|/max = {rel_max:.3%}, rms(d)/rms = {rel_rms:.3%}, margin {margin:.3f}")
-    assert rel_max <= MAX_REL, f"{tag}: max err {err.max().item():.4g} vs scale {scale:.4g}"
-    assert rel_rms <= RMS_REL, f"{tag}: rms err {rel_rms:.3%}"
-    if margin > MARGIN:
-        assert int(torch.argmax(got)) == int(top2.indices[0]), f"{tag}: greedy token differs from the oracle"
-    return rel_max
 
 
 @pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bf16"])
@@ -99,16 +80,18 @@ def test_llama2_7b_geometry_prefill_2048_then_decode(mode):
     y = generate(model, prompt, T + N, temperature=0.0).cpu()
     assert y[T:].tolist() == toks
 
-    ref = om.OracleGPT(cfg, oracle_state_from_model(model), dtype=torch.bfloat16, rope_pos_dtype=torch.bfloat16)
-    ref.set_kv_cache(T + N + 1)
-    p = prompt.cpu()
+    sd = oracle_state_from_model(model)
+    refs = {}
+    for dt in (torch.bfloat16, torch.float64):
+        ref = om.OracleGPT(cfg, sd, dtype=dt, rope_pos_dtype=torch.bfloat16)
+        ref.set_kv_cache(T + N + 1)
+        out = [ref.forward(prompt.cpu(), torch.arange(T), last_only=True)[-1]]
+        for i in range(1, N):
+            out.append(ref.forward(torch.tensor([toks[i - 1]]), torch.tensor([T + i - 1]))[-1])
+        refs[dt] = out
     worst = 0.0
     for i in range(N):
-        if i == 0:
-            e = ref.forward(p, torch.arange(T), last_only=True)[-1].float()
-        else:
-            e = ref.forward(torch.tensor([toks[i - 1]]), torch.tensor([T + i - 1]))[-1].float()
-        worst = max(worst, check_step(got[i], e, f"{mode} step {i}"))
+        worst = max(worst, check_step(got[i], refs[torch.bfloat16][i], refs[torch.float64][i], f"{mode} step {i}"))
     print(f"\n{mode}: worst max|d logit| / max|logit| = {worst:.4%}")
 
 

@@ -5,13 +5,13 @@ configs' per-rank geometry, and the xGMI one-shot all-reduce (lit_gpt/comm.py) t
 The box has ONE GPU: every test runs its ranks as separate processes on cuda:0 (torch.distributed.run, gloo group),
 exactly the code path of one process per GPU. The xGMI kernel then exchanges through same-device IPC mappings.
 Parity is against the oracle run on the UNSHARDED weights assembled from the ranks' shards (tests/workers/
-tp_geometry_worker.py); tolerance as tests/test_gpu_geometry.py (bf16-derived: 1.5 % of max |logit| and of the RMS
-logit per step, greedy tokens equal where the oracle margin exceeds 0.1). Every rank must hold bit-identical logits.
+tp_geometry_worker.py), in bf16 and in float64, with the bounds of tests/parity.py (as accurate as the reference's
+bf16 path, within 3 % of it, greedy tokens equal where the margin is clear); the reference-fixture test uses the
+reference's own bf16 and fp32 TP logits. Every rank must hold bit-identical logits.
 """
 
 from __future__ import annotations
 
-import math
 import os
 import socket
 import subprocess
@@ -21,9 +21,11 @@ from pathlib import Path
 import numpy as np
 import pytest
 
+from parity import check_step
+
 pytestmark = pytest.mark.gpu
 WORKERS = Path(__file__).parent / "workers"
-MAX_REL, RMS_REL, MARGIN = 0.015, 0.015, 0.1
+MOE_GAP = 2 ** -6  # router top-k / next gap below which a step may route differently on the two sides
 
 
 def _launch(worker, nproc, args, timeout=540):
@@ -34,29 +36,18 @@ def _launch(worker, nproc, args, timeout=540):
            "--master-addr=127.0.0.1", f"--master-port={port}", str(WORKERS / worker), *map(str, args)]
     env = dict(os.environ, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
-    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-4000:])
+    errors = [ln for ln in r.stderr.splitlines() if "Error" in ln and "ChildFailedError" not in ln]
+    assert r.returncode == 0, ("\n".join(errors[:8]), r.stdout[-2000:], r.stderr[-3000:])
     return r
 
 
-def _check_logits(d, moe_gap=2 ** -6):
-    assert bool(d["same_across_ranks"]), "ranks disagree (replicated sampling needs identical logits)"
+def _check_logits(d):
     assert int(d["comm_err"]) == 0, "an xGMI all-reduce timed out waiting for a peer"
-    tp, ref = d["tp"], d["ref"]
-    keep = np.minimum(d["gaps"], d["ref_gaps"]) > moe_gap  # dense blocks: +inf (no router)
+    assert bool(d["same_across_ranks"]), "ranks disagree (replicated sampling needs identical logits)"
+    tp, ref, ref64 = d["tp"], d["ref"], d["ref64"]
+    keep = np.minimum(d["gaps"], d["ref_gaps"]) > MOE_GAP  # dense blocks: +inf (no router)
     assert keep.sum() >= (len(tp) + 1) // 2, d["gaps"]
-    worst = 0.0
-    for s in np.nonzero(keep)[0]:
-        e, g = ref[s], tp[s]
-        err = np.abs(g - e)
-        rel_max = err.max() / np.abs(e).max()
-        rel_rms = math.sqrt(float((err ** 2).mean())) / math.sqrt(float((e ** 2).mean()))
-        print(f"step {s}: max|d|/max {rel_max:.3%} rms {rel_rms:.3%}")
-        assert rel_max <= MAX_REL and rel_rms <= RMS_REL, (s, rel_max, rel_rms)
-        top = np.sort(e)
-        if top[-1] - top[-2] > MARGIN:
-            assert int(np.argmax(g)) == int(np.argmax(e)), f"step {s}: greedy token differs from the oracle"
-        worst = max(worst, rel_max)
-    return worst
+    return max(check_step(tp[s], ref[s], ref64[s], f"step {s}") for s in np.nonzero(keep)[0])
 
 
 @pytest.mark.timeout(300)
@@ -109,7 +100,7 @@ def test_tp2_xgmi_graph_decode_matches_tp1(mode, tmp_path):
     t1, t2, l1 = outs[1]["graph_tokens"], outs[2]["graph_tokens"], outs[1]["tp"]
     for s in range(len(t1)):
         top = np.sort(l1[s])
-        if top[-1] - top[-2] <= MAX_REL * np.abs(l1[s]).max():
+        if top[-1] - top[-2] <= 0.03 * np.abs(l1[s]).max():  # within the logit tolerance: a legal tie-break
             break
         assert t1[s] == t2[s], f"TP=2 token {s} differs from TP=1 with a clear margin"
 
@@ -126,23 +117,19 @@ def test_tp2_mixtral_32k_context(tmp_path):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("fam", ["llama", "mixtral"])
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("mode", ["bf16", "int4-g128"])
+@pytest.mark.parametrize("fam,mode", [("llama", "bf16"), ("llama", "int4-g128"), ("mixtral", "int4-g128")])
 def test_tp_matches_reference_tp_fixture(fam, world, mode, tmp_path):
     """The product's TP decode (generate/tp.py sharding, per-shard quantization, xGMI all-reduce) against the
     REFERENCE's own tensor_parallel run under gloo (tests/golden/g4_tp_logits.npz, made by
-    tests/golden/make_golden_tp.py), bf16 activations on both sides, teacher-forced on the reference's tokens."""
+    tests/golden/make_golden_tp.py), bf16 activations on both sides, teacher-forced on the reference's tokens.
+    (Sparse-MoE experts run as 4-bit QuantLinears only — BASELINE config 5 is Mixtral int4 — so Mixtral is compared
+    with its int4-g128 fixture.)"""
     out = tmp_path / "r.npz"
     _launch("tp_golden_worker.py", world, [out, fam, mode], timeout=280)
     d = np.load(out)
     assert int(d["comm_err"]) == 0
-    for s, (g, e) in enumerate(zip(d["logits"], d["ref"])):
-        err = np.abs(g - e)
-        rel_max = err.max() / np.abs(e).max()
-        rel_rms = math.sqrt(float((err ** 2).mean())) / math.sqrt(float((e ** 2).mean()))
-        print(f"{fam} w{world} {mode} step {s}: max {rel_max:.3%} rms {rel_rms:.3%}")
-        assert rel_max <= MAX_REL and rel_rms <= RMS_REL, (s, rel_max, rel_rms)
-        top = np.sort(e)
-        if top[-1] - top[-2] > MARGIN:
-            assert int(np.argmax(g)) == int(np.argmax(e)), f"step {s}: greedy token differs from the reference"
+    keep = d["gaps"] > MOE_GAP
+    assert keep.sum() >= (len(keep) + 1) // 2, d["gaps"]
+    for s in np.nonzero(keep)[0]:
+        check_step(d["logits"][s], d["ref"][s], d["ref_f32"][s], f"{fam} w{world} {mode} step {s}")

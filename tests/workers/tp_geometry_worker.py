@@ -187,35 +187,41 @@ def main():
             st_ = style(name.rsplit(".", 1)[0]) if name.endswith(".weight") else (
                 0 if style(name.rsplit(".", 1)[0]) == 0 else None)
             sd[name] = np.concatenate(entries, axis=st_) if st_ is not None and world > 1 else entries[0]
-        ref = om.OracleGPT(full_cfg, sd, dtype=torch.bfloat16, rope_pos_dtype=torch.bfloat16)
-        ref.set_kv_cache(max_seq)
-        rgaps = []
-        orig = ref._lin
+        def run_oracle(dtype):
+            ref = om.OracleGPT(full_cfg, sd, dtype=dtype, rope_pos_dtype=torch.bfloat16)
+            ref.set_kv_cache(max_seq)
+            rgaps = []
+            orig = ref._lin
 
-        def lin(name, x, *a, **kw):
-            y = orig(name, x, *a, **kw)
-            if name.endswith("mlp.gate"):
-                v = torch.sort(y.float(), dim=-1, descending=True).values
-                k = full_cfg.n_expert_per_token
-                rgaps.append(float((v[:, k - 1] - v[:, k]).min()))
-            return y
+            def lin(name, x, *a, **kw):
+                y = orig(name, x, *a, **kw)
+                if name.endswith("mlp.gate"):
+                    v = torch.sort(y.float(), dim=-1, descending=True).values
+                    k = full_cfg.n_expert_per_token
+                    rgaps.append(float((v[:, k - 1] - v[:, k]).min()))
+                return y
 
-        ref._lin = lin
-        exp, ref_step_gaps = [], []
+            ref._lin = lin
+            exp, ref_step_gaps = [], []
 
-        def ref_record(lg):
-            exp.append(lg[-1].float())
-            ref_step_gaps.append(min(rgaps, default=float("inf")))
-            rgaps.clear()
+            def ref_record(lg):
+                exp.append(lg[-1].double())
+                ref_step_gaps.append(min(rgaps, default=float("inf")))
+                rgaps.clear()
 
-        if P:
-            for i in range(full_cfg.n_layer):
-                ref.cache.write(i, torch.arange(P), cache[i][0], cache[i][1])
-        else:
-            ref_record(ref.forward(ids[:T].long(), torch.arange(T), last_only=True))
-        for s, tok in enumerate(fed):
-            ref_record(ref.forward(torch.tensor([tok]), torch.tensor([base + s])))
-        np.savez(args.out, tp=got, ref=torch.stack(exp).numpy(), gaps=np.array(step_gaps),
+            if P:
+                for i in range(full_cfg.n_layer):
+                    ref.cache.write(i, torch.arange(P), cache[i][0].to(dtype), cache[i][1].to(dtype))
+            else:
+                ref_record(ref.forward(ids[:T].long(), torch.arange(T), last_only=True))
+            for s, tok in enumerate(fed):
+                ref_record(ref.forward(torch.tensor([tok]), torch.tensor([base + s])))
+            return torch.stack(exp).numpy(), ref_step_gaps
+
+        exp, ref_step_gaps = run_oracle(torch.bfloat16)
+        exp64, gaps64 = run_oracle(torch.float64)  # exact-arithmetic side of tests/parity.py
+        ref_step_gaps = np.minimum(ref_step_gaps, gaps64)
+        np.savez(args.out, tp=got, ref=exp, ref64=exp64, gaps=np.array(step_gaps),
                  ref_gaps=np.array(ref_step_gaps), same_across_ranks=same_across_ranks,
                  comm_err=err, graph_tokens=graph_tokens, fed=np.array(fed), oracle_s=time.time() - t0)
     dist.barrier()

@@ -19,6 +19,7 @@ from generate import tp as gtp  # noqa: E402
 from lit_gpt import GPT, Config, comm  # noqa: E402
 from lit_gpt.quantize import QuantizedPrecision  # noqa: E402
 from oracle import synth  # noqa: E402
+from tp_geometry_worker import router_gap_hooks  # noqa: E402
 
 DEV = torch.device("cuda", 0)
 
@@ -47,13 +48,22 @@ def main():
     model = model.to(device=DEV, dtype=torch.bfloat16)
     model.max_seq_length = T + STEPS + 1
     model.set_kv_cache(1, device=DEV)
-    logits = [model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1].float()]
+    gaps, step_gaps = [], []
+    router_gap_hooks(model, gaps)
+
+    def record(lg):
+        step_gaps.append(min(gaps, default=float("inf")))
+        gaps.clear()
+        return lg[0, -1].float()
+
+    logits = [record(model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True))]
     for s in range(STEPS):
-        logits.append(model(torch.tensor([[int(toks[s])]], device=DEV), torch.tensor([T + s], device=DEV),
-                            last_token_only=True)[0, -1].float())
+        logits.append(record(model(torch.tensor([[int(toks[s])]], device=DEV), torch.tensor([T + s], device=DEV),
+                                   last_token_only=True)))
     err = comm.get_default().errors()
     if rank == 0:
-        np.savez(out, logits=torch.stack(logits).cpu().numpy(), ref=g[f"{key}_logits"], comm_err=err)
+        np.savez(out, logits=torch.stack(logits).cpu().numpy(), ref=g[f"{key}_logits"],
+                 ref_f32=g[f"{key}_logits_f32"], gaps=np.array(step_gaps), comm_err=err)
     dist.barrier()
     comm.get_default().close()
     dist.destroy_process_group()
