@@ -404,8 +404,12 @@ def main():
         "load_s": round(load_s, 2),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
-        # the reference's CPU path on all the host cores this process may run on
+        # the reference's CPU path on all the host cores this process may run on — the affinity set,
+        # capped by the CPU share the host grants the job (OMP_NUM_THREADS: 16 per GPU on the MI355X pool, whose
+        # affinity mask shows the whole machine)
         threads = len(os.sched_getaffinity(0)) or os.cpu_count() or 1
+        if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+            threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
         try:
             result["cpu_baseline"] = cpu_baseline(cfg_full, threads, args.cpu_seconds)
         except Exception as e:  # the baseline is reported, never the target: do not lose the GPU number

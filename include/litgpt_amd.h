@@ -52,6 +52,12 @@ int lga_q4_gemv(const void* x, const uint8_t* qweight, const void* scales, const
 int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const void* scales1, const uint8_t* qweight2,
                        const void* scales2, const void* norm_weight, float norm_eps, void* y, int N, int K,
                        int group, int fmt, int variant, lga_stream_t stream);
+/* Attention out-projection (CausalSelfAttention.proj, lit_gpt/model.py:656) whose activation is merged in the
+ * prologue from the split partials of lga_attention_decode_split (the SDPA output, model.py:651, rounded to bf16
+ * once — bit-identical to lga_attention_decode_fused + lga_q4_gemv): K = n_head * head_size. */
+int lga_q4_gemv_attn(const float* partials, int n_splits, int head_size, const uint8_t* qweight, const void* scales,
+                     const void* bias, const void* residual, void* y, int N, int K, int group, int fmt, int variant,
+                     lga_stream_t stream);
 
 /* -- prefill GEMM, M > 1 (bnb dequantize_4bit + cuBLAS GEMM) -------------------------------------------- */
 int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const void* bias, const void* residual,
@@ -65,6 +71,9 @@ int lga_bf16_gemv(const void* x, const void* weight, const void* bias, const voi
 /* y = bf16(silu(bf16(x W1^T))) * bf16(x W2^T) (LLaMAMLP, model.py:715), optional fused RMSNorm of x */
 int lga_bf16_gemv_swiglu(const void* x, const void* weight1, const void* weight2, const void* norm_weight,
                          float norm_eps, void* y, int N, int K, lga_stream_t stream);
+/* bf16 form of lga_q4_gemv_attn */
+int lga_bf16_gemv_attn(const float* partials, int n_splits, int head_size, const void* weight, const void* bias,
+                       const void* residual, void* y, int N, int K, lga_stream_t stream);
 /* prefill GEMM Y (M, N) = X (M, K) . W (N, K)^T [+bias] [+residual] on MFMA; K % 32 == 0 */
 int lga_bf16_gemm(const void* x, const void* weight, const void* bias, const void* residual, void* y, int M, int N,
                   int K, lga_stream_t stream);
@@ -108,6 +117,14 @@ int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, co
                                const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, void* y,
                                float* workspace, unsigned* counters, int n_head, int n_query_groups, int head_size,
                                int rope_n_elem, int max_seq, int n_splits, float scale, lga_stream_t stream);
+/* The same decode attention without the in-launch split merge: every split writes its (m, l, o) to `partials`
+ * (lga_attention_workspace_bytes(1, H, hs, n_splits) bytes; per head row h and split s, hs + 4 floats at
+ * (h * n_splits + s) * (hs + 4): max score, sum of exp, -, -, unnormalised output) for lga_q4_gemv_attn /
+ * lga_bf16_gemv_attn to merge. No counters; caches as lga_attention_decode_fused. */
+int lga_attention_decode_split(const void* qkv, void* k_cache, void* v_cache, const int64_t* cache_pos,
+                               const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows,
+                               float* partials, int n_head, int n_query_groups, int head_size, int rope_n_elem,
+                               int max_seq, int n_splits, float scale, lga_stream_t stream);
 
 /* -- sparse MoE (LLaMAMoE.forward, lit_gpt/model.py:727-743; Mixtral) ------------------------------------------
  * lga_moe_route: per token row of router logits [T][n_expert] bf16 -> expert_ids [T][k] int32 and probs [T][k]
@@ -139,7 +156,7 @@ int lga_moe_combine(const void* expert_out, const void* probs, const int32_t* ex
  * y[n] = bf16(sum over ranks 0..world-1, in that order, of x_r) (+ residual[n]: y = bf16(bf16(sum) + residual),
  * the Block residual add, lit_gpt/model.py:591-592), identical bits on every rank. mailboxes: host array of world
  * device pointers (index rank = this rank's own mailbox); seq_counter: 1 uint32 zeroed once, advanced by every
- * call (the same call sequence on every rank); err: bit 0 set when a peer's flag did not arrive within ~0.2 s
+ * call (the same call sequence on every rank); err: bit 0 set when a peer's flag did not arrive within 5 s
  * (results invalid). n % 8 == 0, n <= cap, world <= 8. One workgroup; graph-capturable. */
 size_t lga_comm_mailbox_bytes(int cap);
 int lga_comm_alloc(size_t bytes, void** ptr, void* ipc_handle);

@@ -4,8 +4,8 @@ Same functions and contract as /root/reference/chat/base.py: ``generate`` (:23-6
 tokens as they are produced, holds back the last ``max(len(stop))`` tokens until they cannot begin a stop
 sequence and returns without yielding a matched stop sequence; ``decode`` (:71-99) prints the stream
 (token-by-token for HuggingFace tokenizers, re-decoding the prefix for sentencepiece) and returns the count;
-``prompt_config`` (:191-365) for the model families this build runs (Llama-2 chat, CodeLlama / Mistral /
-Mixtral instruct, plain); ``main`` (:102-188) is the interactive loop. MI355X difference: greedy chat
+``prompt_config`` (:191-365) for the model families this build runs (Llama-2 chat, CodeLlama / Mistral
+instruct, plain — Mixtral-Instruct gets the plain template, as the reference's ``Mistral.*Instruct`` pattern gives); ``main`` (:102-188) is the interactive loop. MI355X difference: greedy chat
 (``--temperature 0``) replays one HIP graph per token (lit_gpt/runtime.py ``DecodeGraph``) instead of
 ``torch.compile(mode="reduce-overhead")``.
 """
@@ -122,7 +122,7 @@ def prompt_config(checkpoint_dir: Path, tokenizer) -> Tuple[str, Tuple[List[int]
     eos = ([tokenizer.eos_id],)
     if re.search("Llama-2.*-chat", name):
         return f"[INST] <<SYS>>\n{_LLAMA2_SYSTEM}\n<</SYS>>\n\n {{prompt}} [/INST] ", eos
-    if re.search("CodeLlama|Mi[sx]tral.*Instruct", name):
+    if re.search("CodeLlama|Mistral.*Instruct", name):  # the reference's pattern: Mixtral-Instruct falls through
         return "<s>[INST] {prompt} [/INST]", eos
     return "{prompt}", eos
 

@@ -72,11 +72,20 @@ def sequential(model: GPT, root: torch.device, max_seq_length: int, devices: int
             continue
         replace_device(sub, replace=torch.device("cpu"), by=root)
 
+    # one copy of the rope tables per GPU, made here: the blocks' input hook substitutes it for the root tables
+    # instead of copying max_seq x n_elem fp32 twice per block per token
+    replicas = {}
+    for path, part in mapping.items():
+        target = _device(root, device_ids[part])
+        if part > 0 and target not in replicas:
+            replicas[target] = {_tensor_key(t): t.to(target) for t in (model.cos, model.sin)}
+
     for layer_num, (path, part) in enumerate(mapping.items()):
         block = model.get_submodule(path)
         target = _device(root, device_ids[part])
         if part > 0:
             # inputs (x, cos, sin, mask, input_pos) follow the block; the block runs with its GPU current
+            block.register_forward_pre_hook(partial(_use_replicas, replicas[target]))
             block.register_forward_pre_hook(partial(move_block_input, target))
             block.register_forward_pre_hook(partial(_enter_device, target))
             block.register_forward_hook(partial(_leave_device, root))
@@ -94,6 +103,16 @@ def layer_to_device(module: torch.nn.Module, chunk_on: Type[torch.nn.Module],
     """Block path -> partition index, in definition (= execution) order (reference :80-86)."""
     hits = [name for name, sub in module.named_modules() if isinstance(sub, chunk_on)]
     return OrderedDict((name, i // chunk_size) for i, name in enumerate(hits))
+
+
+def _tensor_key(t: torch.Tensor):
+    return (t.device, t.data_ptr(), tuple(t.shape), t.dtype)
+
+
+def _use_replicas(replicas, module: torch.nn.Module, ins):
+    """``forward_pre_hook``: swap inputs that are the root's rope tables for this block's device copy (a table
+    rebuilt since ``sequential`` ran no longer matches and is copied by ``move_block_input`` as before)."""
+    return tuple(replicas.get(_tensor_key(t), t) if isinstance(t, torch.Tensor) else t for t in ins)
 
 
 def move_block_input(device: torch.device, module: torch.nn.Module, ins):

@@ -121,7 +121,22 @@ def _load_shard(path: Path) -> Dict[str, torch.Tensor]:
         from safetensors.torch import load_file
 
         return load_file(str(path))
-    return torch.load(str(path), map_location="cpu", mmap=True, weights_only=True)
+    try:
+        return torch.load(str(path), map_location="cpu", mmap=True, weights_only=True)
+    except RuntimeError as e:  # legacy (non-zip) .bin shards cannot be memory-mapped; load them whole
+        if "mmap" not in str(e) and "zip" not in str(e):
+            raise
+        return torch.load(str(path), map_location="cpu", weights_only=True)
+
+
+def expected_keys(config: Config) -> set:
+    """State-dict names of GPT(config) (rope tables and KV caches are buffers, not checkpoint entries)."""
+    from lit_gpt import GPT
+
+    with torch.device("meta"):
+        model = GPT(config)
+    return {k for k in model.state_dict() if not k.endswith((".cos", ".sin")) and k not in ("cos", "sin")
+            and ".kv_cache." not in k}
 
 
 def shard_files(checkpoint_dir: Path) -> List[Path]:
@@ -159,6 +174,13 @@ def convert_hf_checkpoint(*, checkpoint_dir: Path = Path("checkpoints/meta-llama
     partial = sorted(l for l, qkv in qkv_weights.items() if any(t is not None for t in qkv))
     if partial:
         raise ValueError(f"layers {partial} are missing q, k or v projections")
+    want = expected_keys(config)
+    missing, extra = sorted(want - set(sd)), sorted(set(sd) - want)
+    if missing or extra:  # fail here, not later as a KeyError in generate/base.py build_model
+        raise ValueError(f"converted state does not match {model_name}: missing {missing[:8]}"
+                         f"{' ...' if len(missing) > 8 else ''}, unexpected {extra[:8]}{' ...' if len(extra) > 8 else ''}")
+    # RAM: the whole converted state is held until this single save (~2 bytes/param with --dtype bfloat16, e.g.
+    # ~140 GB for Llama-2-70B); shards are memory-mapped while converting
     print("Saving converted checkpoint")
     torch.save(sd, checkpoint_dir / "lit_model.pth")
 

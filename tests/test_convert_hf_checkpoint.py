@@ -126,3 +126,28 @@ def test_convert_rejects_unsupported(tmp_path):
 
     with pytest.raises(NotImplementedError):
         convert_hf_checkpoint(checkpoint_dir=tmp_path, model_name="pythia-14m")
+
+
+def test_convert_rejects_a_layer_without_attention(tmp_path, monkeypatch):
+    """A shard set whose layer 1 has no q/k/v at all is refused at conversion time (not later as a KeyError in
+    generate/base.py build_model)."""
+    import scripts.convert_hf_checkpoint as cth
+    from lit_gpt import GPT, Config
+    from safetensors.torch import save_file
+
+    kw = dict(n_layer=2, n_embd=64, n_head=4, n_query_groups=2, intermediate_size=32)
+    cfg = Config.from_name("Llama-2-7b-hf", vocab_size=100, padding_multiple=64, block_size=32, **kw)
+    lit = {k: torch.randn_like(v) for k, v in GPT(cfg).state_dict().items() if not k.endswith(("cos", "sin"))}
+    hf = {k: v.contiguous() for k, v in _hf_state(cfg, lit).items() if ".layers.1.self_attn." not in k
+          or "o_proj" in k}
+    save_file(hf, str(tmp_path / "model.safetensors"))
+
+    class TinyConfig(Config):
+        @classmethod
+        def from_name(cls, n, **k):
+            return Config.from_name(n, vocab_size=100, padding_multiple=64, block_size=32, **kw)
+
+    monkeypatch.setattr(cth, "Config", TinyConfig)
+    with pytest.raises(ValueError, match="transformer.h.1.attn.attn.weight"):
+        cth.convert_hf_checkpoint(checkpoint_dir=tmp_path, model_name="Llama-2-7b-hf")
+    assert not (tmp_path / "lit_model.pth").exists()

@@ -1,9 +1,10 @@
 """End-to-end parity of the MI355X decode path (GPT / generate through the C-ABI kernels) against the oracle.
 
-Contract (SURVEY §7 "Hard parts"): logits within a stated tolerance of the CPU restatement run with the SAME
-dequantized weights (bf16 activations, the reference's cast points); greedy tokens identical wherever the
-oracle's top-1/top-2 margin exceeds twice the observed logit error; integer paths (KV positions, argmax tie
-break) exact. Tolerance: max |logit - oracle| <= 4% of max |oracle logit| per step.
+Contract (SURVEY §7 "Hard parts"): logits against the CPU restatement run with the SAME dequantized weights, in
+bf16 (the reference's cast points) and in float64, with the bounds of tests/parity.py (as accurate as the
+reference's bf16 path, within 3 % of it, greedy tokens equal where the margin is clear); integer paths (KV
+positions, argmax tie break) exact; alternative kernel paths of the product (graph / eager, fused / split
+attention) bit-identical.
 """
 
 import numpy as np
@@ -12,6 +13,7 @@ import torch
 
 from oracle import model as om
 from oracle import quant, synth
+from parity import check_step
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -51,7 +53,7 @@ def build_gpu_model(cfg, sd, mode, max_seq):
     return model.eval()
 
 
-def oracle_for(cfg, sd, mode):
+def oracle_for(cfg, sd, mode, dtype=torch.bfloat16):
     def deq(k, v):
         if k.endswith(".weight") and v.ndim == 2 and not k.startswith("transformer.wte"):
             vb = quant.bf16_bits_to_f32(quant.f32_to_bf16_bits(v))
@@ -62,7 +64,7 @@ def oracle_for(cfg, sd, mode):
             return quant.dequantize_nf4(*quant.quantize_nf4(vb, 64), 64)
         return v
 
-    return om.OracleGPT(cfg, sd, dtype=torch.bfloat16, weight_override=deq)
+    return om.OracleGPT(cfg, sd, dtype=dtype, weight_override=deq)
 
 
 def _watch_router_margins(ref):
@@ -99,27 +101,57 @@ def test_teacher_forced_logits_match_oracle(key, mode):
     sd = synth.state_dict(cfg, seed=21)
     T, N = 20, 12
     model = build_gpu_model(cfg, sd, mode, T + N)
-    ref = oracle_for(cfg, sd, mode)
-    ref.set_kv_cache(T + N)
     prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=21))
     stream = torch.from_numpy(synth.token_ids(N, cfg.vocab_size, seed=22))  # forced continuation
-    margins = _watch_router_margins(ref)
     got = [model(prompt.view(1, -1).to(DEV), torch.arange(T, device=DEV))[0, -1].float().cpu()]
-    exp = [ref.forward(prompt, torch.arange(T))[-1].float()]
-    ambiguous = [_routing_ambiguous(margins)]
     for i in range(N - 1):
         got.append(model(stream[i:i + 1].view(1, 1).to(DEV), torch.tensor([T + i], device=DEV))[0, -1].float().cpu())
-        exp.append(ref.forward(stream[i:i + 1], torch.tensor([T + i]))[-1].float())
-        ambiguous.append(_routing_ambiguous(margins))
+    exp, ambiguous = {}, None
+    for dt in (torch.bfloat16, torch.float64):
+        ref = oracle_for(cfg, sd, mode, dt)
+        ref.set_kv_cache(T + N)
+        margins = _watch_router_margins(ref)
+        out = [ref.forward(prompt, torch.arange(T))[-1]]
+        amb = [_routing_ambiguous(margins)]
+        for i in range(N - 1):
+            out.append(ref.forward(stream[i:i + 1], torch.tensor([T + i]))[-1])
+            amb.append(_routing_ambiguous(margins))
+        exp[dt] = out
+        ambiguous = amb if ambiguous is None else [a or b for a, b in zip(ambiguous, amb)]
     assert sum(ambiguous) <= N // 2, ambiguous
-    for g, e, amb in zip(got, exp, ambiguous):
+    for s, (g, amb) in enumerate(zip(got, ambiguous)):
         if amb:  # a router near-tie the two sides may break differently: a different expert, not an error
             continue
-        err = (g - e).abs().max().item()
-        assert err <= 0.04 * e.abs().max().item(), (err, e.abs().max().item())
-        top2 = torch.topk(e, 2).values
-        if float(top2[0] - top2[1]) > 2 * err:
-            assert int(torch.argmax(g)) == int(torch.argmax(e))
+        check_step(g, exp[torch.bfloat16][s], exp[torch.float64][s], f"{key} {mode} step {s}")
+
+
+@pytest.mark.parametrize("key", ["mha", "gqa", "mqa", "moe"])
+@pytest.mark.parametrize("mode", ["int4-g128", "bf16"])
+@torch.inference_mode()
+def test_split_attention_proj_path_is_bit_identical(key, mode):
+    """Decode with the attention split merged inside the out-projection GEMV (CausalSelfAttention.split_proj, the
+    default) == decode with the in-launch merge + plain GEMV: identical logits at every step."""
+    from lit_gpt.model import CausalSelfAttention
+
+    if mode == "bf16" and key == "moe":
+        pytest.skip("sparse-MoE experts run 4-bit weights only")
+    cfg = _cfg(key)
+    sd = synth.state_dict(cfg, seed=23)
+    T, N = 9, 10
+    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=23)).to(DEV)
+    stream = torch.from_numpy(synth.token_ids(N, cfg.vocab_size, seed=24)).to(DEV)
+    outs = {}
+    for split in (True, False):
+        CausalSelfAttention.split_proj = split
+        try:
+            model = build_gpu_model(cfg, sd, mode, T + N)
+            lg = [model(prompt.view(1, -1), torch.arange(T, device=DEV))[0, -1]]
+            for i in range(N - 1):
+                lg.append(model(stream[i:i + 1].view(1, 1), torch.tensor([T + i], device=DEV))[0, -1])
+            outs[split] = torch.stack(lg).cpu()
+        finally:
+            CausalSelfAttention.split_proj = True
+    assert torch.equal(outs[True], outs[False])
 
 
 @pytest.mark.parametrize("key,mode", [("mha", "int4-g128"), ("gqa", "int4-g128"), ("moe", "int4-g128"),
