@@ -95,6 +95,12 @@ int lga_embedding(const void* idx, int idx_is_int64, const void* table, void* ou
 int lga_add(const void* a, const void* b, void* y, long n, lga_stream_t stream);
 /* y = bf16(bf16(silu(a)) * b) (lit_gpt/model.py:715) */
 int lga_swiglu(const void* a, const void* b, void* y, long n, lga_stream_t stream);
+/* torch.nn.LayerNorm over rows of n (GPT-NeoX norm_class, lit_gpt/config.py:137-144; model.py:578-588):
+ * fp32 mean / biased variance, y = bf16((x - mean) * rstd * weight + bias); bias may be NULL */
+int lga_layernorm(const void* x, const void* weight, const void* bias, void* y, int rows, int n, float eps,
+                  lga_stream_t stream);
+/* y = bf16(gelu(a)) — GptNeoxMLP (lit_gpt/model.py:699-702): exact erf form, or tanh form when approximate_tanh */
+int lga_gelu(const void* a, void* y, long n, int approximate_tanh, lga_stream_t stream);
 
 /* -- attention over the KV cache (SDPA with the input_pos mask rows, lit_gpt/model.py:651,658-665) --------
  * q (T, H, hs); caches (G, max_seq, hs); query t attends keys 0..input_pos[t]; y (T, H*hs).

@@ -83,23 +83,28 @@ __device__ __forceinline__ float scale_of(uint32_t bits) {
   return FMT == 0 ? __uint_as_float(bits << 16) : __uint_as_float(bits);
 }
 
-// (v & mask) | 0x43004300 in ONE VOP3 op: the compiler only emits the two-op VOP2 and/or pair (gfx9 VOP3 takes
-// no literal), which makes the nibble unpack 2 ops per bf16 pair instead of 1 (+1 shift for nibbles 1-3)
-__device__ __forceinline__ uint32_t and_or_magic(uint32_t v, uint32_t mask_vgpr) {
-  uint32_t r;
-  asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "v"(mask_vgpr), "s"(0x43004300u));
-  return r;
+// (v & mask) | 0x43004300 in ONE VOP3 op (v_and_or_b32): gfx9 VOP3 takes no literal, so both constants live in
+// registers materialised once per kernel — the mask in a VGPR, the magic in an SGPR — behind asm the compiler
+// cannot constant-fold (with literals it emits the two-op VOP2 and/or pair; as inline asm of its own the op
+// would cost an s_nop hazard slot in front of every dependent v_dot2c).
+__device__ __forceinline__ uint32_t and_or_magic(uint32_t v, uint32_t mask_vgpr, uint32_t magic_sgpr) {
+  return (v & mask_vgpr) | magic_sgpr;
 }
 __device__ __forceinline__ uint32_t nibble_mask() {  // 0x000F000F in a VGPR, materialised once per kernel
   uint32_t m;
   asm volatile("v_mov_b32 %0, 0x000F000F" : "=v"(m));
   return m;
 }
+__device__ __forceinline__ uint32_t bf16_magic() {  // 0x43004300 (bf16 pair 128, 128) in an SGPR
+  uint32_t m;
+  asm volatile("s_mov_b32 %0, 0x43004300" : "=s"(m));
+  return m;
+}
 
 // dot of one 16-byte weight chunk (32 nibbles) with the LDS x chunk (4 uint4 of (x_i, x_i+4) pairs)
 template <int FMT>
 __device__ __forceinline__ float chunk_dot(const uint4 w, const uint4* xc, float xsum, const float* nf4,
-                                           uint32_t mask) {
+                                           uint32_t mask, uint32_t magic) {
   const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
   float d = 0.0f;
 #pragma unroll
@@ -109,7 +114,7 @@ __device__ __forceinline__ float chunk_dot(const uint4 w, const uint4* xc, float
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       if (FMT == 0) {
-        d = dot2_bf16(xp[s], and_or_magic(s == 0 ? wd[j] : wd[j] >> (4 * s), mask), d);
+        d = dot2_bf16(xp[s], and_or_magic(s == 0 ? wd[j] : wd[j] >> (4 * s), mask, magic), d);
       } else {
         d = fmaf(nf4[(wd[j] >> (4 * s)) & 0xF], bflo(xp[s]), d);
         d = fmaf(nf4[(wd[j] >> (4 * s + 16)) & 0xF], bfhi(xp[s]), d);
@@ -119,6 +124,39 @@ __device__ __forceinline__ float chunk_dot(const uint4 w, const uint4* xc, float
   // int4: sum x*(128+q) - 136*sum x = sum x*(q-8), as ONE explicit fma: left to -ffp-contract the compiler fuses
   // it in some kernel variants and not in others, and variants must agree bit for bit (tests compare them)
   return FMT == 0 ? __builtin_fmaf(-136.0f, xsum, d) : d;
+}
+
+// The same dot for R weight chunks (the rows / matrices of a wave) against ONE x chunk, interleaved pair by pair:
+// R independent accumulation chains give the scheduler work between each unpack and its dependent v_dot2c (one
+// chain at a time leaves an s_nop hazard slot in front of every dot). Per-row arithmetic and order are exactly
+// chunk_dot's, so the results are bit-identical.
+template <int FMT, int R>
+__device__ __forceinline__ void chunk_dot_rows(const uint4 (&w)[R], const uint4* xc, float xsum, const float* nf4,
+                                               uint32_t mask, uint32_t magic, float (&d)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) d[r] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const uint4 xv = xc[j];
+    const uint32_t xp[4] = {xv.x, xv.y, xv.z, xv.w};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const uint32_t wd = j == 0 ? w[r].x : (j == 1 ? w[r].y : (j == 2 ? w[r].z : w[r].w));
+        if (FMT == 0) {
+          d[r] = dot2_bf16(xp[s], and_or_magic(s == 0 ? wd : wd >> (4 * s), mask, magic), d[r]);
+        } else {
+          d[r] = fmaf(nf4[(wd >> (4 * s)) & 0xF], bflo(xp[s]), d[r]);
+          d[r] = fmaf(nf4[(wd >> (4 * s + 16)) & 0xF], bfhi(xp[s]), d[r]);
+        }
+      }
+    }
+  }
+  if (FMT == 0) {
+#pragma unroll
+    for (int r = 0; r < R; ++r) d[r] = __builtin_fmaf(-136.0f, xsum, d[r]);
+  }
 }
 
 // One workgroup = 4 independent waves (row slots); a wave handles RPR consecutive rows.

@@ -24,6 +24,7 @@
 //  * Epilogues: +bias, +residual (Block residual add, model.py:591-592), dual-weight SwiGLU
 //    (silu(fc_1 x) * fc_2 x, model.py:715) with the reference's bf16 rounding points.
 #include "gemv_body.h"
+#include "gemv_stream.h"
 
 namespace lga {
 
@@ -42,7 +43,10 @@ template <int RPR, int CPT, int FMT, bool DUAL>
 static void launch(const GemvArgs& a, hipStream_t stream) {
   const int waves = (a.N + RPR - 1) / RPR;
   const dim3 blocks((waves + kGemvNW - 1) / kGemvNW, a.eidx ? a.slots : 1);
-  const size_t lds = (size_t)a.K * 2 + (a.K / 32) * 4 + 16 * 4 + 16 * 4;
+  size_t lds = (size_t)a.K * 2 + (a.K / 32) * 4 + 16 * 4 + 16 * 4;
+#ifdef LGA_LAB_WG_PER_CU  // lab builds only: cap resident workgroups per CU through the LDS footprint
+  lds = lds > (163840 / LGA_LAB_WG_PER_CU) ? lds : (size_t)(163840 / LGA_LAB_WG_PER_CU);
+#endif
   constexpr int NT = kGemvNW * 64;
   const bool norm = a.norm_w != nullptr, res = a.residual != nullptr;
   if (!DUAL && a.xpart) {  // attention out-projection: activation merged from the split partials, no norm
@@ -60,10 +64,70 @@ static void launch(const GemvArgs& a, hipStream_t stream) {
   }
 }
 
+template <int RT, int CPT, int FMT, bool DUAL, bool NORM, bool RES>
+__global__ void __launch_bounds__(256) gemv_q4s_kernel(GemvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  gemv_q4_stream<RT, CPT, FMT, DUAL, NORM, RES>(a, smem);
+}
+
+static int num_cu() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// streaming form (variant bit 2): RT rows per tile, `wpc` workgroups per CU (variant bits 4..7, default 2)
+template <int RT, int CPT, int FMT, bool DUAL>
+static void launch_stream(const GemvArgs& a, int wpc, hipStream_t stream) {
+  const int tiles = (a.N + RT - 1) / RT;
+  const int blocks = max(1, min(num_cu() * wpc, (tiles + 3) / 4));
+  const size_t lds = (size_t)a.K * 2 + (a.K / 32) * 4 + 16 * 4 + 16 * 4;
+  const bool norm = a.norm_w != nullptr, res = a.residual != nullptr;
+  if (DUAL) {
+    if (norm) gemv_q4s_kernel<RT, CPT, FMT, true, true, false><<<blocks, 256, lds, stream>>>(a);
+    else gemv_q4s_kernel<RT, CPT, FMT, true, false, false><<<blocks, 256, lds, stream>>>(a);
+  } else if (norm) {
+    if (res) gemv_q4s_kernel<RT, CPT, FMT, false, true, true><<<blocks, 256, lds, stream>>>(a);
+    else gemv_q4s_kernel<RT, CPT, FMT, false, true, false><<<blocks, 256, lds, stream>>>(a);
+  } else {
+    if (res) gemv_q4s_kernel<RT, CPT, FMT, false, false, true><<<blocks, 256, lds, stream>>>(a);
+    else gemv_q4s_kernel<RT, CPT, FMT, false, false, false><<<blocks, 256, lds, stream>>>(a);
+  }
+}
+
+// The streaming form pays off for tall matrices over short rows (tools/gemv_variants.py, Llama-2-7B shapes):
+// fc_1 || fc_2 (2 x 11008 x 4096) 10.9 vs 12.2 us, lm_head (32000 x 4096) 14.3 vs 15.9 us at 3 workgroups per
+// CU; not for qkv / o_proj / mlp.proj (equal or slower). Instantiated for K <= 4096 only.
+template <int FMT, bool DUAL>
+static int dispatch_stream(const GemvArgs& a, int variant, hipStream_t stream) {
+  const int cpt = (a.K / 32 + 63) / 64;
+  const int wpc = (variant >> 4) & 15 ? (variant >> 4) & 15 : (DUAL ? 2 : 3);
+  switch (cpt) {
+    case 1: launch_stream<(DUAL ? 1 : 2), 1, FMT, DUAL>(a, wpc, stream); break;
+    case 2: launch_stream<(DUAL ? 1 : 2), 2, FMT, DUAL>(a, wpc, stream); break;
+    default:
+      lga_set_error("lga_q4_gemv: the streaming form covers K <= 4096");
+      return (int)hipErrorInvalidValue;
+  }
+  return 0;
+}
+
+static bool stream_default(int N, int K, bool dual) {
+  return K <= 4096 && (dual ? N >= 8192 : N >= 24000);
+}
+
 // variant: 0 = fewer rows per wave (more waves), 1 = more rows per wave; < 0 = heuristic
 template <int FMT, bool DUAL>
 static int dispatch(const GemvArgs& a, int variant, hipStream_t stream) {
   const int cpt = (a.K / 32 + 63) / 64;  // chunks per lane (== uint4 of x per thread)
+  if (!a.eidx && !a.xpart && a.K <= 4096 &&
+      ((variant >= 0 && (variant & 4)) || (variant < 0 && stream_default(a.N, a.K, DUAL))))
+    return dispatch_stream<FMT, DUAL>(a, variant < 0 ? 4 : variant, stream);
   if (variant < 0) {
     const long rows = DUAL ? 2L * a.N : a.N;
     variant = rows >= 24000 ? 1 : 0;  // tall matrices: more rows per wave keep the grid ~3-4 workgroups per CU

@@ -88,8 +88,13 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
     if (XC) {
       xpart_load(a.xpart, a.xsplits, a.xhs, u, 0, xp[i]);
     } else {
+#ifdef LGA_LAB_NOX  // lab builds only: cost of the activation fetch
+      xr[i] = make_uint4(0x3F803F80u + u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+      if (NORM) nr[i] = xr[i];
+#else
       xr[i] = ((const uint4*)a.x)[u];
       if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
+#endif
     }
   }
   // 2. every weight / scale / residual load of this wave (rows past N re-read row N-1; never stored), issued in
@@ -106,10 +111,18 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
     for (int i = 0; i < RPR; ++i) {
       const size_t n = (size_t)min(row0 + i, a.N - 1);
       w[i][j] = ld_nt16(a.qw + n * (a.K / 2) + (size_t)c * 16);
+#ifdef LGA_LAB_NOSCALE  // lab builds only (tools/gemv_variants.py): cost of the scale loads
+      s[i][j] = 0x3F80u + (uint32_t)g;
+#else
       s[i][j] = load_scale_bits<FMT>(a.sc, n * groups + g);
+#endif
       if (DUAL) {
         w2[i][j] = ld_nt16(a.qw2 + n * (a.K / 2) + (size_t)c * 16);
+#ifdef LGA_LAB_NOSCALE
+        s2[i][j] = 0x3F80u + (uint32_t)g;
+#else
         s2[i][j] = load_scale_bits<FMT>(a.sc2, n * groups + g);
+#endif
       }
     }
   }
@@ -176,7 +189,7 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
   LGA_GTRACE(4);
 
   // 4. dequant-dot every row of this wave, then one butterfly for all of them
-  const uint32_t nmask = nibble_mask();
+  const uint32_t nmask = nibble_mask(), nmagic = bf16_magic();
   float part[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) part[i] = 0.0f;
@@ -187,17 +200,43 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
     const int cc = min(c, NC - 1);
     const uint4* xc = xl + cc * 4;
     const float xs = xsum[cc];
+#ifdef LGA_LAB_NOCOMPUTE  // lab builds only: cost of the dequant-dot (weights folded, not multiplied)
 #pragma unroll
     for (int i = 0; i < RPR; ++i) {
-      const float d = chunk_dot<FMT>(w[i][j], xc, xs, nf4, nmask);
-      if (DUAL) {  // value index = 2*row + matrix (so the pair of one row lands in lanes l and l^8 / l^16 / l^32)
+      const float d = __uint_as_float((w[i][j].x ^ w[i][j].y ^ w[i][j].z ^ w[i][j].w) & 0x3FFFFFFFu) + xs;
+      if (DUAL) {
         part[2 * i] = fmaf(ok ? scale_of<FMT>(s[i][j]) : 0.0f, d, part[2 * i]);
-        const float d2 = chunk_dot<FMT>(w2[i][j], xc, xs, nf4, nmask);
+        const float d2 = __uint_as_float((w2[i][j].x ^ w2[i][j].y ^ w2[i][j].z ^ w2[i][j].w) & 0x3FFFFFFFu);
         part[2 * i + 1] = fmaf(ok ? scale_of<FMT>(s2[i][j]) : 0.0f, d2, part[2 * i + 1]);
       } else {
         part[i] = fmaf(ok ? scale_of<FMT>(s[i][j]) : 0.0f, d, part[i]);
       }
     }
+#else
+    // all rows (and both matrices) of chunk j in one interleaved pass; value index = 2*row + matrix (DUAL)
+    uint4 wj[R];
+#pragma unroll
+    for (int i = 0; i < RPR; ++i) {
+      if (DUAL) {
+        wj[2 * i] = w[i][j];
+        wj[2 * i + 1] = w2[DUAL ? i : 0][DUAL ? j : 0];
+      } else {
+        wj[i] = w[i][j];
+      }
+    }
+    float d[R];
+    chunk_dot_rows<FMT, R>(wj, xc, xs, nf4, nmask, nmagic, d);
+#pragma unroll
+    for (int i = 0; i < RPR; ++i) {
+      if (DUAL) {
+        part[2 * i] = fmaf(ok ? scale_of<FMT>(s[i][j]) : 0.0f, d[2 * i], part[2 * i]);
+        part[2 * i + 1] = fmaf(ok ? scale_of<FMT>(s2[DUAL ? i : 0][DUAL ? j : 0]) : 0.0f, d[2 * i + 1],
+                               part[2 * i + 1]);
+      } else {
+        part[i] = fmaf(ok ? scale_of<FMT>(s[i][j]) : 0.0f, d[i], part[i]);
+      }
+    }
+#endif
   }
   const float tot = butterfly<R>(part, lane);
   const int vi = bfly_index<R>(lane);  // value index held by this lane

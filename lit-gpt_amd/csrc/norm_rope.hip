@@ -6,6 +6,9 @@
 //   lga_embedding      token-embedding gather (model.py:515)
 //   lga_add            bf16 residual add (Block.forward :591-592) when the add cannot ride a GEMV epilogue (TP)
 //   lga_swiglu         silu(a) * b with the reference's rounding points (LLaMAMLP.forward :715)
+//   lga_layernorm      torch.nn.LayerNorm (GPT-NeoX / pythia norm_class, reference config.py:137-144): fp32 mean and
+//                      variance, (x - mean) * rstd * w + b in fp32, one bf16 cast
+//   lga_gelu           GptNeoxMLP's activation (model.py:699-702): F.gelu exact (erf) or tanh, fp32, one bf16 cast
 #include "common.h"
 
 namespace lga {
@@ -26,6 +29,50 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict
   __syncthreads();
   const float rs = 1.0f / sqrtf((red[0] + red[1] + red[2] + red[3]) / (float)n + eps);
   for (int i = threadIdx.x; i < n; i += 256) yr[i] = f2bf(__fmul_rn(bf2f(w[i]), __fmul_rn(bf2f(xr[i]), rs)));
+}
+
+__global__ void __launch_bounds__(256) layernorm_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
+                                                        const uint16_t* __restrict__ b, uint16_t* __restrict__ y,
+                                                        int n, float eps) {
+  const size_t row = blockIdx.x;
+  const uint16_t* xr = x + row * n;
+  uint16_t* yr = y + row * n;
+  __shared__ float red[4];
+  float s = 0.0f;
+  for (int i = threadIdx.x; i < n; i += 256) s += bf2f(xr[i]);
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  const float mean = ((red[0] + red[1]) + (red[2] + red[3])) / (float)n;
+  __syncthreads();
+  float ss = 0.0f;  // two-pass variance (biased, as torch.nn.LayerNorm)
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float d = bf2f(xr[i]) - mean;
+    ss = fmaf(d, d, ss);
+  }
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float rstd = 1.0f / sqrtf(((red[0] + red[1]) + (red[2] + red[3])) / (float)n + eps);
+  for (int i = threadIdx.x; i < n; i += 256) {
+    const float v = __fmul_rn(__fmul_rn(bf2f(xr[i]) - mean, rstd), bf2f(w[i]));
+    yr[i] = f2bf(b ? v + bf2f(b[i]) : v);
+  }
+}
+
+__global__ void __launch_bounds__(256) gelu_kernel(const uint16_t* __restrict__ a, uint16_t* __restrict__ y, size_t n,
+                                                   int approximate_tanh) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    const float v = bf2f(a[i]);
+    float g;
+    if (approximate_tanh) {
+      const float inner = 0.7978845608028654f * (v + 0.044715f * v * v * v);
+      g = 0.5f * v * (1.0f + tanhf(inner));
+    } else {
+      g = 0.5f * v * (1.0f + erff(v * 0.7071067811865476f));
+    }
+    y[i] = f2bf(g);
+  }
 }
 
 // grid (T, G): one workgroup per (token, query group); slots 0..qpk-1 = q heads, qpk = k, qpk+1 = v
@@ -144,5 +191,20 @@ extern "C" int lga_swiglu(const void* a, const void* b, void* y, long n, hipStre
   LGA_CHECK_ARG(a && b && y && n > 0, "lga_swiglu: bad arguments");
   lga::swiglu_kernel<<<lga::elementwise_grid(n), 256, 0, stream>>>((const uint16_t*)a, (const uint16_t*)b,
                                                                     (uint16_t*)y, (size_t)n);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_layernorm(const void* x, const void* weight, const void* bias, void* y, int rows, int n, float eps,
+                             hipStream_t stream) {
+  LGA_CHECK_ARG(x && weight && y && rows > 0 && n > 0, "lga_layernorm: bad arguments");
+  lga::layernorm_kernel<<<rows, 256, 0, stream>>>((const uint16_t*)x, (const uint16_t*)weight, (const uint16_t*)bias,
+                                                   (uint16_t*)y, n, eps);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_gelu(const void* a, void* y, long n, int approximate_tanh, hipStream_t stream) {
+  LGA_CHECK_ARG(a && y && n > 0, "lga_gelu: bad arguments");
+  lga::gelu_kernel<<<lga::elementwise_grid(n), 256, 0, stream>>>((const uint16_t*)a, (uint16_t*)y, (size_t)n,
+                                                                  approximate_tanh);
   LGA_LAUNCH_RETURN();
 }

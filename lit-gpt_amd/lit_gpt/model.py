@@ -22,6 +22,7 @@ positions > 256 that the reference's bf16 ``init_tensor`` context produces.
 from __future__ import annotations
 
 import math
+import os
 from typing import Any, Optional, Tuple
 
 import torch
@@ -209,12 +210,11 @@ class Block(nn.Module):
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
                 input_pos: Optional[torch.Tensor] = None) -> torch.Tensor:
         c = self.config
-        if c.parallel_residual or c.shared_attention_norm:
-            if c.shared_attention_norm and not c.parallel_residual:
-                raise NotImplementedError("No checkpoint amongst the ones we support uses this configuration"
-                                          " (non-parallel residual and shared attention norm).")
-            raise NotImplementedError("parallel-residual (GPT-NeoX) blocks have no MI355X kernels in this build; "
-                                      "config 1 (pythia) runs on the CPU oracle")
+        if c.shared_attention_norm and not c.parallel_residual:
+            raise NotImplementedError("No checkpoint amongst the ones we support uses this configuration"
+                                      " (non-parallel residual and shared attention norm).")
+        if c.parallel_residual:
+            return self._parallel_forward(x, cos, sin, mask, input_pos)
         if not isinstance(self.norm_1, RMSNorm) or not isinstance(self.mlp, (LLaMAMLP, LLaMAMoE)):
             raise NotImplementedError(f"{type(self.mlp).__name__} / {type(self.norm_1).__name__} blocks have no "
                                       "MI355X kernels in this build")
@@ -239,6 +239,20 @@ class Block(nn.Module):
         return ops.add(self.mlp(self.norm_2(x)).contiguous(), x)
 
 
+    def _parallel_forward(self, x, cos, sin, mask, input_pos) -> torch.Tensor:
+        """GPT-NeoX block (reference model.py:572-593, parallel_residual): n_1 = norm_1(x), h = attn(n_1),
+        n_2 = n_1 if shared_attention_norm else norm_2(x), x = mlp(n_2) + h + x — the reference's association:
+        bf16(mlp + h) (fused into the mlp.proj epilogue) then + x. Under tensor parallelism the attn / mlp outputs
+        go through their all-reduce hooks first (generate/tp.py), as in the reference."""
+        n_1 = self.norm_1(x)
+        h = self.attn(n_1, cos, sin, mask, input_pos).contiguous()
+        n_2 = n_1 if self.config.shared_attention_norm else self.norm_2(x)
+        if self.mlp._forward_hooks:  # TP: the hook must see the mlp output alone
+            m = ops.add(self.mlp(n_2).contiguous(), h)
+        else:
+            m = self.mlp(n_2, residual=h)
+        return ops.add(m.contiguous(), x.contiguous()).view_as(x)
+
 
 class CausalSelfAttention(nn.Module):
     def __init__(self, config: Config) -> None:
@@ -253,8 +267,10 @@ class CausalSelfAttention(nn.Module):
     # rope_kv_append + attention path (bit-identical; tests compare the two)
     fuse_decode = True
     # ...and with split_proj the attention leaves its per-split partials to the out-projection GEMV, which merges
-    # them in its prologue (lga_attention_decode_split + lga_q4_gemv_attn; bit-identical to fused + gemv)
-    split_proj = True
+    # them in its prologue (lga_attention_decode_split + lga_q4_gemv_attn; bit-identical to fused + gemv). Off by
+    # default: at Llama-2-7B decode the attention gets 1.5 us faster but the GEMV reads 4x its weight bytes in
+    # partials and gets 1.6-2.2 us slower (profiles/r02_*). LGA_SPLIT_PROJ=1 turns it on.
+    split_proj = os.environ.get("LGA_SPLIT_PROJ", "0") == "1"
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
                 input_pos: Optional[torch.Tensor] = None, *, norm: Optional["RMSNorm"] = None,
@@ -335,7 +351,9 @@ class CausalSelfAttention(nn.Module):
 
 
 class GptNeoxMLP(nn.Module):
-    """Kept for the API / TP isinstance checks (model.py:691-702); no MI355X kernels in this build."""
+    """GPT-NeoX / pythia MLP (reference model.py:691-702): fc (+bias) -> GELU -> proj (+bias). The Linears run the
+    GEMV / GEMM kernels (4-bit or bf16), the activation ``lga_gelu`` (exact erf, or tanh per
+    ``config.gelu_approximate``) with the reference's bf16 rounding points."""
 
     def __init__(self, config: Config) -> None:
         super().__init__()
@@ -343,8 +361,14 @@ class GptNeoxMLP(nn.Module):
         self.proj = nn.Linear(config.intermediate_size, config.n_embd, bias=config.bias)
         self.config = config
 
-    def forward(self, x: torch.Tensor) -> torch.Tensor:
-        raise NotImplementedError("GptNeoxMLP runs on the CPU oracle only in this build")
+    def forward(self, x: torch.Tensor, *, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``residual`` fuses an add into the proj epilogue (bf16(bf16(proj(x)) + residual)); Block uses it for the
+        parallel residual's ``mlp(n_2) + h``."""
+        if not x.is_cuda:
+            _gpu_only("GptNeoxMLP")
+        h = _lin(self.fc, x)
+        h = ops.gelu(h.contiguous(), self.config.gelu_approximate)
+        return _lin(self.proj, h, residual=residual)
 
 
 class LLaMAMLP(nn.Module):
@@ -471,7 +495,17 @@ class LLaMAMoE(nn.Module):
         return ops.moe_combine(eout.contiguous(), probs, ids, residual=res).view(*lead, C)
 
 
-LayerNorm = nn.LayerNorm  # config.norm_class for GPT-NeoX (reference config.py:137-144)
+class LayerNorm(nn.LayerNorm):
+    """config.norm_class for GPT-NeoX (reference config.py:137-144: torch.nn.LayerNorm) on the ``lga_layernorm``
+    kernel: same parameters (weight, bias) and state-dict names, fp32 statistics, one bf16 cast."""
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not x.is_cuda:
+            _gpu_only("LayerNorm")
+        w = self.weight.to(torch.bfloat16) if self.weight.dtype != torch.bfloat16 else self.weight
+        b = None if self.bias is None else (self.bias.to(torch.bfloat16) if self.bias.dtype != torch.bfloat16
+                                            else self.bias)
+        return ops.layernorm(x.contiguous(), w, b, self.eps)
 
 
 class KVCache(nn.Module):

@@ -49,6 +49,8 @@ SIGNATURES = {
     "lga_embedding": [_P, _I, _P, _P, _I, _I, _I, _P],
     "lga_add": [_P, _P, _P, _L, _P],
     "lga_swiglu": [_P, _P, _P, _L, _P],
+    "lga_layernorm": [_P, _P, _P, _P, _I, _I, _F, _P],
+    "lga_gelu": [_P, _P, _L, _I, _P],
     "lga_attention": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_attention_workspace_bytes": [_I, _I, _I, _I],
     "lga_attention_decode_fused": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
@@ -377,6 +379,26 @@ def add(a, b, out=None):
     y = out if out is not None else torch.empty_like(a)
     _check(load_library().lga_add(_dev(a, "a", torch.bfloat16), _dev(b, "b", torch.bfloat16),
                                   _dev(y, "y", torch.bfloat16), a.numel(), _stream()))
+    return y
+
+
+def layernorm(x, weight, bias, eps, out=None):
+    """torch.nn.LayerNorm over the last dim of a contiguous bf16 GPU tensor (GPT-NeoX)."""
+    n = x.shape[-1]
+    y = out if out is not None else torch.empty_like(x)
+    _check(load_library().lga_layernorm(_dev(x, "x", torch.bfloat16), _dev(weight, "weight", torch.bfloat16),
+                                        _opt(bias, "bias", torch.bfloat16), _dev(y, "y", torch.bfloat16),
+                                        x.numel() // n, n, float(eps), _stream()))
+    return y
+
+
+def gelu(a, approximate: str = "none", out=None):
+    """bf16(F.gelu(a, approximate)) (GptNeoxMLP)."""
+    if approximate not in ("none", "tanh"):
+        raise ValueError(f"gelu approximate must be 'none' or 'tanh', got {approximate!r}")
+    y = out if out is not None else torch.empty_like(a)
+    _check(load_library().lga_gelu(_dev(a, "a", torch.bfloat16), _dev(y, "y", torch.bfloat16), a.numel(),
+                                   int(approximate == "tanh"), _stream()))
     return y
 
 

@@ -114,22 +114,16 @@ def linear(x: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor] = None) -
 
 @dataclass
 class Cache:
-    """Per-layer K/V for positions written so far (lit_gpt/model.py:776-799); stored un-expanded (G heads).
-
-    ``k`` / ``v`` hold the values in the activation dtype (the reference's cache dtype); ``kf`` / ``vf`` hold the
-    same values widened to fp32 once at append time, so a decode step's attention reads the cache without
-    re-casting (or re-expanding) the whole context every step."""
+    """Per-layer K/V for positions written so far (lit_gpt/model.py:776-799), in the activation dtype (the
+    reference's cache dtype); stored un-expanded (G heads: the attention below runs SDPA with enable_gqa, the same
+    math as the reference's expand-to-H-heads)."""
     k: List[torch.Tensor] = field(default_factory=list)  # (G, S, hs) per layer
     v: List[torch.Tensor] = field(default_factory=list)
-    kf: List[torch.Tensor] = field(default_factory=list)
-    vf: List[torch.Tensor] = field(default_factory=list)
 
     def write(self, i: int, pos, k: torch.Tensor, v: torch.Tensor) -> None:
         """KVCache.forward's index_copy_ (model.py:788-795) at positions ``pos`` of layer i; k, v (G, T, hs)."""
         self.k[i][:, pos] = k
         self.v[i][:, pos] = v
-        self.kf[i][:, pos] = self.k[i][:, pos].float()
-        self.vf[i][:, pos] = self.v[i][:, pos].float()
 
 
 class OracleGPT:
@@ -161,9 +155,7 @@ class OracleGPT:
         shape = (c.n_query_groups, S, c.head_size)
         self.cache = Cache(
             k=[torch.zeros(shape, dtype=self.dtype) for _ in range(c.n_layer)],
-            v=[torch.zeros(shape, dtype=self.dtype) for _ in range(c.n_layer)],
-            kf=[torch.zeros(shape, dtype=torch.float32) for _ in range(c.n_layer)],
-            vf=[torch.zeros(shape, dtype=torch.float32) for _ in range(c.n_layer)])
+            v=[torch.zeros(shape, dtype=self.dtype) for _ in range(c.n_layer)])
 
     def _norm(self, prefix: str, x: torch.Tensor) -> torch.Tensor:
         c = self.cfg
@@ -187,26 +179,21 @@ class OracleGPT:
         n = c.rope_n_elem
         q = torch.cat((apply_rope(q[..., :n], cos, sin), q[..., n:]), dim=-1)
         k = torch.cat((apply_rope(k[..., :n], cos, sin), k[..., n:]), dim=-1)
+        scale = 1.0 / math.sqrt(hs)
         if input_pos is not None:
             if self.cache is None:
                 raise TypeError("You need to call `gpt.set_kv_cache()`")
             self.cache.write(i, input_pos, k, v)
-            L = int(input_pos.max()) + 1  # keys beyond the last written position are masked out
-            kk, vv = self.cache.kf[i][:, :L], self.cache.vf[i][:, :L]  # fp32 views, no per-step copy
-            allowed = torch.arange(L)[None, :] <= input_pos[:, None]  # (T, L) = mask_cache rows
+            kk, vv = self.cache.k[i], self.cache.v[i]  # the whole cache, as KVCache.forward returns it
+            # mask_cache rows input_pos (model.py:509): key j visible to query t iff j <= input_pos[t]
+            mask = torch.arange(kk.size(1))[None, :] <= input_pos[:, None]
+            y = F.scaled_dot_product_attention(q[None], kk[None], vv[None], attn_mask=mask[None, None], scale=scale,
+                                               enable_gqa=G != H)
         else:
-            kk, vv = k.float(), v.float()
-            L = T
-            allowed = torch.ones(T, T, dtype=torch.bool).tril()
-        # the reference expands k/v from G groups to H heads (model.py:633-635); the same math without the copy:
-        # the qpk heads of group g attend g's keys, so fold them into the row dimension of one (G, qpk*T, L) matmul
-        scale = 1.0 / math.sqrt(hs)
-        qg = q.float().reshape(G, qpk * T, hs)
-        att = torch.matmul(qg, kk.transpose(-1, -2)) * scale
-        att = att.masked_fill(~allowed.repeat(qpk, 1), float("-inf"))
-        att = torch.softmax(att, dim=-1)
-        y = torch.matmul(att, vv).to(self.dtype).reshape(H, T, hs)
-        y = y.transpose(0, 1).reshape(T, H * hs)
+            y = F.scaled_dot_product_attention(q[None], k[None], v[None], is_causal=True, scale=scale,
+                                               enable_gqa=G != H)
+        # SDPA in the activation dtype, exactly the reference's call (model.py:658-665)
+        y = y[0].transpose(0, 1).reshape(T, H * hs)
         return self._lin(f"transformer.h.{i}.attn.proj", y)
 
     def _mlp(self, i: int, x: torch.Tensor) -> torch.Tensor:

@@ -31,8 +31,8 @@ AGREE_REL = 0.03
 
 
 def rel_err(got, exp):
-    got = np.asarray(got, dtype=np.float64)
-    exp = np.asarray(exp, dtype=np.float64)
+    got = np.asarray(_np(got), dtype=np.float64)
+    exp = np.asarray(_np(exp), dtype=np.float64)
     err = np.abs(got - exp)
     return (float(err.max() / np.abs(exp).max()), math.sqrt(float((err ** 2).mean()) / float((exp ** 2).mean())),
             float(err.max()))

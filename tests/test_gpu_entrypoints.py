@@ -1,12 +1,13 @@
 """GPU tests for the remaining inference entry points over the same kernels: generate/sequentially.py (layer
 placement; reference tests/test_generate_sequentially.py) and chat/base.py streaming (reference
-tests/test_chat.py). Outputs must be token-identical to generate/base.py's on the same weights."""
+tests/test_chat.py). Outputs must be token-identical to generate/base.py's on the same weights AND follow the CPU
+oracle (the restatement of the reference, teacher-forced on the produced tokens) wherever its margin is clear."""
 
 import pytest
 import torch
 
 from oracle import synth
-from test_gpu_model import DEV, _cfg, build_gpu_model
+from test_gpu_model import DEV, _cfg, assert_tokens_follow_oracle, build_gpu_model
 
 pytestmark = pytest.mark.gpu
 
@@ -38,6 +39,7 @@ def test_sequential_partitions_match_single_device(key, mode, parts, use_graph):
     assert len(hooked) == cfg.n_layer - cfg.n_layer // parts
     y = generate(model, prompt, T + N, temperature=0.0, use_graph=use_graph).cpu()
     assert torch.equal(y, y_ref)
+    assert assert_tokens_follow_oracle(cfg, sd, mode, prompt.cpu(), y) >= N // 4
 
 
 @torch.inference_mode()
@@ -52,6 +54,7 @@ def test_chat_stream_matches_generate_and_stops():
     model = build_gpu_model(cfg, sd, "int4-g128", T + N)
     y = generate(model, prompt, T + N, temperature=0.0).cpu()
     new = [int(v) for v in y[T:]]
+    assert assert_tokens_follow_oracle(cfg, sd, "int4-g128", prompt.cpu(), y) >= N // 4
     for use_graph in (True, False):
         _reset(model)
         got = [int(t) for t in chat_generate(model, prompt, T + N, temperature=0.0, use_graph=use_graph)]

@@ -83,7 +83,7 @@ def _deq(ops, w, fmt, group):
 
 @pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (0, 32)])
 @pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 11008), (1000, 256), (77, 1376), (640, 4096)])
-@pytest.mark.parametrize("variant", [-1, 0, 3, 6])
+@pytest.mark.parametrize("variant", [-1, 0, 3, 4, 38])  # 4 / 38: the streaming form (2 / 3 workgroups per CU)
 def test_gemv_matches_reference(ops, fmt, group, N, K, variant):
     if K % group:
         pytest.skip("group does not divide K")
@@ -116,15 +116,16 @@ def test_gemv_fused_norm_residual_bias(ops, fmt, group):
 
 
 @pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
-def test_gemv_swiglu(ops, fmt, group):
+@pytest.mark.parametrize("variant", [-1, 0, 1, 36])  # -1 picks the streaming form at this shape, 0 / 1 one-shot
+def test_gemv_swiglu(ops, fmt, group, variant):
     N, K = 11008, 4096
     w1, w2 = _weights(N, K, "s1"), _weights(N, K, "s2")
     x = bf16_np(synth.normal((K,), "xs", 5, 1.0))
     nw = bf16_np(np.ones(K, np.float32))
     q1, s1 = ops.quantize(torch.from_numpy(w1).to(DEV), fmt, group)
     q2, s2 = ops.quantize(torch.from_numpy(w2).to(DEV), fmt, group)
-    y = ops.q4_gemv_swiglu(to_dev_bf16(x), q1, s1, q2, s2, N, K, group, fmt, norm_weight=to_dev_bf16(nw)
-                           ).float().cpu().numpy()
+    y = ops.q4_gemv_swiglu(to_dev_bf16(x), q1, s1, q2, s2, N, K, group, fmt, norm_weight=to_dev_bf16(nw),
+                           variant=variant).float().cpu().numpy()
     xn = om.rms_norm(torch.from_numpy(x).bfloat16(), torch.from_numpy(nw).bfloat16(), 1e-5).float().numpy()
     a = _ref_linear(xn, _deq(ops, w1, fmt, group))
     b = _ref_linear(xn, _deq(ops, w2, fmt, group))

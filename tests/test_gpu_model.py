@@ -129,8 +129,9 @@ def test_teacher_forced_logits_match_oracle(key, mode):
 @pytest.mark.parametrize("mode", ["int4-g128", "bf16"])
 @torch.inference_mode()
 def test_split_attention_proj_path_is_bit_identical(key, mode):
-    """Decode with the attention split merged inside the out-projection GEMV (CausalSelfAttention.split_proj, the
-    default) == decode with the in-launch merge + plain GEMV: identical logits at every step."""
+    """Decode with the attention split merged inside the out-projection GEMV (CausalSelfAttention.split_proj,
+    LGA_SPLIT_PROJ=1) == decode with the in-launch merge + plain GEMV (the default): identical logits at every
+    step."""
     from lit_gpt.model import CausalSelfAttention
 
     if mode == "bf16" and key == "moe":
@@ -141,6 +142,7 @@ def test_split_attention_proj_path_is_bit_identical(key, mode):
     prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=23)).to(DEV)
     stream = torch.from_numpy(synth.token_ids(N, cfg.vocab_size, seed=24)).to(DEV)
     outs = {}
+    default = CausalSelfAttention.split_proj
     for split in (True, False):
         CausalSelfAttention.split_proj = split
         try:
@@ -150,7 +152,7 @@ def test_split_attention_proj_path_is_bit_identical(key, mode):
                 lg.append(model(stream[i:i + 1].view(1, 1), torch.tensor([T + i], device=DEV))[0, -1])
             outs[split] = torch.stack(lg).cpu()
         finally:
-            CausalSelfAttention.split_proj = True
+            CausalSelfAttention.split_proj = default
     assert torch.equal(outs[True], outs[False])
 
 
@@ -185,6 +187,27 @@ def test_greedy_generate_graph_equals_eager_and_oracle(key, mode):
             assert int(y_graph[T + i]) == int(top2.indices[0]), f"step {i}"
         if i + 1 < N:
             lg = ref.forward(y_graph[T + i:T + i + 1], torch.tensor([T + i]))[-1].float()
+
+
+def assert_tokens_follow_oracle(cfg, sd, mode, prompt, tokens, margin_rel=0.03):
+    """Teacher-force the bf16 oracle on the GPU's greedy tokens: each GPU token must be the oracle's argmax unless
+    the oracle's top-1/top-2 margin is within the logit agreement bound (tests/parity.py AGREE_REL) or a MoE router
+    choice of that step was a near-tie. Returns the number of steps checked."""
+    T = prompt.numel()
+    N = tokens.numel() - T
+    ref = oracle_for(cfg, sd, mode)
+    ref.set_kv_cache(T + N)
+    margins = _watch_router_margins(ref)
+    lg = ref.forward(prompt.cpu(), torch.arange(T))[-1].float()
+    checked = 0
+    for i in range(N):
+        top2 = torch.topk(lg, 2)
+        if not _routing_ambiguous(margins) and float(top2.values[0] - top2.values[1]) > margin_rel * lg.abs().max().item():
+            assert int(tokens[T + i]) == int(top2.indices[0]), f"step {i}: GPU token differs from the oracle"
+            checked += 1
+        if i + 1 < N:
+            lg = ref.forward(tokens[T + i:T + i + 1].cpu(), torch.tensor([T + i]))[-1].float()
+    return checked
 
 
 @torch.inference_mode()
