@@ -40,6 +40,12 @@ int lga_device_info(int device, int* n_cu, char* arch_name, int arch_len);
  * scales: (N, K/group) bf16 for Q4G, fp32 for NF4. Layout spec: oracle/quant.py. */
 int lga_quantize(const void* w, int w_is_bf16, uint8_t* qweight, void* scales, int N, int K, int group, int fmt,
                  lga_stream_t stream);
+/* bitsandbytes double quantization of nf4 statistics ("bnb.nf4-dq"; quantize_4bit(compress_statistics=True),
+ * generate/base.py:105): absmax (n fp32, bnb's flattened 64-blocks, i.e. the NF4 scales of lga_quantize) is
+ * replaced in place by code[q] * absmax2 + offset — q = nearest entry of `code` (the 256-entry signed dynamic
+ * map, device fp32) to (absmax - offset) / absmax2 per block of 256, offset = mean(absmax) (written to
+ * offset_out) — the statistic bnb's dequantize_4bit reconstructs. */
+int lga_nf4_double_quant(float* absmax, long n, const float* code, float* offset_out, lga_stream_t stream);
 
 /* -- decode GEMV, M = 1 (bnb gemv_4bit for one-token inputs; every Linear of lit_gpt/model.py:519,619,656,
  *    712-716) -----------------------------------------------------------------------------------------------

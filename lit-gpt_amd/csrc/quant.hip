@@ -6,6 +6,12 @@
 //   LGA_FMT_Q4G (0): symmetric int4, group G along K, scale = bf16(absmax / 7), nibble = q + 8
 //   LGA_FMT_NF4 (1): bnb NF4 codebook, block G along K, fp32 absmax
 // Packed byte j of a row holds k = 2j (low nibble) and k = 2j + 1 (high nibble).
+//
+// lga_nf4_double_quant: bitsandbytes' double quantization of the nf4 statistics ("bnb.nf4-dq",
+// quantize_4bit(compress_statistics=True), generate/base.py:105): offset = mean(absmax), the centred absmax
+// quantized in blocks of 256 to the signed 8-bit dynamic map (kQuantizeBlockwise + dQuantize<0>), and the
+// statistic the kernels scale by replaced IN PLACE by its dequantized value code[q] * absmax2 + offset (fp32
+// multiply, fp32 add — dequantize_4bit's order). Restated and tested against oracle/quant.py double_quant_absmax.
 #include "common.h"
 
 namespace lga {
@@ -67,7 +73,78 @@ __global__ void __launch_bounds__(256) quantize_kernel(const void* __restrict__ 
   }
 }
 
+// offset = mean(absmax), accumulated in fp64 in a fixed order (one workgroup)
+__global__ void __launch_bounds__(1024) absmax_mean_kernel(const float* __restrict__ a, long n, float* __restrict__ out) {
+  __shared__ double part[1024];
+  double s = 0.0;
+  for (long i = threadIdx.x; i < n; i += 1024) s += (double)a[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (int w = 512; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = (float)(part[0] / (double)n);
+}
+
+// dQuantize<0> of bitsandbytes' kQuantizeBlockwise: binary search in the sorted 256-entry code, then the nearer
+// of the bracketing pair (midpoint rule, ties to the lower pivot / pivot as the upstream comparisons fall)
+__device__ int dq_index(const float* code, float x) {
+  int pivot = 127, upper_pivot = 255, lower_pivot = 0;
+  float lower = -1.0f, upper = 1.0f, val = code[pivot];
+  for (int i = 64; i > 0; i >>= 1) {
+    if (x > val) {
+      lower_pivot = pivot;
+      lower = val;
+      pivot += i;
+    } else {
+      upper_pivot = pivot;
+      upper = val;
+      pivot -= i;
+    }
+    val = code[pivot];
+  }
+  if (upper_pivot == 255) upper = code[upper_pivot];
+  if (lower_pivot == 0) lower = code[lower_pivot];
+  if (x > val) return x > __fmul_rn(__fadd_rn(upper, val), 0.5f) ? upper_pivot : pivot;
+  return x < __fmul_rn(__fadd_rn(lower, val), 0.5f) ? lower_pivot : pivot;
+}
+
+// one workgroup per 256 statistics
+__global__ void __launch_bounds__(256) double_quant_kernel(float* __restrict__ a, long n, const float* __restrict__ code_g,
+                                                           const float* __restrict__ offset_p) {
+  __shared__ float code[256];
+  __shared__ float red[4];
+  code[threadIdx.x] = code_g[threadIdx.x];
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const float offset = *offset_p;
+  const float v = i < n ? __fsub_rn(a[i], offset) : 0.0f;
+  float m = fabsf(v);
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  const float amax2 = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  if (i >= n) return;
+  int q;
+  if (amax2 > 0.0f) {
+    q = dq_index(code, __fmul_rn(v, __fdiv_rn(1.0f, amax2)));
+  } else {  // all statistics of the block equal the offset: the code's zero
+    q = 0;
+    for (int j = 1; j < 256; ++j)
+      if (fabsf(code[j]) < fabsf(code[q])) q = j;
+  }
+  a[i] = __fadd_rn(__fmul_rn(code[q], amax2), offset);
+}
+
 }  // namespace lga
+
+extern "C" int lga_nf4_double_quant(float* absmax, long n, const float* code, float* offset_out,
+                                    hipStream_t stream) {
+  LGA_CHECK_ARG(absmax && code && offset_out && n > 0, "lga_nf4_double_quant: bad arguments");
+  lga::absmax_mean_kernel<<<1, 1024, 0, stream>>>(absmax, n, offset_out);
+  lga::double_quant_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(absmax, n, code, offset_out);
+  LGA_LAUNCH_RETURN();
+}
 
 extern "C" int lga_quantize(const void* w, int w_is_bf16, uint8_t* qweight, void* scales, int N, int K,
                             int group, int fmt, hipStream_t stream) {

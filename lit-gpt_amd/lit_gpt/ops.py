@@ -36,6 +36,7 @@ SIGNATURES = {
     "lga_last_error_string": [],
     "lga_device_info": [_I, _P, _P, _I],
     "lga_quantize": [_P, _I, _P, _P, _I, _I, _I, _I, _P],
+    "lga_nf4_double_quant": [_P, _L, _P, _P, _P],
     "lga_q4_gemv": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemv_swiglu": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemv_attn": [_P, _I, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
@@ -139,6 +140,15 @@ def quantize(weight: torch.Tensor, fmt: int, group: int):
 
 
 # ------------------------------------------------------------------------------------------------ linear
+def nf4_double_quant(absmax: torch.Tensor, code: torch.Tensor) -> torch.Tensor:
+    """In place: nf4 absmax (fp32, contiguous) -> bitsandbytes' double-quantized statistic; returns the offset."""
+    off = torch.empty(1, dtype=torch.float32, device=absmax.device)
+    _check(load_library().lga_nf4_double_quant(_dev(absmax, "absmax", torch.float32), absmax.numel(),
+                                               _dev(code, "code", torch.float32), _dev(off, "offset", torch.float32),
+                                               _stream()))
+    return off
+
+
 def q4_gemv(x, qweight, scales, N, K, group, fmt, *, bias=None, residual=None, norm_weight=None, eps=1e-5,
             out=None, variant=-1):
     """y (N,) = x (K,) . dequant(W)^T  [+bias] [+residual]; optional fused RMSNorm of x (norm_weight)."""

@@ -11,7 +11,10 @@ still float) model for ``QuantLinear`` modules that quantize their weight on the
 Modes:
   "int4-g128" (also "int4-g64", "int4-g32")  symmetric int4, per-group bf16 scale (BASELINE config 3)
   "nf4"  / "bnb.nf4"                          NF4 codebook, fp32 absmax per 64 (bitsandbytes nf4 layout)
-  "bnb.nf4-dq"                                accepted; absmax kept fp32 (no double quantization)
+  "bnb.nf4-dq"                                nf4 + bitsandbytes double quantization of the absmax (offset =
+                                              mean, 8-bit dynamic-map codes per 256 blocks, fp32 absmax2): the
+                                              kernels scale by the dequantized statistic code[q]*absmax2+offset,
+                                              held expanded as fp32 per 64-block (lga_nf4_double_quant)
 Group sizes must divide in_features; for a TP row-shard whose width is not a multiple of the requested group
 (e.g. Llama-2-7B mlp.proj at TP=8: 1376) the largest of {128, 64, 32} that divides it is used.
 """
@@ -24,6 +27,25 @@ import torch
 import torch.nn as nn
 
 from lit_gpt import ops
+
+_DOUBLE_QUANT = {"bnb.nf4-dq"}
+_CODE_CACHE = {}
+
+
+def bnb_dynamic_map(device) -> torch.Tensor:
+    """bitsandbytes create_dynamic_map(signed=True, max_exponent_bits=7, total_bits=8): the 256 sorted fp32 codes
+    of the absmax double quantization (7 decades of 2^i linearly spaced means, +-, plus 0 and 1)."""
+    key = str(device)
+    if key not in _CODE_CACHE:
+        data = []
+        for i in range(7):
+            b = torch.linspace(0.1, 1, 2 ** i + 1)
+            means = ((b[:-1] + b[1:]) / 2.0) * (10 ** (-6 + i))
+            data += means.tolist() + (-means).tolist()
+        data += [0.0, 1.0]
+        _CODE_CACHE[key] = torch.tensor(sorted(data), dtype=torch.float32, device=device)
+    return _CODE_CACHE[key]
+
 
 _MODES = {
     "int4-g128": (ops.FMT_Q4G, 128),
@@ -84,6 +106,8 @@ class QuantLinear(nn.Module):
         qw, sc = ops.quantize(w, fmt, group)
         m.qweight.copy_(qw)
         m.scales.copy_(sc)
+        if mode in _DOUBLE_QUANT:
+            m.dq_offset = ops.nf4_double_quant(m.scales, bnb_dynamic_map(device))
         return m
 
     def forward(self, x: torch.Tensor, *, residual: Optional[torch.Tensor] = None,

@@ -106,3 +106,87 @@ def dequantize_nf4(packed: np.ndarray, absmax: np.ndarray, block: int = 64) -> n
     K = codes.shape[1]
     vals = NF4[codes].reshape(N, K // block, block)
     return (vals * absmax[..., None]).reshape(N, K).astype(np.float32)
+
+
+# ---- bitsandbytes double quantization of the nf4 absmax ("bnb.nf4-dq", compress_statistics=True) --------------
+# Restated from bitsandbytes 0.41.0 (requirements-all.txt:3; not vendored in /root/reference, not importable here —
+# parity unpinned): functional.quantize_4bit(compress_statistics=True) computes the per-64 absmax as nf4 does, then
+#   offset = absmax.mean(); qabsmax, state2 = quantize_blockwise(absmax - offset, blocksize=256)
+# with the signed 8-bit dynamic map (create_dynamic_map(signed=True, max_exponent_bits=7, total_bits=8)) and the
+# kQuantizeBlockwise nearest-code binary search (dQuantize<0>); dequantize_4bit uses
+#   absmax' = code[qabsmax] * absmax2[block] + offset      (fp32 multiply, then fp32 add)
+# The 4-bit codes themselves stay those computed from the exact absmax.
+
+def dynamic_map(max_exponent_bits: int = 7, total_bits: int = 8) -> np.ndarray:
+    """bitsandbytes create_dynamic_map(signed=True): 256 sorted float32 values in [-1, 1]."""
+    import torch
+
+    data = []
+    non_sign_bits = total_bits - 1
+    additional_items = 2 ** (non_sign_bits - max_exponent_bits) - 1
+    for i in range(max_exponent_bits):
+        fraction_items = int(2 ** (i + non_sign_bits - max_exponent_bits) + 1)
+        boundaries = torch.linspace(0.1, 1, fraction_items)
+        means = (boundaries[:-1] + boundaries[1:]) / 2.0
+        data += ((10 ** (-(max_exponent_bits - 1) + i)) * means).tolist()
+        data += (-(10 ** (-(max_exponent_bits - 1) + i)) * means).tolist()
+    if additional_items > 0:
+        boundaries = torch.linspace(0.1, 1, additional_items + 1)
+        means = (boundaries[:-1] + boundaries[1:]) / 2.0
+        data += ((10 ** (-(max_exponent_bits - 1) + i)) * means).tolist()
+        data += (-(10 ** (-(max_exponent_bits - 1) + i)) * means).tolist()
+    data.append(0)
+    data.append(1.0)
+    data += [0] * (256 - len(data))
+    data.sort()
+    return np.array(data, dtype=np.float32)
+
+
+def _dquantize(code: np.ndarray, x: np.float32) -> int:
+    """kQuantizeBlockwise's dQuantize<0>: binary search over the sorted code, nearest of the bracketing pair."""
+    pivot, upper_pivot, lower_pivot = 127, 255, 0
+    lower, upper = np.float32(-1.0), np.float32(1.0)
+    val = code[pivot]
+    i = 64
+    while i > 0:
+        if x > val:
+            lower_pivot, lower = pivot, val
+            pivot += i
+        else:
+            upper_pivot, upper = pivot, val
+            pivot -= i
+        val = code[pivot]
+        i >>= 1
+    if upper_pivot == 255:
+        upper = code[upper_pivot]
+    if lower_pivot == 0:
+        lower = code[lower_pivot]
+    if x > val:
+        mid = np.float32((upper + val) * np.float32(0.5))
+        return upper_pivot if x > mid else pivot
+    mid = np.float32((lower + val) * np.float32(0.5))
+    return lower_pivot if x < mid else pivot
+
+
+def double_quant_absmax(absmax: np.ndarray, block: int = 256):
+    """nf4 absmax (any shape, flattened row-major as bnb's blocks) -> (qabsmax uint8, absmax2 float32 per 256,
+    offset float32, absmax' float32 in the input shape: the dequantized statistic the GEMV / GEMM scale by).
+    The mean is accumulated in float64 (the product's kernel does the same; bnb uses torch's fp32 mean)."""
+    a = np.ascontiguousarray(absmax, dtype=np.float32).ravel()
+    code = dynamic_map()
+    offset = np.float32(a.astype(np.float64).sum() / a.size)
+    v = (a - offset).astype(np.float32)
+    n_blk = (a.size + block - 1) // block
+    q = np.zeros(a.size, dtype=np.uint8)
+    amax2 = np.zeros(n_blk, dtype=np.float32)
+    for b in range(n_blk):
+        blk = v[b * block:(b + 1) * block]
+        m = np.float32(np.abs(blk).max())
+        amax2[b] = m
+        inv = np.float32(1.0) / m if m > 0 else np.float32(0.0)
+        for j, x in enumerate(blk):
+            q[b * block + j] = _dquantize(code, np.float32(x * inv)) if m > 0 else int(np.argmin(np.abs(code)))
+    deq = (code[q] * np.repeat(amax2, block)[: a.size]).astype(np.float32)
+    out = (deq + offset).astype(np.float32)
+    return q, amax2, offset, out.reshape(np.shape(absmax))
+

@@ -39,6 +39,10 @@ FAMILIES = {
     "mixtral": ("Mixtral-8x7B-v0.1", dict(n_layer=2, n_embd=512, n_head=8, n_query_groups=4, intermediate_size=1024,
                                           n_expert=4, n_expert_per_token=2, padded_vocab_size=1024, vocab_size=1024,
                                           block_size=64)),
+    # GPT-NeoX (pythia): biased Linears (the row-parallel proj bias stays whole on every rank, generate/tp.py:43-45),
+    # LayerNorm, partial rotary (16 of 64 dims), parallel residual, GELU MLP
+    "neox": ("pythia-160m", dict(n_layer=2, n_embd=512, n_head=8, intermediate_size=1024, vocab_size=1000,
+                                 padded_vocab_size=1024, block_size=64)),
 }
 VARIANTS = [("fp32", torch.float32), ("fp32", torch.bfloat16), ("q4g", torch.bfloat16)]
 T, STEPS = 12, 8

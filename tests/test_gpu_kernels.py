@@ -68,6 +68,23 @@ def test_quantizer_bit_exact(ops, fmt, group, in_bf16):
 
 
 # ------------------------------------------------------------------------------------------------ GEMV
+@pytest.mark.parametrize("n", [1, 255, 256, 4096 * 64 // 64 * 3 + 17, 11008 * 4096 // 64])
+def test_nf4_double_quant_bit_exact(ops, n):
+    """lga_nf4_double_quant == oracle/quant.py double_quant_absmax (bitsandbytes compress_statistics restated):
+    every dequantized statistic bit-identical, the offset too."""
+    from lit_gpt.quantize import bnb_dynamic_map
+
+    rng = np.random.default_rng(n)
+    a = (np.abs(rng.standard_normal(n)) * 0.05 + 0.01).astype(np.float32)
+    if n >= 256:
+        a[:256] = np.float32(0.03)  # a block whose centred values are all equal (absmax2 can be tiny / zero)
+    dev = torch.from_numpy(a.copy()).to(DEV)
+    off = ops.nf4_double_quant(dev, bnb_dynamic_map(DEV))
+    q, amax2, offset, ref = quant.double_quant_absmax(a)
+    assert float(off.item()) == float(offset)
+    np.testing.assert_array_equal(dev.cpu().numpy(), ref)
+
+
 def _ref_linear(x, wdeq, bias=None):
     y = x.astype(np.float64) @ wdeq.astype(np.float64).T
     return y if bias is None else y + bias

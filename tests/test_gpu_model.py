@@ -61,7 +61,10 @@ def oracle_for(cfg, sd, mode, dtype=torch.bfloat16):
                 return vb
             if mode == "int4-g128":
                 return quant.dequantize_q4g(*quant.quantize_q4g(vb, 128), 128)
-            return quant.dequantize_nf4(*quant.quantize_nf4(vb, 64), 64)
+            packed, absmax = quant.quantize_nf4(vb, 64)
+            if mode == "bnb.nf4-dq":  # bitsandbytes double quantization of the statistics
+                absmax = quant.double_quant_absmax(absmax)[3]
+            return quant.dequantize_nf4(packed, absmax, 64)
         return v
 
     return om.OracleGPT(cfg, sd, dtype=dtype, weight_override=deq)
@@ -92,7 +95,7 @@ def _routing_ambiguous(margins, tol=2 ** -6):
 
 
 @pytest.mark.parametrize("key", list(CFGS))
-@pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bf16"])
+@pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bnb.nf4-dq", "bf16"])
 @torch.inference_mode()
 def test_teacher_forced_logits_match_oracle(key, mode):
     if mode == "bf16" and key == "moe":

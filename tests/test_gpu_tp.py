@@ -118,7 +118,8 @@ def test_tp2_mixtral_32k_context(tmp_path):
 
 @pytest.mark.timeout(300)
 @pytest.mark.parametrize("world", [2, 4])
-@pytest.mark.parametrize("fam,mode", [("llama", "bf16"), ("llama", "int4-g128"), ("mixtral", "int4-g128")])
+@pytest.mark.parametrize("fam,mode", [("llama", "bf16"), ("llama", "int4-g128"), ("mixtral", "int4-g128"),
+                                      ("neox", "bf16"), ("neox", "int4-g128")])
 def test_tp_matches_reference_tp_fixture(fam, world, mode, tmp_path):
     """The product's TP decode (generate/tp.py sharding, per-shard quantization, xGMI all-reduce) against the
     REFERENCE's own tensor_parallel run under gloo (tests/golden/g4_tp_logits.npz, made by

@@ -239,3 +239,20 @@ def test_decode_attention_split_heuristic_per_tp_rank():
     assert ops.decode_splits(1, 8, 128, 2304) == 16  # 70B TP=8: one KV group, 8 heads per group
     assert ops.decode_splits(4, 4, 128, 32768) == 16  # Mixtral TP=2 at 32k context
     assert ops.decode_splits(4, 1, 128, 64) == 4  # short caches: >= 16 keys per split
+
+
+def test_double_quant_code_table_is_bitsandbytes_dynamic_map():
+    """The product's 256-entry code for bnb.nf4-dq (lit_gpt/quantize.py) equals the oracle's restatement of
+    bitsandbytes create_dynamic_map(signed=True) bit for bit, and the mode parses as nf4 blocks of 64."""
+    import numpy as np
+
+    from lit_gpt import ops
+    from lit_gpt.quantize import bnb_dynamic_map, parse_mode
+    from oracle import quant
+
+    assert np.array_equal(bnb_dynamic_map("cpu").numpy(), quant.dynamic_map())
+    assert parse_mode("bnb.nf4-dq") == (ops.FMT_NF4, 64)
+    a = np.linspace(0.01, 0.2, 1000, dtype=np.float32)
+    q, amax2, off, out = quant.double_quant_absmax(a)
+    assert q.dtype == np.uint8 and amax2.shape == (4,) and np.abs(out - a).max() <= 0.01 * a.max()
+

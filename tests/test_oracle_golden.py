@@ -189,7 +189,7 @@ def test_synth_is_deterministic():
     assert not np.array_equal(a, synth.normal((1000,), "y", 1))
 
 
-@pytest.mark.parametrize("fam", ["llama", "mixtral"])
+@pytest.mark.parametrize("fam", ["llama", "mixtral", "neox"])
 @pytest.mark.parametrize("world", [2, 4])
 def test_reference_tp_logits_equal_unsharded_oracle(fam, world, golden):
     """G4: the reference's own tensor_parallel under gloo TP=2/4 (tests/golden/make_golden_tp.py)
