@@ -43,9 +43,17 @@ __device__ __forceinline__ float group_sum(float v) {
   return v;
 }
 
-// exact-order (no FMA contraction) helpers used where the reference's CPU math does mul then add
-__device__ __forceinline__ float mul_rn(float a, float b) { return __fmul_rn(a, b); }
-__device__ __forceinline__ float add_rn(float a, float b) { return __fadd_rn(a, b); }
+// exact-order (no FMA contraction) helpers used where the reference's CPU math does mul then add. HIP's
+// __fmul_rn / __fadd_rn are plain `a * b` / `a + b` (clang __clang_hip_math.h) and -ffp-contract may fuse them;
+// the pragma drops the `contract` flag from these ops, which survives inlining.
+__device__ __forceinline__ float mul_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a * b;
+}
+__device__ __forceinline__ float add_rn(float a, float b) {
+#pragma clang fp contract(off)
+  return a + b;
+}
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
 

@@ -133,7 +133,13 @@ __global__ void __launch_bounds__(256) double_quant_kernel(float* __restrict__ a
     for (int j = 1; j < 256; ++j)
       if (fabsf(code[j]) < fabsf(code[q])) q = j;
   }
-  a[i] = __fadd_rn(__fmul_rn(code[q], amax2), offset);
+  {
+    // two roundings, as bitsandbytes (kDequantizeBlockwise multiplies, then `absmax += offset` is a separate op):
+    // HIP's __fmul_rn / __fadd_rn alone do not stop -ffp-contract from fusing them into one fma
+#pragma clang fp contract(off)
+    const float deq = code[q] * amax2;
+    a[i] = deq + offset;
+  }
 }
 
 }  // namespace lga
