@@ -11,7 +11,9 @@
 // W is dequantised while it is staged, to bf16(value(nibble) * scale) — the rounding the reference's path applies
 // (bitsandbytes dequantize_4bit to the bf16 weight, then the GEMM), and exactly the bf16 weights the CPU oracle
 // multiplies: int4-g value = nibble - 8 with the bf16 group scale, nf4 value = NF4[nibble] with the fp32 absmax.
-// (An exact-integer-B variant with per-group fp32 partial sums needed 324 VGPRs and ran at half the speed.)
+// (An exact-integer-B variant with per-group fp32 partial sums needed 324 VGPRs and ran at half the speed; a
+// three-stage form — X two K-steps ahead in a ring of 3 LDS tiles, packed W one step ahead in registers, 80 KB LDS —
+// ran at 533 vs 644 TFLOP/s per int4 layer, tools/gemm_sweep.py round 2: the two-stage loop is not latency-bound.)
 #include "common.h"
 
 namespace lga {
