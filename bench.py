@@ -78,7 +78,52 @@ def prefill_flops(cfg, T: int, tp: int = 1) -> float:
     return L * (2.0 * T * per_tok + attn) + 2.0 * cfg.padded_vocab_size * C
 
 
-DOMINANT = "gemv_q4_kernel<.., DUAL> (RMSNorm + fc_1/fc_2 int4 GEMV + SwiGLU of one block)"
+DOMINANT = ("gemv_q4s_kernel<.., DUAL> (streaming form: RMSNorm + fc_1/fc_2 int4 GEMV + SwiGLU of one block; the "
+            "largest per-step kernel)")
+
+
+def time_attention(model, pos: int, replays: int = 5):
+    """Average launch duration of the decode attention (RoPE + KV append + split attention, one launch per block)
+    over the blocks' own KV caches at position ``pos`` — the second-largest per-step kernel — with HIP events on
+    the launch stream (32 launches captured back to back in a HIP graph). Returns (ms, algorithmic bytes per
+    launch): K and V rows 0..pos of every query group + the qkv row in + the attention row out."""
+    from lit_gpt import ops
+
+    blocks = model.transformer.h
+    c = blocks[0].attn.config  # this rank's heads under tensor parallelism
+    H, G, hs = c.n_head, c.n_query_groups, c.head_size
+    if not ops.decode_fusable(hs, c.rope_n_elem) or blocks[0].attn.kv_cache is None:
+        return None, None
+    cos, sin = model._rope_tables()
+    qkv = torch.randn(1, (H + 2 * G) * hs, device="cuda").to(torch.bfloat16)
+    p = torch.tensor([pos], device="cuda")
+    S = blocks[0].attn.kv_cache.k.size(-2)
+    splits = ops.decode_splits(G, H // G, hs, S)
+    ws = ops.AttentionWorkspace(1, H, G, hs, splits, torch.device("cuda", torch.cuda.current_device()))
+    out = torch.empty(1, H * hs, device="cuda", dtype=torch.bfloat16)
+
+    def launch_all():
+        for blk in blocks:
+            kv = blk.attn.kv_cache
+            ops.attention_decode_fused(qkv, kv.k, kv.v, p, p, cos, sin, H, G, hs, c.rope_n_elem, 1.0 / math.sqrt(hs),
+                                       splits, workspace=ws, out=out)
+
+    launch_all()
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        launch_all()
+    graph.replay()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record(stream)
+    for _ in range(replays):
+        graph.replay()
+    e.record(stream)
+    e.synchronize()
+    nbytes = 2 * G * hs * 2 * (pos + 1) + (H + 2 * G) * hs * 2 + H * hs * 2
+    return s.elapsed_time(e) / (replays * len(blocks)), nbytes
 
 
 def _dual_gemv_bytes(f1, C: int) -> int:
@@ -141,8 +186,9 @@ def time_dominant_kernel(model, replays: int = 5):
 
 
 def pmc_child() -> None:
-    """Run under `rocprofv3 --pmc FETCH_SIZE` by measure_traffic(): the dominant kernel at Llama-2-7B shape over
-    24 distinct weight sets (1.1 GB, beyond the 256 MB Infinity Cache), one launch each."""
+    """Run under `rocprofv3 --pmc FETCH_SIZE` by measure_traffic(): the fc_1||fc_2 GEMV at Llama-2-7B shape over
+    24 distinct weight sets (1.1 GB, beyond the 256 MB Infinity Cache), one launch each, then the decode attention
+    over 24 distinct K/V caches."""
     from lit_gpt import ops
 
     C, N, copies = 4096, 11008, 24
@@ -159,13 +205,28 @@ def pmc_child() -> None:
     for q1, s1, q2, s2 in sets:
         ops.q4_gemv_swiglu(x, q1, s1, q2, s2, N, C, 128, 0, norm_weight=nw, out=out)
     torch.cuda.synchronize()
+    del sets
+    # the decode attention over 24 distinct layers' K/V caches at the bench's last position (0.9 GB)
+    H = G = 32
+    hs, S = 128, PROMPT_LEN + 256
+    pos = torch.tensor([PROMPT_LEN + 254], device=dev)
+    cos, sin = torch.ones(S, hs, device=dev), torch.zeros(S, hs, device=dev)
+    qkv = torch.randn(1, (H + 2 * G) * hs, device=dev).to(torch.bfloat16)
+    splits = ops.decode_splits(G, H // G, hs, S)
+    ws = ops.AttentionWorkspace(1, H, G, hs, splits, dev)
+    caches = [(torch.randn(G, S, hs, device=dev).to(torch.bfloat16), torch.randn(G, S, hs, device=dev).to(torch.bfloat16))
+              for _ in range(copies)]
+    torch.cuda.synchronize()
+    for kc, vc in caches:
+        ops.attention_decode_fused(qkv, kc, vc, pos, pos, cos, sin, H, G, hs, hs, hs ** -0.5, splits, workspace=ws)
+    torch.cuda.synchronize()
 
 
 def measure_traffic(timeout_s: float = 240.0):
     """HBM bytes per launch of the dominant kernel from the PMC counters, collected as MI355X_MICROARCH.md's HBM
     section prescribes: FETCH_SIZE (KiB, TCC_EA0_RDREQ x 64 B) in its own rocprofv3 pass, doubled (gfx950 tallies
     128-B requests of a 16-B/lane streaming read at 64 B). Runs in a child process started BEFORE this process
-    touches the GPU. Returns (bytes per launch or None, note)."""
+    touches the GPU. Returns {"gemv" | "attention": (bytes per launch or None, note)}."""
     import csv
     import shutil
     import statistics
@@ -181,14 +242,18 @@ def measure_traffic(timeout_s: float = 240.0):
     try:
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=timeout_s, check=True)
         files = list(out.rglob("*counter_collection.csv"))
-        vals = [float(r["Counter_Value"]) for f in files for r in csv.DictReader(open(f))
-                if "gemv_q4_kernel" in r.get("Kernel_Name", "") and r.get("Counter_Name") == "FETCH_SIZE"]
-        if not vals:
-            return None, "no FETCH_SIZE rows for the dominant kernel"
-        kib = statistics.median(vals)
-        return 2.0 * kib * 1024.0, f"median FETCH_SIZE {kib:.0f} KiB over {len(vals)} launches, x2 (gfx950)"
+        rows = [r for f in files for r in csv.DictReader(open(f)) if r.get("Counter_Name") == "FETCH_SIZE"]
+        res = {}
+        for key, pat in (("gemv", "gemv_q4"), ("attention", "attn_kernel")):
+            vals = [float(r["Counter_Value"]) for r in rows if pat in r.get("Kernel_Name", "")]
+            if not vals:
+                res[key] = (None, f"no FETCH_SIZE rows for {pat}")
+                continue
+            kib = statistics.median(vals)
+            res[key] = (2.0 * kib * 1024.0, f"median FETCH_SIZE {kib:.0f} KiB over {len(vals)} launches, x2 (gfx950)")
+        return res
     except Exception as e:  # traffic is diagnostic; never lose the bench line over it
-        return None, f"pmc pass failed: {type(e).__name__}"
+        return {k: (None, f"pmc pass failed: {type(e).__name__}") for k in ("gemv", "attention")}
     finally:
         shutil.rmtree(out, ignore_errors=True)
 
@@ -264,12 +329,12 @@ def main():
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child()
-    traffic, traffic_note = None, "skipped"
+    traffic = {k: (None, "skipped") for k in ("gemv", "attention")}
     under_profiler = any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
     headline = args.model == MODEL and args.quantize == "int4-g128"
     dense = args.quantize in ("bf16", "none")
     if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_traffic and not under_profiler and headline:
-        traffic, traffic_note = measure_traffic()  # before this process initialises the GPU
+        traffic = measure_traffic()  # before this process initialises the GPU
 
     import torch.distributed as dist
 
@@ -354,6 +419,7 @@ def main():
         tok_s = args.steps / elapsed
         ms_step = elapsed / args.steps * 1e3
         avg_ms, kbytes = time_dominant_kernel(model)
+        att_ms, att_bytes = time_attention(model, T + args.warmup + args.steps)
 
     cfg_full = Config.from_name(args.model)
     mean_pos = T + args.warmup + 1 + (args.steps - 1) / 2
@@ -385,9 +451,16 @@ def main():
                      "gemv_q4_kernel<.., DUAL> routed (RMSNorm + fc_1/fc_2 of 2 experts + SwiGLU of one block)"),
                      "achieved": round(kern_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(kern_gbs / HBM_PEAK_GBS, 4),
-                     "traffic": None if traffic is None else int(traffic),
-                     "traffic_note": traffic_note,
+                     "traffic": None if traffic["gemv"][0] is None else int(traffic["gemv"][0]),
+                     "traffic_note": traffic["gemv"][1],
                      "bytes_per_launch": int(kbytes), "avg_launch_us": round(avg_ms * 1e3, 2)},
+        "roofline_attention": None if att_ms is None else {
+            "bound": "hbm", "kernel": "attn_kernel<..,FUSED> (RoPE + KV append + split decode attention of one block)",
+            "achieved": round(att_bytes / (att_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(att_bytes / (att_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": int(att_bytes),
+            "traffic": None if traffic["attention"][0] is None else int(traffic["attention"][0]),
+            "traffic_note": traffic["attention"][1], "avg_launch_us": round(att_ms * 1e3, 2),
+            "position": T + args.warmup + args.steps},
         "step_roofline": {"bytes_per_token": int(step_bytes), "achieved": round(step_gbs, 1),
                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(step_gbs / HBM_PEAK_GBS, 4),
                           "roofline_tokens_per_s": round(HBM_PEAK_GBS * 1e9 / step_bytes, 1)},
