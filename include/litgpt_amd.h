@@ -68,6 +68,16 @@ int lga_q4_gemv_attn(const float* partials, int n_splits, int head_size, const u
 /* -- prefill GEMM, M > 1 (bnb dequantize_4bit + cuBLAS GEMM) -------------------------------------------- */
 int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const void* bias, const void* residual,
                 void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
+/* bnb dequantize_4bit (the first half of the reference's M > 1 Linear4bit path): w (N, K) bf16 =
+ * bf16(value(nibble) * scale) — the same bits lga_q4_gemm stages, so lga_bf16_gemm over w == lga_q4_gemm.
+ * QuantLinear uses it for long prefills (M >= 512), where the bf16 GEMM's rate pays for the extra pass. */
+int lga_q4_dequantize(const uint8_t* qweight, const void* scales, void* w, int N, int K, int group, int fmt,
+                      lga_stream_t stream);
+/* Long-prefill bf16 GEMM (the cuBLAS GEMM behind F.linear / after dequantize_4bit) on hipBLASLt: y (M, N) =
+ * x (M, K) . W (N, K)^T [+bias] [+residual, added after the bf16 rounding of the product]. N, K multiples of 8;
+ * `workspace` (may be NULL) of `workspace_bytes` is caller-owned scratch for split-K algorithms. */
+int lga_gemm_bf16_blaslt(const void* x, const void* weight, const void* bias, const void* residual, void* y, int M,
+                         int N, int K, void* workspace, size_t workspace_bytes, lga_stream_t stream);
 
 /* -- unquantized bf16 Linears (BASELINE config 2: no --quantize, precision bf16-true; the reference runs
  *    F.linear on the bf16 nn.Linear weight, lit_gpt/model.py:619, :656, :712-716, :519) ------------------- */

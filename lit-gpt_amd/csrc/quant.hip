@@ -142,7 +142,44 @@ __global__ void __launch_bounds__(256) double_quant_kernel(float* __restrict__ a
   }
 }
 
+// Dequantise packed 4-bit rows to bf16: w[n][k] = bf16(value(nibble) * scale), value = nibble - 8 (int4-g, bf16
+// group scale) or NF4[nibble] (nf4, fp32 block absmax) — bit for bit the B tiles gemm_q4_kernel stages, so a bf16
+// GEMM over the result equals lga_q4_gemm. One thread: 8 weights (4 B in, 16 B out), so every wave instruction
+// reads 256 and writes 1024 contiguous bytes.
+template <int FMT>
+__global__ void __launch_bounds__(256) dequant_kernel(const uint32_t* __restrict__ qw, const void* __restrict__ sc,
+                                                       uint4* __restrict__ w, long words, int K, int group) {
+  const long c = (long)blockIdx.x * 256 + threadIdx.x;
+  if (c >= words) return;
+  const long n = c / (K / 8), k0 = (c % (K / 8)) * 8;
+  const uint32_t q = __builtin_nontemporal_load(qw + c);
+  const size_t si = (size_t)n * (K / group) + k0 / group;
+  const float s = FMT == 0 ? bf2f(((const uint16_t*)sc)[si]) : ((const float*)sc)[si];
+  uint32_t o[4];
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const uint32_t lo = (q >> (4 * e)) & 0xF, hi = (q >> (4 * e + 4)) & 0xF;
+    const float vl = FMT == 0 ? (float)((int)lo - 8) : kNF4[lo], vh = FMT == 0 ? (float)((int)hi - 8) : kNF4[hi];
+    o[e / 2] = pack2(mul_rn(vl, s), mul_rn(vh, s));
+  }
+  w[c] = make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 }  // namespace lga
+
+extern "C" int lga_q4_dequantize(const uint8_t* qweight, const void* scales, void* w, int N, int K, int group,
+                                 int fmt, hipStream_t stream) {
+  LGA_CHECK_ARG(qweight && scales && w, "lga_q4_dequantize: null pointer");
+  LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0 && group >= 32 && group % 32 == 0 && K % group == 0,
+                "lga_q4_dequantize: K must be a positive multiple of 32 and of the group (a multiple of 32)");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_dequantize: fmt must be 0 (int4-g) or 1 (nf4)");
+  LGA_CHECK_ARG(((uintptr_t)qweight | (uintptr_t)w) % 16 == 0, "lga_q4_dequantize: 16-B aligned buffers required");
+  const long words = (long)N * (K / 8);
+  const dim3 grid((unsigned)((words + 255) / 256));
+  if (fmt == 0) lga::dequant_kernel<0><<<grid, 256, 0, stream>>>((const uint32_t*)qweight, scales, (uint4*)w, words, K, group);
+  else lga::dequant_kernel<1><<<grid, 256, 0, stream>>>((const uint32_t*)qweight, scales, (uint4*)w, words, K, group);
+  LGA_LAUNCH_RETURN();
+}
 
 extern "C" int lga_nf4_double_quant(float* absmax, long n, const float* code, float* offset_out,
                                     hipStream_t stream) {

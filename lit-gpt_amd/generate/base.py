@@ -181,6 +181,10 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
     finally:
         torch.set_default_dtype(prev)
     model.set_kv_cache(batch_size=1, device=device)
+    # the prefill's library GEMM (hipBLASLt) loads its kernels on first use: do it here, at load, not in the prompt
+    from lit_gpt import ops
+
+    ops.warm_gemm_library(device, K=config.n_embd)
     return model.eval()
 
 

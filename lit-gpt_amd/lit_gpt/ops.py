@@ -29,6 +29,7 @@ _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_long
 _F = ctypes.c_float
+_SZ = ctypes.c_size_t
 
 # symbol -> argtypes; the exported surface of include/litgpt_amd.h (tests check the .so exports each one)
 SIGNATURES = {
@@ -41,10 +42,12 @@ SIGNATURES = {
     "lga_q4_gemv_swiglu": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemv_attn": [_P, _I, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemm": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lga_q4_dequantize": [_P, _P, _P, _I, _I, _I, _I, _P],
     "lga_bf16_gemv": [_P, _P, _P, _P, _P, _F, _P, _I, _I, _P],
     "lga_bf16_gemv_swiglu": [_P, _P, _P, _P, _F, _P, _I, _I, _P],
     "lga_bf16_gemv_attn": [_P, _I, _I, _P, _P, _P, _P, _I, _I, _P],
     "lga_bf16_gemm": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lga_gemm_bf16_blaslt": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P],
     "lga_rmsnorm": [_P, _P, _P, _I, _I, _F, _P],
     "lga_rope_kv_append": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lga_embedding": [_P, _I, _P, _P, _I, _I, _I, _P],
@@ -195,6 +198,16 @@ def q4_gemm(x, qweight, scales, N, K, group, fmt, *, bias=None, residual=None, o
     return y
 
 
+def q4_dequantize(qweight, scales, N, K, group, fmt, *, out=None):
+    """W (N, K) bf16 = bf16(value(nibble) * scale): the bits lga_q4_gemm stages (bnb dequantize_4bit)."""
+    w = out if out is not None else torch.empty(N, K, dtype=torch.bfloat16, device=qweight.device)
+    if w.numel() < N * K:
+        raise ValueError(f"q4_dequantize: out holds {w.numel()} elements, needs {N * K}")
+    _check(load_library().lga_q4_dequantize(_dev(qweight, "qweight", torch.uint8), _dev(scales, "scales"),
+                                            _dev(w, "w", torch.bfloat16), N, K, group, fmt, _stream()))
+    return w[: N * K].view(N, K) if w.dim() == 1 else w
+
+
 def bf16_gemv(x, weight, *, bias=None, residual=None, norm_weight=None, eps=1e-5, out=None):
     """y (N,) = x (K,) . W (N, K)^T [+bias] [+residual] with bf16 weights; optional fused RMSNorm of x."""
     N, K = weight.shape
@@ -231,11 +244,38 @@ def bf16_gemv_attn(partials, n_splits, head_size, weight, *, bias=None, residual
     return y
 
 
-def bf16_gemm(x, weight, *, bias=None, residual=None, out=None):
-    """Y (M, N) = X (M, K) . W (N, K)^T [+bias] [+residual] with bf16 weights, MFMA tiles."""
+LIB_GEMM_MIN_M = 16  # rows from which the hipBLASLt bf16 GEMM replaces gemm.hip's tiles (tools/gemm_rates.py)
+LIB_GEMM_WORKSPACE = 32 << 20
+_GEMM_WS: dict = {}
+
+
+def warm_gemm_library(device, K: int = 4096) -> None:
+    """Load hipBLASLt and its gfx950 kernels before the first prefill (one small GEMM), so the first prompt does
+    not pay the library's start-up."""
+    x = torch.zeros(LIB_GEMM_MIN_M, K, dtype=torch.bfloat16, device=device)
+    bf16_gemm(x, torch.zeros(64, K, dtype=torch.bfloat16, device=device), impl="blaslt")
+
+
+def bf16_gemm(x, weight, *, bias=None, residual=None, out=None, impl=None):
+    """Y (M, N) = X (M, K) . W (N, K)^T [+bias] [+residual] with bf16 weights. impl "mfma" = gemm.hip's MFMA tiles
+    (bias and residual fused in its epilogue), "blaslt" = hipBLASLt (bias epilogue; residual added after the
+    product's bf16 rounding, as the reference Block adds it); default: hipBLASLt from LIB_GEMM_MIN_M rows."""
     M = x.shape[0]
     N, K = weight.shape
     y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    if impl is None:
+        impl = "blaslt" if M >= LIB_GEMM_MIN_M and N % 8 == 0 and K % 8 == 0 else "mfma"
+    if impl == "blaslt":
+        ws = _GEMM_WS.get(x.device)
+        if ws is None:
+            ws = _GEMM_WS[x.device] = torch.empty(LIB_GEMM_WORKSPACE, dtype=torch.uint8, device=x.device)
+        _check(load_library().lga_gemm_bf16_blaslt(
+            _dev(x, "x", torch.bfloat16), _dev(weight, "weight", torch.bfloat16), _opt(bias, "bias", torch.bfloat16),
+            _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16), M, N, K,
+            _dev(ws, "workspace", torch.uint8), ws.numel(), _stream()))
+        return y
+    if impl != "mfma":
+        raise ValueError(f"bf16_gemm: unknown impl {impl!r}")
     _check(load_library().lga_bf16_gemm(_dev(x, "x", torch.bfloat16), _dev(weight, "weight", torch.bfloat16),
                                         _opt(bias, "bias", torch.bfloat16), _opt(residual, "residual", torch.bfloat16),
                                         _dev(y, "y", torch.bfloat16), M, N, K, _stream()))

@@ -72,6 +72,21 @@ def _fit_group(K: int, group: int) -> int:
     raise ValueError(f"in_features={K} is not a multiple of 32; no 4-bit group layout fits")
 
 
+# prefill rows from which dequantize + the library bf16 GEMM beats the fused int4 GEMM (tools/gemm_rates.py, Llama-2-7B
+# layer: 0.21 vs 0.44 ms at M = 64, 0.63 vs 1.04 ms at M = 2048; gemm.hip's 128-row tiles idle most CUs below M = 256)
+DEQUANT_GEMM_MIN_M = 16
+_SCRATCH: dict = {}
+
+
+def _dequant_scratch(numel: int, device: torch.device) -> torch.Tensor:
+    """One growing bf16 buffer per device for dequantized weights: the Linears of a forward run one after
+    another on the device's stream, so one buffer serves them all."""
+    buf = _SCRATCH.get(device)
+    if buf is None or buf.numel() < numel:
+        buf = _SCRATCH[device] = torch.empty(numel, dtype=torch.bfloat16, device=device)
+    return buf
+
+
 class QuantLinear(nn.Module):
     """Packed 4-bit weight ``qweight`` (N, K/2) uint8 + ``scales`` (N, K/group) on the GPU.
 
@@ -128,8 +143,16 @@ class QuantLinear(nn.Module):
         else:
             if norm_weight is not None:
                 x2 = ops.rmsnorm(x2, norm_weight, norm_eps)
-            y = ops.q4_gemm(x2, self.qweight, self.scales, self.out_features, self.in_features, self.group, self.fmt,
-                            bias=self.bias, residual=res)
+            if M >= DEQUANT_GEMM_MIN_M:
+                # long prefill: dequantize to bf16 once (bnb's dequantize_4bit, the reference's own M > 1 path),
+                # then the library bf16 GEMM (hipBLASLt): 1.1-1.25 PFLOP/s vs 0.5-0.7 for the fused int4 GEMM at
+                # M = 2048, the dequantize pass included (tools/gemm_rates.py)
+                w = ops.q4_dequantize(self.qweight, self.scales, self.out_features, self.in_features, self.group,
+                                      self.fmt, out=_dequant_scratch(self.out_features * self.in_features, x2.device))
+                y = ops.bf16_gemm(x2, w, bias=self.bias, residual=res)
+            else:
+                y = ops.q4_gemm(x2, self.qweight, self.scales, self.out_features, self.in_features, self.group,
+                                self.fmt, bias=self.bias, residual=res)
         return y.view(*lead, self.out_features)
 
     def forward_attn(self, partials: torch.Tensor, n_splits: int, head_size: int, *,

@@ -169,6 +169,35 @@ def test_gemm_matches_reference(ops, fmt, group, M, N, K):
     assert np.max(err) <= 2e-3, float(np.max(err))
 
 
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (0, 32)])
+@pytest.mark.parametrize("M,N,K", [(512, 768, 256), (600, 1024, 4096), (2048, 640, 1376), (517, 4096, 11008)])
+def test_dequantize_then_bf16_gemm_is_q4_gemm(ops, fmt, group, M, N, K):
+    """lga_q4_dequantize == the oracle's bf16(dequantize) bit for bit; gemm.hip's bf16 GEMM over it == lga_q4_gemm
+    bit for bit (the same bf16 B tiles, the same MFMA order); QuantLinear's long-prefill path (dequantize +
+    hipBLASLt) within bf16 rounding of the fp64 product."""
+    if K % group:
+        group = 32
+    w = _weights(N, K, f"dq{N}x{K}")
+    qw, sc = ops.quantize(torch.from_numpy(w).to(DEV), fmt, group)
+    wd = ops.q4_dequantize(qw, sc, N, K, group, fmt)
+    np.testing.assert_array_equal(wd.float().cpu().numpy(), bf16_np(_deq(ops, w, fmt, group)))
+    xn = bf16_np(synth.normal((M, K), f"dqx{M}x{K}", 5, 1.0))
+    resn = bf16_np(synth.normal((M, N), "dqres", 5, 1.0))
+    x, res = to_dev_bf16(xn), to_dev_bf16(resn)
+    ref = ops.q4_gemm(x, qw, sc, N, K, group, fmt, residual=res)
+    assert torch.equal(ops.bf16_gemm(x, wd, residual=res, impl="mfma"), ref)
+    from lit_gpt.quantize import DEQUANT_GEMM_MIN_M, QuantLinear
+
+    lin = QuantLinear(K, N, fmt, group, device=DEV)
+    lin.qweight.copy_(qw)
+    lin.scales.copy_(sc)
+    assert M >= DEQUANT_GEMM_MIN_M
+    y = lin(x, residual=res).float().cpu().numpy()  # dequantize + hipBLASLt: vs the fp64 product
+    h = _ref_linear(xn, bf16_np(_deq(ops, w, fmt, group)))
+    exp = bf16_np(h.astype(np.float32)) + resn
+    assert np.max(np.abs(y - exp) - (np.abs(exp) + np.abs(h)) * 2 ** -7) <= 2e-3
+
+
 # ------------------------------------------------------------------------------------------------ bf16 weights
 # BASELINE config 2: unquantized nn.Linear in bf16-true. Reference: fp64 product of the same bf16 x and W.
 @pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 11008), (32000, 4096), (1000, 256), (77, 1376), (40, 8),
@@ -213,14 +242,17 @@ def test_bf16_gemv_swiglu(ops, N, K):
 
 
 @pytest.mark.parametrize("M,N,K", [(200, 768, 256), (2048, 1024, 4096), (5, 640, 1376), (130, 4096, 11008),
-                                   (64, 96, 32)])
-def test_bf16_gemm_matches_reference(ops, M, N, K):
+                                   (64, 96, 32), (300, 1000, 1376), (2048, 12288, 4096)])
+@pytest.mark.parametrize("impl", ["mfma", "blaslt"])
+def test_bf16_gemm_matches_reference(ops, M, N, K, impl):
+    """Both bf16 GEMMs (gemm.hip MFMA tiles; hipBLASLt for long prefills) vs an fp64 product of the same bf16
+    operands, bias in the product, residual added after the bf16 rounding (Block's `proj(y) + h`)."""
     w = bf16_np(_weights(N, K, f"bgm{N}x{K}"))
     x = bf16_np(synth.normal((M, K), f"bgx{M}x{K}", 5, 1.0))
     res = bf16_np(synth.normal((M, N), "bgres", 5, 1.0))
     bias = bf16_np(synth.normal((N,), "bgbias", 5, 0.1))
-    y = ops.bf16_gemm(to_dev_bf16(x), to_dev_bf16(w), bias=to_dev_bf16(bias), residual=to_dev_bf16(res)
-                      ).float().cpu().numpy()
+    y = ops.bf16_gemm(to_dev_bf16(x), to_dev_bf16(w), bias=to_dev_bf16(bias), residual=to_dev_bf16(res),
+                      impl=impl).float().cpu().numpy()
     h = _ref_linear(x, w) + bias
     ref = bf16_np(h.astype(np.float32)) + res
     err = np.abs(y - ref) - (np.abs(ref) + np.abs(h)) * 2 ** -7

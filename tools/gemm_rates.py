@@ -1,0 +1,50 @@
+"""Lab: prefill GEMM rates at Llama-2-7B layer shapes (M = 2048 prompt rows) — the product's int4 GEMM, its
+dequantize pass + bf16 GEMM (gemm.hip's MFMA tiles, and lga_gemm_bf16_blaslt), and torch.matmul on the same bf16
+operands for comparison.
+
+usage: python tools/gemm_rates.py [M]
+"""
+import sys
+from pathlib import Path
+
+import torch
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(REPO / "lit-gpt_amd"), str(REPO)]
+from lit_gpt import ops  # noqa: E402
+
+M = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+dev = torch.device("cuda")
+SHAPES = {"qkv": (12288, 4096), "proj": (4096, 4096), "fc": (11008, 4096), "down": (4096, 11008)}
+
+
+def timed(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps * 1e3  # us
+
+
+tot = {}
+for name, (N, K) in SHAPES.items():
+    w = torch.randn(N, K, device=dev) * 0.02
+    qw, sc = ops.quantize(w, 0, 128)
+    wb = ops.q4_dequantize(qw, sc, N, K, 128, 0)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    fl = 2.0 * M * N * K
+    r = {"q4_gemm": timed(lambda: ops.q4_gemm(x, qw, sc, N, K, 128, 0)),
+         "dequant": timed(lambda: ops.q4_dequantize(qw, sc, N, K, 128, 0, out=wb)),
+         "bf16_gemm": timed(lambda: ops.bf16_gemm(x, wb, impl="mfma")),
+         "blaslt": timed(lambda: ops.bf16_gemm(x, wb, impl="blaslt")),
+         "torch_mm": timed(lambda: torch.matmul(x, wb.t()))}
+    for k, v in r.items():
+        tot[k] = tot.get(k, 0.0) + v
+    print(f"{name:5s} N={N:6d} K={K:6d}  " + "  ".join(
+        f"{k} {v:8.1f} us" + (f" ({fl / v / 1e6:6.1f} TF/s)" if k != "dequant" else
+                              f" ({(N * K * 2.5) / v / 1e3:6.1f} GB/s)") for k, v in r.items()), flush=True)
+print("per layer: " + "  ".join(f"{k} {v:8.1f} us" for k, v in tot.items()) + "  (fc counted once; x2 in a layer)")
