@@ -444,7 +444,9 @@ def main():
                    "weights": args.quantize, "prompt_len": T, "decode_positions": [T + args.warmup + 1,
                                                                                    T + args.warmup + args.steps],
                    "global_batch": 1, "seq_len": T, "parallelism": f"tp{world}",
-                   "graph": use_graph, **({"graph_note": graph_note} if graph_note else {})},
+                   "graph": use_graph, **({"graph_note": graph_note} if graph_note else {}),
+                   **({"allreduce": "xgmi one-shot" if gtp.comm.get_default() is not None else
+                       f"rccl ({gtp.comm.fallback_reason or 'LGA_TP_ALLREDUCE=rccl'})"} if world > 1 else {})},
         "roofline": {"bound": "hbm", "kernel": (
                      "gemv_bf16_kernel<.., DUAL> (RMSNorm + fc_1/fc_2 bf16 GEMV + SwiGLU of one block)" if dense else
                      DOMINANT if not cfg._mlp_class == "LLaMAMoE" else

@@ -303,207 +303,214 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
   LGA_TRACE(6);
 }
 
-// ---------------------------------------------------------------------------------------------------------------
-// Prefill (T > 1): flash attention on MFMA (v_mfma_f32_16x16x32_bf16). A workgroup = 4 waves = 64 query rows of one
-// head; each wave owns 16 rows. Key tiles of 32 rows stream through LDS: K as stored ([key][hs], XOR-swizzled 16-B
-// chunks) is the B operand of S = Q.K^T directly; V is staged transposed ([hs][key]) so it is the B operand of
-// O += P.V; P goes through a per-wave LDS tile to change from the accumulator layout (lane = key column) to the A
-// operand layout (lane = query row). Online softmax in fp32 per query row (16-lane shuffles). Query t sees keys
-// <= input_pos[t] (the reference's mask rows, lit_gpt/model.py:509,651); the key loop stops at the block's
-// largest position.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ int swz64(int row, int chunk) { return row * 64 + 16 * (chunk ^ ((row >> 2) & 3)); }
-__device__ __forceinline__ int swz256(int row, int chunk) { return row * 256 + 16 * (chunk ^ (row & 15)); }
+// ---------------------------------------------------------------------------------------------------------------
+// Prefill (T >= 16): flash attention on MFMA, swapped form. A workgroup = 4 waves x 32 query rows of one head;
+// key tiles of 64 rows stream through a double-buffered LDS image (register-staged: the next tile's global loads are issued
+// before this tile's MFMAs and written after them). Per 32-key half-tile, S^T = K . Q^T on v_mfma_f32_32x32x16_bf16
+// (A = K rows from LDS, B = this wave's Q^T held in registers), so lane l holds the scores of ONE query (l % 32)
+// for 16 keys and its partner lane l ^ 32 the other 16: the online-softmax max / sum are in-lane chains plus one
+// exchange. P goes to bf16 in registers and two v_permlane32_swap per 16 keys regroup it into the B operand of
+// O^T += V^T . P^T, whose A operand comes straight from the row-major V image by ds_read_b64_tr_b16 (transposed
+// LDS read) — no P or V^T round trip through LDS. O^T's lane also owns one query, so the rescale by
+// exp(m_old - m_new) is a per-lane scalar, skipped when no row max of the wave moved. Causal masking only on the
+// tiles that cross a row's position; query blocks are dispatched heaviest first. Llama-2-7B, T = 2048: 102 us per
+// layer = 336 TFLOP/s (tools/prefill_attn_bench.py), was 295 us with 16-row query blocks on 16x16x32 MFMAs.
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef short i16x8_t __attribute__((ext_vector_type(8)));
 
-#ifndef LGA_PREFILL_MB
-#define LGA_PREFILL_MB 1  // 2 (128 rows per workgroup, K/V fragments shared) measured 365 vs 297 us: 212 VGPRs, 1 wave/SIMD
-#endif
-template <int HS, int MB>
-__global__ void __launch_bounds__(256) attn_prefill_kernel(const uint16_t* __restrict__ q,
-                                                           const uint16_t* __restrict__ kc,
-                                                           const uint16_t* __restrict__ vc,
-                                                           const int64_t* __restrict__ input_pos,
-                                                           uint16_t* __restrict__ y, int T, int n_head, int G,
-                                                           int max_seq, float scale) {
-  constexpr int KB = 32;          // keys per tile
-  constexpr int KS = HS / 32;     // MFMA k-steps over the head dim
-  constexpr int NT = HS / 16;     // output column tiles
-  __shared__ __attribute__((aligned(16))) unsigned char k_lds[KB * HS * 2];
-  __shared__ __attribute__((aligned(16))) unsigned char vt_lds[HS * KB * 2];
-  __shared__ __attribute__((aligned(16))) unsigned char p_lds[4][MB][16 * KB * 2];
-  __shared__ long s_kmax;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int fr = lane & 15, fk = lane >> 4;
-  const int h = blockIdx.y, g = h / (n_head / G);
-  const int q0 = blockIdx.x * (64 * MB), qw = q0 + wave * (16 * MB);  // wave rows qw + 16 mb + (0..15)
+// LDS image of a [64 keys][HS] bf16 tile: 16-B chunk ch of row r at byte r * 2HS + 16 (ch ^ sw(r)). For HS = 128
+// this is cdna_hip_programming.md T10 image (b): conflict-free for both the 32x32x16 row reads (K) and the
+// transposed reads (V).
+template <int HS>
+__device__ __forceinline__ int kv_off(int row, int ch) {
+  constexpr int CH = HS / 8;
+  const int sw = CH == 16 ? (((row & 3) << 2) | ((row >> 2) & 3)) : (((row & 3) << 1) | ((row >> 2) & 1));
+  return row * (HS * 2) + 16 * (ch ^ sw);
+}
 
-  // the block's key range: max position over its rows
-  if (tid < 64) {
-    long pm = -1;
+template <int HS>
+__global__ void __launch_bounds__(256, 2) attn_prefill_kernel(const uint16_t* __restrict__ q,
+                                                               const uint16_t* __restrict__ kc,
+                                                               const uint16_t* __restrict__ vc,
+                                                               const int64_t* __restrict__ input_pos,
+                                                               uint16_t* __restrict__ y, int T, int n_head, int G,
+                                                               int max_seq, float scale) {
+  constexpr int KT = 64;         // keys per tile
+  constexpr int CH = HS / 8;     // 16-B chunks per key row
+  constexpr int DK = HS / 16;    // 32x32x16 k-steps over the head dim (S^T)
+  constexpr int DT = HS / 32;    // 32-row tiles of O^T
+  constexpr int TB = KT * HS * 2;  // bytes of one K or V tile image
+  constexpr int LPT = KT * CH / 256;  // 16-B chunks per thread per tile (K and V each)
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2][2][TB];  // [buffer][K | V]
+  __shared__ long s_pos[2][4];                                          // per wave: max / min row position
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hh = lane >> 5, lq = lane & 31;
+  const int head = blockIdx.y, g = head / (n_head / G);
+  const int blk = gridDim.x - 1 - blockIdx.x;  // heaviest (latest) query blocks first
+  const int q0 = blk * 128 + wave * 32;
+  const int t = q0 + lq;
+  const long mypos = t < T ? input_pos[t] : -1;
+
+  // positions: this wave's max (key range) and min (masking needed from there); the workgroup's max
+  {
+    long mx = mypos, mn = t < T ? mypos : LONG_MAX;
 #pragma unroll
-    for (int i = 0; i < MB; ++i) pm = max(pm, tid + 64 * i < T - q0 ? (long)input_pos[q0 + tid + 64 * i] : -1L);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) pm = max(pm, (long)__shfl_xor(pm, o));
-    if (tid == 0) s_kmax = min(pm, (long)max_seq - 1);
-  }
-  // Q fragments (A operand): row fr of each 16-row block, k-slice ks*32 + fk*8
-  bf16x8_t qa[MB][KS];
-  long rpos[MB][4];  // positions of the 4 accumulator rows this lane holds per block
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
-    const int qrow = min(qw + 16 * mb + fr, T - 1);
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-      qa[mb][ks] = *(const bf16x8_t*)(q + ((size_t)qrow * n_head + h) * HS + ks * 32 + fk * 8);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = qw + 16 * mb + fk * 4 + r;
-      rpos[mb][r] = t < T ? input_pos[t] : -1;
+    for (int o = 32; o > 0; o >>= 1) {
+      mx = max(mx, (long)__shfl_xor(mx, o));
+      mn = min(mn, (long)__shfl_xor(mn, o));
     }
+    if (lane == 0) {
+      s_pos[0][wave] = mx;
+      s_pos[1][wave] = mn;
+    }
+  }
+  // Q^T fragments (B operand): lane l holds Q[t][ks*16 + 8*hh .. +8]
+  bf16x8_t qb[DK];
+  {
+    const uint16_t* qr = q + ((size_t)min(t, T - 1) * n_head + head) * HS + 8 * hh;
+#pragma unroll
+    for (int ks = 0; ks < DK; ++ks) qb[ks] = *(const bf16x8_t*)(qr + ks * 16);
   }
   __syncthreads();
-  const int kend = (int)s_kmax + 1;
+  const long wmax = s_pos[0][wave], wmin = s_pos[1][wave];
+  long bmax = max(max(s_pos[0][0], s_pos[0][1]), max(s_pos[0][2], s_pos[0][3]));
+  bmax = min(bmax, (long)max_seq - 1);
+  const int kend = (int)bmax + 1;
+  const int ntiles = (kend + KT - 1) / KT;
 
-  f32x4_t o[MB][NT];
-  float m[MB][4], l[MB][4];
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
-#pragma unroll
-    for (int j = 0; j < NT; ++j) o[mb][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      m[mb][r] = -INFINITY;
-      l[mb][r] = 0.f;
-    }
-  }
   const uint16_t* kbase = kc + (size_t)g * max_seq * HS;
   const uint16_t* vbase = vc + (size_t)g * max_seq * HS;
-  constexpr int CPR = HS / 8;                // 16-B chunks per key row
-  constexpr int LPT = KB * CPR / 256;        // chunks per thread per tile (K and V each)
-  constexpr bool VPAIR = LPT == 2;
-  // K / V tiles are register-staged one tile ahead: tile k0 + KB's global loads are in flight while tile k0 is
-  // multiplied, so each tile costs its MFMA + softmax time, not a global-load round trip
-  // scores in the log2 domain: exp(s * scale - m) = exp2(s * scale * log2(e) - m'), one v_exp_f32 per element
-  const float sl2 = scale * 1.4426950408889634f;
+  // staging: thread tid moves chunks c = tid + 256 i (row c / CH, chunk c % CH) of the K and V tiles
   uint4 kr[LPT], vr[LPT];
-  auto gload = [&](int k0) {
+  int soff[LPT];
 #pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int c = tid + 256 * i, row = c / CPR, ch = c % CPR;
-      const int key = min(k0 + row, max_seq - 1);
-      kr[i] = *(const uint4*)(kbase + (size_t)key * HS + ch * 8);
-      // V: with two chunks per thread, a thread takes keys 2kp, 2kp+1 of one hs chunk so V^T is written as
-      // (key pair) 32-bit words; otherwise the same chunks as K
-      const int vkey = VPAIR ? min(k0 + 2 * (tid / CPR) + i, max_seq - 1) : key;
-      const int vch = VPAIR ? tid % CPR : ch;
-      vr[i] = *(const uint4*)(vbase + (size_t)vkey * HS + vch * 8);
-    }
-  };
-  gload(0);
-  for (int k0 = 0; k0 < kend; k0 += KB) {
-    // stage K (row-major, swizzled) and V^T
-    __syncthreads();  // previous tile's LDS reads are done
-#pragma unroll
-    for (int i = 0; i < LPT; ++i) {
-      const int c = tid + 256 * i, row = c / CPR, ch = c % CPR;
-      *(uint4*)(k_lds + (HS == 128 ? swz256(row, ch) : row * HS * 2 + 16 * (ch ^ (row & 7)))) = kr[i];
-      if (!VPAIR) {
-        const uint32_t d[4] = {vr[i].x, vr[i].y, vr[i].z, vr[i].w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const int col = ch * 8 + e;  // hs index -> row of V^T
-          const uint16_t val = (uint16_t)(e & 1 ? d[e >> 1] >> 16 : d[e >> 1] & 0xFFFF);
-          *(uint16_t*)(vt_lds + swz64(col, row >> 3) + (row & 7) * 2) = val;
-        }
-      }
-    }
-    if (VPAIR) {  // V^T row (hs col) <- 32-bit (key 2kp, key 2kp+1) words: 8 ds_write_b32 instead of 16 b16
-      const int key = 2 * (tid / CPR), ch = tid % CPR;
-      const uint32_t a[4] = {vr[0].x, vr[0].y, vr[0].z, vr[0].w}, b[4] = {vr[1].x, vr[1].y, vr[1].z, vr[1].w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t w = __builtin_amdgcn_perm(b[e >> 1], a[e >> 1], (e & 1) ? 0x07060302u : 0x05040100u);
-        *(uint32_t*)(vt_lds + swz64(ch * 8 + e, key >> 3) + (key & 7) * 2) = w;
-      }
-    }
-    if (k0 + KB < kend) gload(k0 + KB);
-    __syncthreads();
-    // S = Q K^T for this wave's MB x 16 rows x 32 keys (2 column tiles); every K fragment feeds MB MFMAs
-    f32x4_t sacc[MB][2];
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) sacc[mb][0] = sacc[mb][1] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int krow = j * 16 + fr, ch = ks * 4 + fk;
-        const bf16x8_t kb =
-            *(const bf16x8_t*)(k_lds + (HS == 128 ? swz256(krow, ch) : krow * HS * 2 + 16 * (ch ^ (krow & 7))));
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-          sacc[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[mb][ks], kb, sacc[mb][j], 0, 0, 0);
-      }
-    // online softmax per row (lane holds rows fk*4+r of each block, key columns fr and 16+fr); P -> LDS (bf16,
-    // [16 rows][32 keys] per block) -> A fragments
-    bf16x8_t pa[MB];
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      float pr[2][4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float s0 = (k0 + fr <= rpos[mb][r]) ? sacc[mb][0][r] * sl2 : -INFINITY;
-        float s1 = (k0 + 16 + fr <= rpos[mb][r]) ? sacc[mb][1][r] * sl2 : -INFINITY;
-        float mx = fmaxf(s0, s1);
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
-        const float mn = fmaxf(m[mb][r], mx);
-        const float c = mn == -INFINITY ? 1.0f : __builtin_amdgcn_exp2f(m[mb][r] - mn);
-        const float e0 = mn == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(s0 - mn);
-        const float e1 = mn == -INFINITY ? 0.0f : __builtin_amdgcn_exp2f(s1 - mn);
-        float rs = e0 + e1;
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) rs += __shfl_xor(rs, off);
-        l[mb][r] = l[mb][r] * c + rs;
-        m[mb][r] = mn;
-#pragma unroll
-        for (int j = 0; j < NT; ++j) o[mb][j][r] *= c;
-        pr[0][r] = e0;
-        pr[1][r] = e1;
-      }
-      unsigned char* pl = p_lds[wave][mb];
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = fk * 4 + r, key = j * 16 + fr;
-          *(uint16_t*)(pl + swz64(row, key >> 3) + (key & 7) * 2) = f2bf(pr[j][r]);
-        }
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed (the tiles are wave-private)
-    __builtin_amdgcn_wave_barrier();
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) pa[mb] = *(const bf16x8_t*)(p_lds[wave][mb] + swz64(fr, fk));
-    // O += P V; every V fragment feeds MB MFMAs
-#pragma unroll
-    for (int j = 0; j < NT; ++j) {
-      const bf16x8_t vb = *(const bf16x8_t*)(vt_lds + swz64(j * 16 + fr, fk));
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) o[mb][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa[mb], vb, o[mb][j], 0, 0, 0);
-    }
+  for (int i = 0; i < LPT; ++i) soff[i] = kv_off<HS>((tid + 256 * i) / CH, (tid + 256 * i) % CH);
+#define LGA_PF2_GLOAD(K0)                                                                                       \
+  _Pragma("unroll") for (int i = 0; i < LPT; ++i) {                                                             \
+    const int c_ = tid + 256 * i;                                                                               \
+    const size_t key_ = (size_t)min((K0) + c_ / CH, max_seq - 1); /* past the cache: its last row (masked) */  \
+    kr[i] = *(const uint4*)(kbase + key_ * HS + (c_ % CH) * 8);                                                 \
+    vr[i] = *(const uint4*)(vbase + key_ * HS + (c_ % CH) * 8);                                                 \
   }
-  // y[t][h*HS + col] = O / l
+#define LGA_PF2_LSTORE(BUF)                                              \
+  _Pragma("unroll") for (int i = 0; i < LPT; ++i) {                      \
+    *(uint4*)(lds[BUF][0] + soff[i]) = kr[i];                            \
+    *(uint4*)(lds[BUF][1] + soff[i]) = vr[i];                            \
+  }
+
+  f32x16_t o[DT];
 #pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
+  for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int t = qw + 16 * mb + fk * 4 + r;
-      if (t >= T) continue;
-      const float inv = 1.0f / l[mb][r];
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.0f;
+  float m = -INFINITY, l = 0.0f;
+  const float sl2 = scale * 1.4426950408889634f;  // scores in the log2 domain: one v_exp_f32 per element
+
+  if (ntiles > 0) {
+    LGA_PF2_GLOAD(0)
+    LGA_PF2_LSTORE(0)
+  }
+  __syncthreads();
+  for (int it = 0; it < ntiles; ++it) {
+    const int k0 = it * KT, buf = it & 1;
+    LGA_PF2_GLOAD(k0 + KT)  // next tile, in flight under this tile's MFMAs (past the end: clamped, unused)
+    if (k0 <= wmax) {                      // wave-uniform: some row of this wave sees keys of this tile
+      const unsigned char* K = lds[buf][0];
+      const unsigned char* V = lds[buf][1];
+      // S^T for keys k0 + 32 st + crow(r), crow(r) = (r & 3) + 8 (r >> 2) + 4 hh; query t
+      f32x16_t sacc[2];
 #pragma unroll
-      for (int j = 0; j < NT; ++j) y[((size_t)t * n_head + h) * HS + j * 16 + fr] = f2bf(o[mb][j][r] * inv);
+      for (int st = 0; st < 2; ++st) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sacc[st][r] = 0.0f;
+#pragma unroll
+        for (int ks = 0; ks < DK; ++ks) {
+          const bf16x8_t ka = *(const bf16x8_t*)(K + kv_off<HS>(st * 32 + lq, 2 * ks + hh));
+          sacc[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qb[ks], sacc[st], 0, 0, 0);
+        }
+      }
+      const bool need_mask = (long)(k0 + KT - 1) > wmin;  // wave-uniform
+      float x[2][16];
+      float tmax = -INFINITY;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int key = k0 + st * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+          const float v = sacc[st][r] * sl2;
+          x[st][r] = (!need_mask || key <= mypos) ? v : -INFINITY;
+          tmax = fmaxf(tmax, x[st][r]);
+        }
+      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
+      const float mnew = fmaxf(m, tmax);
+      const float mref = mnew == -INFINITY ? 0.0f : mnew;  // rows with no visible key yet: p = 0, o stays 0
+      if (!__all(mnew == m)) {  // some row max moved: rescale (exactly; no threshold)
+        const float c = __builtin_amdgcn_exp2f(m - mref);
+        l *= c;
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[dt][r] *= c;
+      }
+      m = mnew;
+      float rs = 0.0f;
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          x[st][r] = __builtin_amdgcn_exp2f(x[st][r] - mref);
+          rs += x[st][r];
+        }
+      l += rs + __shfl_xor(rs, 32);
+      // P^T as B operands: k-step kk (16 keys) = half-tile kk / 2, registers 8 (kk & 1) .. +7
+      bf16x8_t pb[4];
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        const int st = kk >> 1, r0 = 8 * (kk & 1);
+        const uint32_t w0 = pack2(x[st][r0], x[st][r0 + 1]), w1 = pack2(x[st][r0 + 2], x[st][r0 + 3]);
+        const uint32_t w2 = pack2(x[st][r0 + 4], x[st][r0 + 5]), w3 = pack2(x[st][r0 + 6], x[st][r0 + 7]);
+        const auto a = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
+        const auto b = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
+        const u32x4_t f = {a[0], b[0], a[1], b[1]};  // keys 8 hh + 0..7 of the k-step, in order
+        pb[kk] = __builtin_bit_cast(bf16x8_t, f);
+      }
+      // O^T[d][t] += V^T[d][key] . P^T[key][t]; A = V^T by transposed reads of the row-major V image
+      const int gi = lane & 15, qq = gi >> 2, pp = gi & 3, grp = lane >> 4;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const int c0 = dt * 32 + 16 * (grp & 1);  // first column (d) of this 16-lane group
+#pragma unroll
+        for (int kk = 0; kk < 4; ++kk) {
+          const int r0 = kk * 16 + 8 * (grp >> 1);
+          const int a0 = kv_off<HS>(r0 + qq, (c0 >> 3) + (pp >> 1)) + 8 * (pp & 1);
+          const int a1 = kv_off<HS>(r0 + 4 + qq, (c0 >> 3) + (pp >> 1)) + 8 * (pp & 1);
+          const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(V + a0));
+          const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(V + a1));
+          const i16x8_t f = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, f), pb[kk], o[dt], 0, 0, 0);
+        }
+      }
     }
+    LGA_PF2_LSTORE(buf ^ 1)  // the other buffer: every wave finished reading it before the last barrier
+    __syncthreads();
+  }
+#undef LGA_PF2_GLOAD
+#undef LGA_PF2_LSTORE
+  // y[t][head * HS + d] = O^T[d][t] / l, d = dt * 32 + crow(r): pairs (r, r + 1) are adjacent columns
+  if (t < T) {
+    const float inv = 1.0f / l;
+    uint16_t* yr = y + ((size_t)t * n_head + head) * HS;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int d = dt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        *(uint32_t*)(yr + d) = pack2(o[dt][r] * inv, o[dt][r + 1] * inv);
+      }
+  }
 }
 
 // (keys in flight per row group, waves per workgroup) by q_per_kv; -D overrides are for tools/attn_sweep.py
@@ -561,14 +568,13 @@ extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_c
   LGA_CHECK_ARG(n_splits >= 1 && n_splits <= 256, "lga_attention: n_splits must be in [1, 256]");
   LGA_CHECK_ARG(n_splits == 1 || (workspace && counters), "lga_attention: split attention needs workspace + counters");
   if (T >= 16 && n_splits == 1 && (head_size == 128 || head_size == 64)) {  // prefill: flash attention on MFMA
-    constexpr int MB = LGA_PREFILL_MB;  // 16-row query blocks per wave (64 * MB rows per workgroup)
-    const dim3 grid((T + 64 * MB - 1) / (64 * MB), n_head);
+    const dim3 grid((T + 127) / 128, n_head);
     if (head_size == 128)
-      lga::attn_prefill_kernel<128, MB><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+      lga::attn_prefill_kernel<128><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
                                                               (const uint16_t*)v_cache, input_pos, (uint16_t*)y, T,
                                                               n_head, n_query_groups, max_seq, scale);
     else
-      lga::attn_prefill_kernel<64, MB><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+      lga::attn_prefill_kernel<64><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
                                                              (const uint16_t*)v_cache, input_pos, (uint16_t*)y, T,
                                                              n_head, n_query_groups, max_seq, scale);
     LGA_LAUNCH_RETURN();

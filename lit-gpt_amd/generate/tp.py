@@ -119,7 +119,12 @@ def init_distributed(allreduce: Optional[str] = None) -> Fabric:
     if mode not in ("xgmi", "rccl"):
         raise ValueError(f"allreduce must be 'xgmi' or 'rccl', got {mode!r}")
     if world > 1 and mode == "xgmi" and comm.get_default() is None:
-        comm.set_default(comm.XgmiAllReduce(device=torch.device("cuda", local)))
+        try:
+            comm.set_default(comm.XgmiAllReduce(device=torch.device("cuda", local)))
+        except comm.XgmiUnavailable as e:  # every rank gets here together: all stay on RCCL
+            comm.fallback_reason = str(e)
+            print(f"[generate/tp.py] xGMI one-shot all-reduce unavailable, decode all-reduces use RCCL: {e}",
+                  file=sys.stderr)
     return Fabric(world, rank)
 
 

@@ -26,6 +26,12 @@ from lit_gpt import ops
 DEFAULT_CAP = 32768  # bf16 elements per message (64 KB): decode activations of every config (k * C for MoE)
 
 _default: Optional["XgmiAllReduce"] = None
+fallback_reason: Optional[str] = None  # why init_distributed fell back to RCCL (None: it did not)
+
+
+class XgmiUnavailable(RuntimeError):
+    """Raised on EVERY rank (the outcome is agreed over the group) when the peer mailboxes cannot be mapped or the
+    start-up self-test of the one-shot all-reduce fails."""
 
 
 class XgmiAllReduce:
@@ -48,19 +54,51 @@ class XgmiAllReduce:
         dist.all_gather_object(handles, bytes(handle.raw), group=group)
         ptrs = []
         self._opened = []
+        failure = None
         with torch.cuda.device(self.device):
             for r, h in enumerate(handles):
                 if r == self.rank:
                     ptrs.append(own.value)
                     continue
                 p = ctypes.c_void_p()
-                ops._check(lib.lga_comm_open(h, ctypes.byref(p)))
+                try:
+                    ops._check(lib.lga_comm_open(h, ctypes.byref(p)))
+                except RuntimeError as e:  # agreed below, so no rank waits on a peer that gave up
+                    failure = f"rank {self.rank}: mapping rank {r}'s mailbox failed: {e}"
+                    break
                 self._opened.append(p)
                 ptrs.append(p.value)
-        self._mailboxes = (ctypes.c_void_p * self.world)(*ptrs)
         self.seq = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
-        dist.barrier(group=group)
+        self._agree(failure, "mailbox mapping")
+        self._mailboxes = (ctypes.c_void_p * self.world)(*ptrs)
+        self._self_test()
+
+    def _agree(self, failure: Optional[str], what: str) -> None:
+        """All ranks learn whether any rank failed (MIN over a flag); on failure every rank raises."""
+        flag = torch.tensor([0 if failure else 1], dtype=torch.int32,
+                            device=self.device if dist.get_backend(self.group) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) == 0:
+            self.close()
+            raise XgmiUnavailable(failure or f"{what} failed on another rank")
+
+    def _self_test(self) -> None:
+        """One reduction of known values (rank r contributes r + 1 at every element, + a residual of 0.5): checks
+        that the peers' pushes and flags are visible through the mapped memory before any real call trusts it."""
+        n = 1024
+        x = torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device=self.device)
+        res = torch.full((n,), 0.5, dtype=torch.bfloat16, device=self.device)
+        with torch.cuda.device(self.device):
+            y = self.all_reduce(x, residual=res)
+            torch.cuda.synchronize(self.device)
+        want = float(self.world * (self.world + 1) // 2) + 0.5
+        failure = None
+        if self.errors():
+            failure = f"rank {self.rank}: self-test timed out waiting for a peer"
+        elif not bool((y.float() == want).all()):
+            failure = f"rank {self.rank}: self-test sum wrong ({y.float()[:4].tolist()} vs {want})"
+        self._agree(failure, "self-test")
 
     def supports(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype == torch.bfloat16 and t.numel() <= self.cap and t.numel() % 8 == 0
@@ -92,6 +130,7 @@ class XgmiAllReduce:
     def close(self) -> None:
         lib = ops.load_library()
         torch.cuda.synchronize(self.device)
+        self._mailboxes = None
         for p in self._opened:
             lib.lga_comm_close(p)
         self._opened = []
