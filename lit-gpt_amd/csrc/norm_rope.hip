@@ -9,6 +9,8 @@
 //   lga_layernorm      torch.nn.LayerNorm (GPT-NeoX / pythia norm_class, reference config.py:137-144): fp32 mean and
 //                      variance, (x - mean) * rstd * w + b in fp32, one bf16 cast
 //   lga_gelu           GptNeoxMLP's activation (model.py:699-702): F.gelu exact (erf) or tanh, fp32, one bf16 cast
+#include <algorithm>
+
 #include "common.h"
 
 namespace lga {
@@ -112,6 +114,83 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(const uint16_t* __restrict
   }
 }
 
+// Vector form of rope_kv_kernel (same arithmetic per element): one thread moves one 16-B chunk (8 elements) of a
+// (token, group, slot) row; the rotate-half partner is the chunk half / 8 away. Needs hs % 8 == 0 and
+// (rope_n_elem / 2) % 8 == 0 (Llama: 128 / 64, pythia: 16 / 8); other geometries take the scalar kernel.
+__global__ void __launch_bounds__(256) rope_kv_vec_kernel(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ q_out,
+                                                          uint16_t* __restrict__ k_cache,
+                                                          uint16_t* __restrict__ v_cache,
+                                                          const int64_t* __restrict__ cache_pos,
+                                                          const int64_t* __restrict__ rope_pos,
+                                                          const float* __restrict__ cos, const float* __restrict__ sin,
+                                                          int T, int n_head, int n_groups, int hs, int n_elem,
+                                                          int max_seq, int rope_rows) {
+  const int qpk = n_head / n_groups, cph = hs / 8, half = n_elem / 2;
+  const long per_t = (long)n_groups * (qpk + 2) * cph;  // chunks per token
+  const long total = (long)T * per_t;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    const int t = (int)(i / per_t);
+    const int rem = (int)(i % per_t);
+    const int g = rem / ((qpk + 2) * cph), slot = (rem / cph) % (qpk + 2), c = rem % cph;
+    const long p = cache_pos[t], rp = rope_pos[t];
+    if (p < 0 || p >= max_seq || rp < 0 || rp >= rope_rows) continue;  // host validates; never out of bounds
+    const uint16_t* xs = qkv + ((size_t)t * (n_head + 2 * n_groups) + (size_t)g * (qpk + 2) + slot) * hs;
+    uint4 v = ((const uint4*)xs)[c];
+    const int d0 = c * 8;
+    if (slot <= qpk && d0 < n_elem) {
+      const bool lo = d0 < half;
+      const uint4 pv = ((const uint4*)xs)[lo ? c + half / 8 : c - half / 8];
+      const float4* cr = (const float4*)(cos + (size_t)rp * n_elem + d0);
+      const float4* sr = (const float4*)(sin + (size_t)rp * n_elem + d0);
+      const float4 c0 = cr[0], c1 = cr[1], s0 = sr[0], s1 = sr[1];
+      const float cf[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+      const float sf[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+      const uint32_t xw[4] = {v.x, v.y, v.z, v.w}, pw[4] = {pv.x, pv.y, pv.z, pv.w};
+      uint32_t ow[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float x0 = bflo(xw[k]), x1 = bfhi(xw[k]);
+        const float r0 = lo ? -bflo(pw[k]) : bflo(pw[k]), r1 = lo ? -bfhi(pw[k]) : bfhi(pw[k]);
+        const float o0 = add_rn(mul_rn(x0, cf[2 * k]), mul_rn(r0, sf[2 * k]));
+        const float o1 = add_rn(mul_rn(x1, cf[2 * k + 1]), mul_rn(r1, sf[2 * k + 1]));
+        ow[k] = (uint32_t)f2bf(o0) | ((uint32_t)f2bf(o1) << 16);
+      }
+      v = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    }
+    uint4* dst = slot < qpk ? (uint4*)(q_out + ((size_t)t * n_head + (size_t)g * qpk + slot) * hs)
+                            : (uint4*)((slot == qpk ? k_cache : v_cache) + ((size_t)g * max_seq + p) * hs);
+    dst[c] = v;
+  }
+}
+
+__global__ void __launch_bounds__(256) add_vec_kernel(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                      uint4* __restrict__ y, size_t n8) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    const uint4 u = a[i], w = b[i];
+    const uint32_t ua[4] = {u.x, u.y, u.z, u.w}, wa[4] = {w.x, w.y, w.z, w.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      o[k] = (uint32_t)f2bf(bflo(ua[k]) + bflo(wa[k])) | ((uint32_t)f2bf(bfhi(ua[k]) + bfhi(wa[k])) << 16);
+    y[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+__global__ void __launch_bounds__(256) swiglu_vec_kernel(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                         uint4* __restrict__ y, size_t n8) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n8; i += (size_t)gridDim.x * 256) {
+    const uint4 u = a[i], w = b[i];
+    const uint32_t ua[4] = {u.x, u.y, u.z, u.w}, wa[4] = {w.x, w.y, w.z, w.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float g0 = round_bf(silu_f(bflo(ua[k]))), g1 = round_bf(silu_f(bfhi(ua[k])));
+      o[k] = (uint32_t)f2bf(__fmul_rn(g0, bflo(wa[k]))) | ((uint32_t)f2bf(__fmul_rn(g1, bfhi(wa[k]))) << 16);
+    }
+    y[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 template <typename IDX>
 __global__ void __launch_bounds__(256) embedding_kernel(const IDX* __restrict__ idx, const uint16_t* __restrict__ table,
                                                         uint16_t* __restrict__ out, int C, int V) {
@@ -161,6 +240,15 @@ extern "C" int lga_rope_kv_append(const void* qkv, void* q_out, void* k_cache, v
                 "lga_rope_kv_append: bad head geometry");
   LGA_CHECK_ARG(rope_n_elem >= 0 && rope_n_elem <= head_size && rope_n_elem % 2 == 0,
                 "lga_rope_kv_append: rope_n_elem must be even and <= head_size");
+  if (head_size % 8 == 0 && (rope_n_elem / 2) % 8 == 0 &&
+      ((uintptr_t)qkv | (uintptr_t)q_out | (uintptr_t)k_cache | (uintptr_t)v_cache | (uintptr_t)cos | (uintptr_t)sin) % 16 == 0) {
+    const long chunks = (long)T * (n_head + 2 * n_query_groups) * (head_size / 8);
+    const unsigned blocks = (unsigned)std::min<long>((chunks + 255) / 256, 8192);
+    lga::rope_kv_vec_kernel<<<blocks, 256, 0, stream>>>((const uint16_t*)qkv, (uint16_t*)q_out, (uint16_t*)k_cache,
+                                                       (uint16_t*)v_cache, cache_pos, rope_pos, cos, sin, T, n_head,
+                                                       n_query_groups, head_size, rope_n_elem, max_seq, rope_rows);
+    LGA_LAUNCH_RETURN();
+  }
   const dim3 grid(T, n_query_groups);
   lga::rope_kv_kernel<<<grid, 256, 0, stream>>>((const uint16_t*)qkv, (uint16_t*)q_out, (uint16_t*)k_cache,
                                                 (uint16_t*)v_cache, cache_pos, rope_pos, cos, sin, n_head,
@@ -182,6 +270,11 @@ extern "C" int lga_embedding(const void* idx, int idx_is_int64, const void* tabl
 
 extern "C" int lga_add(const void* a, const void* b, void* y, long n, hipStream_t stream) {
   LGA_CHECK_ARG(a && b && y && n > 0, "lga_add: bad arguments");
+  if (n % 8 == 0 && ((uintptr_t)a | (uintptr_t)b | (uintptr_t)y) % 16 == 0) {
+    lga::add_vec_kernel<<<lga::elementwise_grid(n / 8), 256, 0, stream>>>((const uint4*)a, (const uint4*)b, (uint4*)y,
+                                                                         (size_t)n / 8);
+    LGA_LAUNCH_RETURN();
+  }
   lga::add_kernel<<<lga::elementwise_grid(n), 256, 0, stream>>>((const uint16_t*)a, (const uint16_t*)b,
                                                                  (uint16_t*)y, (size_t)n);
   LGA_LAUNCH_RETURN();
@@ -189,6 +282,11 @@ extern "C" int lga_add(const void* a, const void* b, void* y, long n, hipStream_
 
 extern "C" int lga_swiglu(const void* a, const void* b, void* y, long n, hipStream_t stream) {
   LGA_CHECK_ARG(a && b && y && n > 0, "lga_swiglu: bad arguments");
+  if (n % 8 == 0 && ((uintptr_t)a | (uintptr_t)b | (uintptr_t)y) % 16 == 0) {
+    lga::swiglu_vec_kernel<<<lga::elementwise_grid(n / 8), 256, 0, stream>>>((const uint4*)a, (const uint4*)b,
+                                                                            (uint4*)y, (size_t)n / 8);
+    LGA_LAUNCH_RETURN();
+  }
   lga::swiglu_kernel<<<lga::elementwise_grid(n), 256, 0, stream>>>((const uint16_t*)a, (const uint16_t*)b,
                                                                     (uint16_t*)y, (size_t)n);
   LGA_LAUNCH_RETURN();

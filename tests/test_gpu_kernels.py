@@ -282,7 +282,8 @@ def test_rmsnorm_matches_oracle(ops, golden):
     assert (y == ref).float().mean() > 0.97
 
 
-@pytest.mark.parametrize("H,G,hs,n_elem", [(32, 32, 128, 128), (8, 2, 128, 128), (4, 1, 64, 64), (12, 12, 64, 16)])
+@pytest.mark.parametrize("H,G,hs,n_elem", [(32, 32, 128, 128), (8, 2, 128, 128), (4, 1, 64, 64), (12, 12, 64, 16),
+                                           (4, 2, 80, 20)])  # the last: scalar kernel (half not a multiple of 8)
 def test_rope_kv_append_bit_exact(ops, H, G, hs, n_elem):
     T, S = 7, 40
     qkv = bf16_np(synth.normal((T, (H + 2 * G) * hs), "qkv", 5, 1.0))
@@ -493,6 +494,17 @@ def test_embedding_and_add(ops):
     np.testing.assert_array_equal(out, table[idx.numpy()])
     a, b = to_dev_bf16(table[:4]), to_dev_bf16(table[4:8])
     assert torch.equal(ops.add(a, b), (a.float() + b.float()).bfloat16())
+
+
+@pytest.mark.parametrize("n", [8, 4096, 2048 * 11008])
+def test_vector_elementwise_equals_scalar(ops, n):
+    """lga_add / lga_swiglu take 16-B vector kernels when n % 8 == 0: same bits as the scalar kernels (odd n)."""
+    a = (torch.randn(n + 1, device=DEV) * 3).bfloat16()
+    b = (torch.randn(n + 1, device=DEV) * 3).bfloat16()
+    assert torch.equal(ops.add(a[:n], b[:n]), (a[:n].float() + b[:n].float()).bfloat16())
+    vec = ops.swiglu(a[:n], b[:n])
+    sca = ops.swiglu(a[: n + 1], b[: n + 1])  # n + 1 is odd: the scalar kernel
+    assert torch.equal(vec, sca[:n])
 
 
 def test_errors_are_raised(ops):
