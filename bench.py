@@ -38,6 +38,7 @@ for _p in (str(REPO / "lit-gpt_amd"), str(REPO)):
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 MODEL = "Llama-2-7b-hf"
 PROMPT_LEN = 2048
+CHUNK = 8  # decode steps per graph launch (generate/base.py DECODE_CHUNK)
 
 
 def algorithmic_bytes_per_token(cfg, pos: float, group: int = 128, tp: int = 1, dense: bool = False) -> float:
@@ -383,8 +384,8 @@ def main():
         use_graph = not args.no_graph
         graph_note = None
         if use_graph:
-            try:
-                dg = DecodeGraph(model, first, T)  # first decode step runs eagerly, then the step is captured
+            try:  # first decode step runs eagerly, then the step (and CHUNK steps as one graph) is captured
+                dg = DecodeGraph(model, first, T, chunk=CHUNK)
             except Exception as e:  # e.g. a collective backend that cannot be captured: time the eager loop
                 use_graph, graph_note = False, f"graph capture failed ({type(e).__name__}); eager steps"
                 torch.cuda.synchronize()
@@ -402,13 +403,19 @@ def main():
                 nonlocal tok
                 tok = next_token(model, pos, tok.view(1, 1), temperature=0.0)
                 pos.add_(1)
-        for _ in range(args.warmup):
-            step()
+        def run(n):  # n decode steps: whole CHUNK-step graph launches, then single steps
+            done = 0
+            while use_graph and n - done >= CHUNK > 1:
+                dg.steps()
+                done += CHUNK
+            for _ in range(n - done):
+                step()
+
+        run(args.warmup)
         torch.cuda.synchronize()
         barrier()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
+        run(args.steps)
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
@@ -444,7 +451,8 @@ def main():
                    "weights": args.quantize, "prompt_len": T, "decode_positions": [T + args.warmup + 1,
                                                                                    T + args.warmup + args.steps],
                    "global_batch": 1, "seq_len": T, "parallelism": f"tp{world}",
-                   "graph": use_graph, **({"graph_note": graph_note} if graph_note else {}),
+                   "graph": use_graph, "steps_per_graph_launch": CHUNK if use_graph else 0,
+                   **({"graph_note": graph_note} if graph_note else {}),
                    **({"allreduce": "xgmi one-shot" if gtp.comm.get_default() is not None else
                        f"rccl ({gtp.comm.fallback_reason or 'LGA_TP_ALLREDUCE=rccl'})"} if world > 1 else {})},
         "roofline": {"bound": "hbm", "kernel": (

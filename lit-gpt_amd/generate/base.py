@@ -54,6 +54,9 @@ def next_token(model: GPT, input_pos: torch.Tensor, x: torch.Tensor, **kwargs: A
     return sample(logits, **kwargs).to(dtype=x.dtype)
 
 
+DECODE_CHUNK = 8  # greedy decode steps per graph launch (lit_gpt/runtime.py DecodeGraph.steps)
+
+
 @torch.inference_mode()
 def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temperature: float = 1.0,
              top_k: Optional[int] = None, eos_id: Optional[int] = None, use_graph: bool = True) -> torch.Tensor:
@@ -73,18 +76,29 @@ def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temp
     if temperature == 0.0 and use_graph:
         from lit_gpt.runtime import DecodeGraph
 
-        if eos_id is not None and int(token) == eos_id:
-            return torch.cat(tokens)
-        dg = DecodeGraph(model, token, T)  # runs the first decode step eagerly, then captures the step
+        # (the prefill's token is never tested against eos: the reference's loop only tests the decoded ones,
+        # generate/base.py:86-92)
+        # runs the first decode step eagerly, then captures the step (and DECODE_CHUNK steps as one graph)
+        dg = DecodeGraph(model, token, T, chunk=DECODE_CHUNK if n_steps > DECODE_CHUNK else 1)
         out = torch.empty(n_steps, dtype=prompt.dtype, device=device)
         out[0] = dg.token.view(-1)[0]
         produced = 1
         if not (eos_id is not None and int(out[0]) == eos_id):
-            for i in range(1, n_steps):
-                out[i] = dg.step().view(-1)[0]
-                produced = i + 1
-                if eos_id is not None and int(out[i]) == eos_id:
-                    break
+            i = 1
+            while i < n_steps:
+                if dg.chunk > 1 and n_steps - i >= dg.chunk:
+                    out[i:i + dg.chunk] = dg.steps()
+                    n = dg.chunk
+                else:
+                    out[i] = dg.step().view(-1)[0]
+                    n = 1
+                produced = i + n
+                if eos_id is not None:  # one host check per launch; tokens past an eos are dropped
+                    hit = (out[i:i + n] == eos_id).nonzero()
+                    if hit.numel():
+                        produced = i + int(hit[0]) + 1
+                        break
+                i += n
         tokens.append(out[:produced])
         return torch.cat(tokens)
     input_pos = torch.tensor([T], device=device)

@@ -6,7 +6,7 @@ chain of hand-written HIP kernels (per layer: fused RMSNorm+qkv GEMV, RoPE+KV ap
 combine, proj GEMV+residual, fused RMSNorm+SwiGLU GEMV, down GEMV+residual; then RMSNorm+lm_head GEMV and
 argmax). ``DecodeGraph`` captures that chain once with static input buffers — the token id and ``input_pos``
 live on the device, the argmax kernel writes the next token and advances ``input_pos`` — so a decode step is a
-single ``hipGraphLaunch`` with no host<->device synchronisation.
+single ``hipGraphLaunch`` with no host<->device synchronisation (or, with ``chunk``, several steps are).
 """
 
 from __future__ import annotations
@@ -19,24 +19,36 @@ from lit_gpt import ops
 
 
 class DecodeGraph:
-    def __init__(self, model, first_token: torch.Tensor, first_pos: int) -> None:
+    def __init__(self, model, first_token: torch.Tensor, first_pos: int, chunk: int = 1) -> None:
         """Runs one real decode step eagerly (token ``first_token`` at position ``first_pos``) to warm up, then
-        captures the step. Afterwards ``self.token`` holds the newest token and ``self.pos`` its position."""
+        captures the step. Afterwards ``self.token`` holds the newest token and ``self.pos`` its position.
+        ``chunk`` > 1 also captures ``chunk`` consecutive steps as one graph (``steps()``): the argmax of step i
+        writes its token into ``self.history[i]`` as well, and one launch replaces ``chunk`` (≈9 us of
+        graph-launch gap per step on MI355X, profiles/r02b_*)."""
         dev = first_token.device
         self.model = model
         self.token = first_token.reshape(1, 1).to(torch.int32).clone()
         self.pos = torch.tensor([first_pos], dtype=torch.int64, device=dev)
+        self.chunk = max(1, int(chunk))
+        self.history = torch.zeros(self.chunk, dtype=torch.int64, device=dev)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
+        self.chunk_graph: Optional[torch.cuda.CUDAGraph] = None
         self._step_eager()
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self._step_body()
         self.graph = g
+        if self.chunk > 1:
+            gc = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(gc):
+                for i in range(self.chunk):
+                    self._step_body(self.history[i:i + 1])
+            self.chunk_graph = gc
 
-    def _step_body(self) -> None:
+    def _step_body(self, idx_out: Optional[torch.Tensor] = None) -> None:
         logits = self.model(self.token, self.pos, last_token_only=True)
-        ops.argmax(logits.reshape(-1), token_out=self.token.view(-1), pos_inout=self.pos)
+        ops.argmax(logits.reshape(-1), out_idx=idx_out, token_out=self.token.view(-1), pos_inout=self.pos)
 
     def _step_eager(self) -> None:
         self._step_body()
@@ -45,3 +57,10 @@ class DecodeGraph:
         """One decode step; returns the (device) token buffer holding the new token."""
         self.graph.replay()
         return self.token
+
+    def steps(self) -> torch.Tensor:
+        """``chunk`` decode steps in one graph launch; returns the (device, int64) buffer of their tokens."""
+        if self.chunk_graph is None:
+            raise RuntimeError("DecodeGraph was built with chunk=1")
+        self.chunk_graph.replay()
+        return self.history

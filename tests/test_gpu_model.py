@@ -213,6 +213,16 @@ def test_greedy_generate_graph_equals_eager_and_oracle(key, mode):
     y_eager = generate(model, prompt, T + N, temperature=0.0, use_graph=False).cpu()
     assert torch.equal(y_graph, y_eager)
     assert y_graph.shape == (T + N,) and torch.equal(y_graph[:T], prompt.cpu())
+    # eos inside a multi-step graph launch (generate/base.py DECODE_CHUNK): the stream stops at its first
+    # occurrence exactly as the eager loop does
+    eos = int(y_graph[T + 12])
+    stops = {}
+    for graph in (True, False):
+        for b in model.transformer.h:
+            b.attn.kv_cache.reset_parameters()
+        stops[graph] = generate(model, prompt, T + N, temperature=0.0, eos_id=eos, use_graph=graph).cpu()
+    assert torch.equal(stops[True], stops[False]) and int(stops[True][-1]) == eos
+    assert torch.equal(stops[True], y_graph[:stops[True].numel()])
     # oracle, teacher-forced on the GPU's own tokens: each GPU token must be the oracle's argmax unless the
     # oracle's top-2 margin is within the logit tolerance
     ref = oracle_for(cfg, sd, mode)
