@@ -13,6 +13,12 @@ __device__ __forceinline__ uint4 ld_nt16(const void* p) {  // 16-B non-temporal 
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float dot2_f16(uint32_t a, uint32_t b, float c) {
+  return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2_t, a), __builtin_bit_cast(f16x2_t, b), c, false);
+}
+
 __device__ __forceinline__ float dot2_bf16(uint32_t a, uint32_t b, float c) {
   return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, a), __builtin_bit_cast(bf16x2_t, b), c,
                                          false);
@@ -83,7 +89,7 @@ __device__ __forceinline__ float scale_of(uint32_t bits) {
   return FMT == 0 ? __uint_as_float(bits << 16) : __uint_as_float(bits);
 }
 
-// (v & mask) | 0x43004300 in ONE VOP3 op (v_and_or_b32): gfx9 VOP3 takes no literal, so both constants live in
+// (v & mask) | magic in ONE VOP3 op (v_and_or_b32): gfx9 VOP3 takes no literal, so both constants live in
 // registers materialised once per kernel — the mask in a VGPR, the magic in an SGPR — behind asm the compiler
 // cannot constant-fold (with literals it emits the two-op VOP2 and/or pair; as inline asm of its own the op
 // would cost an s_nop hazard slot in front of every dependent v_dot2c).
@@ -95,44 +101,54 @@ __device__ __forceinline__ uint32_t nibble_mask() {  // 0x000F000F in a VGPR, ma
   asm volatile("v_mov_b32 %0, 0x000F000F" : "=v"(m));
   return m;
 }
-__device__ __forceinline__ uint32_t bf16_magic() {  // 0x43004300 (bf16 pair 128, 128) in an SGPR
+
+__device__ __forceinline__ uint32_t nibble_mask_hi() {  // 0x00F000F0 in a VGPR (fp16 int4 dot)
   uint32_t m;
-  asm volatile("s_mov_b32 %0, 0x43004300" : "=s"(m));
+  asm volatile("v_mov_b32 %0, 0x00F000F0" : "=v"(m));
+  return m;
+}
+__device__ __forceinline__ uint32_t f16_magic() {  // 0x64006400 (fp16 pair 1024, 1024) in an SGPR
+  uint32_t m;
+  asm volatile("s_mov_b32 %0, 0x64006400" : "=s"(m));
   return m;
 }
 
-// dot of one 16-byte weight chunk (32 nibbles) with the LDS x chunk (4 uint4 of (x_i, x_i+4) pairs)
+// Stage 8 activations (bf16 pairs d = (x0,x1) (x2,x3) (x4,x5) (x6,x7)) as the LDS pair layout the chunk dot reads:
+// (x0,x4) (x1,x5) (x2,x6) (x3,x7); returns this thread's share of the chunk correction. nf4: bf16 pairs by byte
+// permutes (the codebook FMAs read them), correction unused. int4: fp16 pairs with the odd slots pre-divided by 16
+// (bf16 values convert exactly for |x| in [2^-10, 65504]; smaller ones round toward zero in fp16's subnormals, at
+// most 2^-24 absolute), correction = 1032 sum x_even + 72 sum x_odd (see chunk_dot_rows).
 template <int FMT>
-__device__ __forceinline__ float chunk_dot(const uint4 w, const uint4* xc, float xsum, const float* nf4,
-                                           uint32_t mask, uint32_t magic) {
-  const uint32_t wd[4] = {w.x, w.y, w.z, w.w};
-  float d = 0.0f;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const uint4 xv = xc[j];
-    const uint32_t xp[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      if (FMT == 0) {
-        d = dot2_bf16(xp[s], and_or_magic(s == 0 ? wd[j] : wd[j] >> (4 * s), mask, magic), d);
-      } else {
-        d = fmaf(nf4[(wd[j] >> (4 * s)) & 0xF], bflo(xp[s]), d);
-        d = fmaf(nf4[(wd[j] >> (4 * s + 16)) & 0xF], bfhi(xp[s]), d);
-      }
-    }
+__device__ __forceinline__ float stage_x8(const uint32_t (&d)[4], uint4& out) {
+  if (FMT == 0) {
+    const float x0 = bflo(d[0]), x1 = bfhi(d[0]), x2 = bflo(d[1]), x3 = bfhi(d[1]);
+    const float x4 = bflo(d[2]), x5 = bfhi(d[2]), x6 = bflo(d[3]), x7 = bfhi(d[3]);
+    const float k = 0.0625f;
+    out = make_uint4(__builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(x0, x4)),
+                     __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(x1 * k, x5 * k)),
+                     __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(x2, x6)),
+                     __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(x3 * k, x7 * k)));
+    return 1032.0f * ((x0 + x2) + (x4 + x6)) + 72.0f * ((x1 + x3) + (x5 + x7));
   }
-  // int4: sum x*(128+q) - 136*sum x = sum x*(q-8), as ONE explicit fma: left to -ffp-contract the compiler fuses
-  // it in some kernel variants and not in others, and variants must agree bit for bit (tests compare them)
-  return FMT == 0 ? __builtin_fmaf(-136.0f, xsum, d) : d;
+  out = make_uint4(__builtin_amdgcn_perm(d[2], d[0], 0x05040100u), __builtin_amdgcn_perm(d[2], d[0], 0x07060302u),
+                   __builtin_amdgcn_perm(d[3], d[1], 0x05040100u), __builtin_amdgcn_perm(d[3], d[1], 0x07060302u));
+  return ((bflo(d[0]) + bfhi(d[0])) + (bflo(d[1]) + bfhi(d[1]))) + ((bflo(d[2]) + bfhi(d[2])) + (bflo(d[3]) + bfhi(d[3])));
 }
 
-// The same dot for R weight chunks (the rows / matrices of a wave) against ONE x chunk, interleaved pair by pair:
-// R independent accumulation chains give the scheduler work between each unpack and its dependent v_dot2c (one
-// chain at a time leaves an s_nop hazard slot in front of every dot). Per-row arithmetic and order are exactly
-// chunk_dot's, so the results are bit-identical.
+// Dot of R 16-byte weight chunks (32 nibbles each: the rows / matrices of a wave) against ONE x chunk, interleaved
+// pair by pair: R independent accumulation chains give the scheduler work between each unpack and its dependent
+// v_dot2c (one chain at a time leaves an s_nop hazard slot in front of every dot). Every caller (one-shot and
+// streaming GEMV, every epilogue) goes through this function, so their results agree bit for bit.
+//
+// int4: fp16 magic bias — (w & 0x000F000F) | 0x64006400 = fp16 (1024 + q) and (w & 0x00F000F0) | 0x64006400 =
+// fp16 (1024 + 16 q) need no shift for nibbles 0, 1 (4, 5) and one shared w >> 8 for 2, 3 (6, 7): 5 unpack ops
+// per 8 weights (bf16's 128 + q bias needed 7: three shifts), fed to v_dot2c_f32_f16; with the odd x slots staged
+// / 16, sum x (q - 8) = dot - (1032 sum x_even + 72 sum x_odd) = dot - corr. tools/gemv_variants.py, 7B shapes:
+// qkv -0.2..0.4, o_proj -0.2, fc_1||fc_2 -0.6..0.8, mlp.proj -0.1..0.3, lm_head -0.8..1.1 us per launch vs the
+// bf16 form. nf4: codebook values from LDS, fp32 FMAs against the bf16 x pairs.
 template <int FMT, int R>
-__device__ __forceinline__ void chunk_dot_rows(const uint4 (&w)[R], const uint4* xc, float xsum, const float* nf4,
-                                               uint32_t mask, uint32_t magic, float (&d)[R]) {
+__device__ __forceinline__ void chunk_dot_rows(const uint4 (&w)[R], const uint4* xc, float corr, const float* nf4,
+                                               uint32_t mask, uint32_t magic, uint32_t mask_hi, float (&d)[R]) {
 #pragma unroll
   for (int r = 0; r < R; ++r) d[r] = 0.0f;
 #pragma unroll
@@ -140,22 +156,26 @@ __device__ __forceinline__ void chunk_dot_rows(const uint4 (&w)[R], const uint4*
     const uint4 xv = xc[j];
     const uint32_t xp[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int r = 0; r < R; ++r) {
+      const uint32_t wd = j == 0 ? w[r].x : (j == 1 ? w[r].y : (j == 2 ? w[r].z : w[r].w));
+      if (FMT == 0) {
+        const uint32_t w8 = wd >> 8;
+        d[r] = dot2_f16(xp[0], and_or_magic(wd, mask, magic), d[r]);
+        d[r] = dot2_f16(xp[1], and_or_magic(wd, mask_hi, magic), d[r]);
+        d[r] = dot2_f16(xp[2], and_or_magic(w8, mask, magic), d[r]);
+        d[r] = dot2_f16(xp[3], and_or_magic(w8, mask_hi, magic), d[r]);
+      } else {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const uint32_t wd = j == 0 ? w[r].x : (j == 1 ? w[r].y : (j == 2 ? w[r].z : w[r].w));
-        if (FMT == 0) {
-          d[r] = dot2_bf16(xp[s], and_or_magic(s == 0 ? wd : wd >> (4 * s), mask, magic), d[r]);
-        } else {
+        for (int s = 0; s < 4; ++s) {
           d[r] = fmaf(nf4[(wd >> (4 * s)) & 0xF], bflo(xp[s]), d[r]);
           d[r] = fmaf(nf4[(wd >> (4 * s + 16)) & 0xF], bfhi(xp[s]), d[r]);
         }
       }
     }
   }
-  if (FMT == 0) {
+  if (FMT == 0) {  // ONE explicit op: left to -ffp-contract the compiler could fuse it differently per variant
 #pragma unroll
-    for (int r = 0; r < R; ++r) d[r] = __builtin_fmaf(-136.0f, xsum, d[r]);
+    for (int r = 0; r < R; ++r) d[r] = __builtin_fmaf(-1.0f, corr, d[r]);
   }
 }
 

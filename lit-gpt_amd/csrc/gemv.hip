@@ -17,8 +17,9 @@
 //    loads in flight), then staged once per workgroup in LDS as bf16 pairs (x_k, x_k+4) with per-chunk sums;
 //    the fused RMSNorm (lit_gpt/rmsnorm.py:19-25: bf16(w * (x * rsqrt(mean(x^2) + eps))), the reference's
 //    rounding point) runs during that staging, while the weights stream.
-//  * int4-g: one AND-OR turns two nibbles into the bf16 pair (128+q_k, 128+q_k+4) for v_dot2c_f32_bf16, and
-//    sum x*(q-8) = dot - 136*sum(x); nf4: codebook in LDS, fp32 FMAs; one scale/absmax FMA per 32 weights.
+//  * int4-g: one AND-OR turns two nibbles into the fp16 pair (1024 + q, or 1024 + 16 q for the high nibble of a
+//    byte) for v_dot2c_f32_f16 against fp16 x pairs (odd slots staged / 16), and sum x*(q-8) = dot - corr
+//    (decode_ops.h chunk_dot_rows); nf4: codebook in LDS, fp32 FMAs; one scale/absmax FMA per 32 weights.
 //  * Reduction: a transposed butterfly sums R = RPR (x2 for the dual GEMV) row partials across the wave with
 //    log2(R) halving exchanges + DPP, instead of R separate wave reductions.
 //  * Epilogues: +bias, +residual (Block residual add, model.py:591-592), dual-weight SwiGLU

@@ -173,14 +173,12 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
         d[q] = pack2(__fmul_rn(bflo(nw[q]), __fmul_rn(bflo(d[q]), rs)),
                      __fmul_rn(bfhi(nw[q]), __fmul_rn(bfhi(d[q]), rs)));
     }
-    float cs = ((bflo(d[0]) + bfhi(d[0])) + (bflo(d[1]) + bfhi(d[1]))) +
-               ((bflo(d[2]) + bfhi(d[2])) + (bflo(d[3]) + bfhi(d[3])));
+    uint4 xv;
+    float cs = stage_x8<FMT>(d, xv);
     cs += __shfl_xor(cs, 1);  // 4 consecutive threads hold one 32-element chunk
     cs += __shfl_xor(cs, 2);
     if (u < n8) {
-      // (x0,x4) (x1,x5) (x2,x6) (x3,x7): byte permutes of the bf16 pairs
-      xl[u] = make_uint4(__builtin_amdgcn_perm(d[2], d[0], 0x05040100u), __builtin_amdgcn_perm(d[2], d[0], 0x07060302u),
-                         __builtin_amdgcn_perm(d[3], d[1], 0x05040100u), __builtin_amdgcn_perm(d[3], d[1], 0x07060302u));
+      xl[u] = xv;  // (x0,x4) (x1,x5) (x2,x6) (x3,x7) pairs (stage_x8)
       if ((u & 3) == 0) xsum[u >> 2] = cs;
     }
   }
@@ -189,7 +187,7 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
   LGA_GTRACE(4);
 
   // 4. dequant-dot every row of this wave, then one butterfly for all of them
-  const uint32_t nmask = nibble_mask(), nmagic = bf16_magic();
+  const uint32_t nmask = nibble_mask(), nmagic = f16_magic(), nmask_hi = nibble_mask_hi();
   float part[R];
 #pragma unroll
   for (int i = 0; i < R; ++i) part[i] = 0.0f;
@@ -225,7 +223,7 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
       }
     }
     float d[R];
-    chunk_dot_rows<FMT, R>(wj, xc, xs, nf4, nmask, nmagic, d);
+    chunk_dot_rows<FMT, R>(wj, xc, xs, nf4, nmask, nmagic, nmask_hi, d);
 #pragma unroll
     for (int i = 0; i < RPR; ++i) {
       if (DUAL) {

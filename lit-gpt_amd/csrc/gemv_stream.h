@@ -100,20 +100,19 @@ __device__ __forceinline__ void gemv_q4_stream(GemvArgs a, unsigned char* smem) 
         d[q] = pack2(__fmul_rn(bflo(nw[q]), __fmul_rn(bflo(d[q]), rs)),
                      __fmul_rn(bfhi(nw[q]), __fmul_rn(bfhi(d[q]), rs)));
     }
-    float cs = ((bflo(d[0]) + bfhi(d[0])) + (bflo(d[1]) + bfhi(d[1]))) +
-               ((bflo(d[2]) + bfhi(d[2])) + (bflo(d[3]) + bfhi(d[3])));
+    uint4 xv;
+    float cs = stage_x8<FMT>(d, xv);
     cs += __shfl_xor(cs, 1);
     cs += __shfl_xor(cs, 2);
     if (u < n8) {
-      xl[u] = make_uint4(__builtin_amdgcn_perm(d[2], d[0], 0x05040100u), __builtin_amdgcn_perm(d[2], d[0], 0x07060302u),
-                         __builtin_amdgcn_perm(d[3], d[1], 0x05040100u), __builtin_amdgcn_perm(d[3], d[1], 0x07060302u));
+      xl[u] = xv;
       if ((u & 3) == 0) xsum[u >> 2] = cs;
     }
   }
   __syncthreads();
 
   // 4. tile loop: dot + butterfly + epilogue of tile k, then issue tile k + 2 into the freed buffer
-  const uint32_t nmask = nibble_mask(), nmagic = bf16_magic();
+  const uint32_t nmask = nibble_mask(), nmagic = f16_magic(), nmask_hi = nibble_mask_hi();
   auto consume = [&](const Tile& b, int tile) {
     float part[R];
 #pragma unroll
@@ -127,7 +126,7 @@ __device__ __forceinline__ void gemv_q4_stream(GemvArgs a, unsigned char* smem) 
 #pragma unroll
       for (int r = 0; r < R; ++r) wj[r] = b.w[r][j];
       float d[R];
-      chunk_dot_rows<FMT, R>(wj, xl + cc * 4, xsum[cc], nf4, nmask, nmagic, d);
+      chunk_dot_rows<FMT, R>(wj, xl + cc * 4, xsum[cc], nf4, nmask, nmagic, nmask_hi, d);
 #pragma unroll
       for (int r = 0; r < R; ++r) part[r] = fmaf(ok ? scale_of<FMT>(b.s[r][j]) : 0.0f, d[r], part[r]);
     }
