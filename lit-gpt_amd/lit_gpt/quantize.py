@@ -21,6 +21,7 @@ Group sizes must divide in_features; for a TP row-shard whose width is not a mul
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -76,6 +77,26 @@ def _fit_group(K: int, group: int) -> int:
 # layer: 0.21 vs 0.44 ms at M = 64, 0.63 vs 1.04 ms at M = 2048; gemm.hip's 128-row tiles idle most CUs below M = 256)
 DEQUANT_GEMM_MIN_M = 16
 _SCRATCH: dict = {}
+
+
+# Prefill weight cache: a Linear keeps the bf16 weight its first long prefill dequantized (the same bits
+# lga_q4_dequantize writes every time) and later prefills skip the dequantize pass — 0.13 ms of HBM-bound work per
+# Llama-2-7B layer, the largest non-GEMM cost of a warm 2048-token prefill. Decode keeps streaming the packed 4-bit
+# weights. Costs 2 bytes per weight of HBM: 13 GB for Llama-2-7B of an MI355X's 288 GB, so it is bounded per device
+# by PREFILL_CACHE_FRACTION of the device memory and by what is free (keeping PREFILL_CACHE_HEADROOM free); a Linear
+# that does not fit dequantizes into the shared scratch as before. LGA_PREFILL_CACHE=0 turns it off.
+PREFILL_CACHE = os.environ.get("LGA_PREFILL_CACHE", "1") != "0"
+PREFILL_CACHE_FRACTION = 0.25
+PREFILL_CACHE_HEADROOM = 16 << 30
+_CACHED_BYTES: dict = {}
+
+
+def _cache_admits(nbytes: int, device: torch.device) -> bool:
+    if not PREFILL_CACHE:
+        return False
+    free, total = torch.cuda.mem_get_info(device)
+    used = _CACHED_BYTES.get(device, 0)
+    return used + nbytes <= PREFILL_CACHE_FRACTION * total and free - nbytes >= PREFILL_CACHE_HEADROOM
 
 
 def _dequant_scratch(numel: int, device: torch.device) -> torch.Tensor:
@@ -147,13 +168,31 @@ class QuantLinear(nn.Module):
                 # long prefill: dequantize to bf16 once (bnb's dequantize_4bit, the reference's own M > 1 path),
                 # then the library bf16 GEMM (hipBLASLt): 1.1-1.25 PFLOP/s vs 0.5-0.7 for the fused int4 GEMM at
                 # M = 2048, the dequantize pass included (tools/gemm_rates.py)
-                w = ops.q4_dequantize(self.qweight, self.scales, self.out_features, self.in_features, self.group,
-                                      self.fmt, out=_dequant_scratch(self.out_features * self.in_features, x2.device))
-                y = ops.bf16_gemm(x2, w, bias=self.bias, residual=res)
+                y = ops.bf16_gemm(x2, self._prefill_weight(x2.device), bias=self.bias, residual=res)
             else:
                 y = ops.q4_gemm(x2, self.qweight, self.scales, self.out_features, self.in_features, self.group,
                                 self.fmt, bias=self.bias, residual=res)
         return y.view(*lead, self.out_features)
+
+    def _prefill_weight(self, device: torch.device) -> torch.Tensor:
+        """bf16(dequant(W)) for the library GEMM: the cached copy when it is current (same packed weights and
+        scales as when it was made), else a fresh dequantize — into a cache buffer if the device budget admits one,
+        into the shared scratch otherwise."""
+        key = (self.qweight.data_ptr(), self.qweight._version, self.scales.data_ptr(), self.scales._version)
+        cached = getattr(self, "_w_bf16", None)
+        if cached is not None and self._w_key == key:
+            return cached
+        if cached is not None:  # weights changed in place (e.g. load_state_dict): drop the stale copy
+            _CACHED_BYTES[cached.device] = _CACHED_BYTES.get(cached.device, 0) - cached.numel() * 2
+            self._w_bf16 = None
+        N, K = self.out_features, self.in_features
+        if _cache_admits(N * K * 2, device):
+            out = torch.empty(N, K, dtype=torch.bfloat16, device=device)
+            _CACHED_BYTES[device] = _CACHED_BYTES.get(device, 0) + N * K * 2
+            self._w_bf16, self._w_key = out, key
+        else:
+            out = _dequant_scratch(N * K, device)
+        return ops.q4_dequantize(self.qweight, self.scales, N, K, self.group, self.fmt, out=out)
 
     def forward_attn(self, partials: torch.Tensor, n_splits: int, head_size: int, *,
                      residual: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -198,6 +198,36 @@ def test_dequantize_then_bf16_gemm_is_q4_gemm(ops, fmt, group, M, N, K):
     assert np.max(np.abs(y - exp) - (np.abs(exp) + np.abs(h)) * 2 ** -7) <= 2e-3
 
 
+def test_prefill_weight_cache(ops, monkeypatch):
+    """QuantLinear's prefill weight cache: the cached bf16 weight is the dequantized weight bit for bit, later
+    prefills reuse it (same output as the uncached path), and an in-place weight change (load_state_dict's copy_)
+    invalidates it."""
+    from lit_gpt import quantize as qz
+
+    N, K, M = 1024, 4096, 64
+    q1, s1 = ops.quantize(torch.from_numpy(_weights(N, K, "pc1")).to(DEV), 0, 128)
+    q2, s2 = ops.quantize(torch.from_numpy(_weights(N, K, "pc2")).to(DEV), 0, 128)
+    x = to_dev_bf16(synth.normal((M, K), "pcx", 5, 1.0))
+
+    def make(qw, sc):
+        lin = qz.QuantLinear(K, N, 0, 128, device=DEV)
+        lin.qweight.copy_(qw)
+        lin.scales.copy_(sc)
+        return lin
+
+    monkeypatch.setattr(qz, "PREFILL_CACHE", False)
+    ref1, ref2 = make(q1, s1)(x), make(q2, s2)(x)
+    monkeypatch.setattr(qz, "PREFILL_CACHE", True)
+    lin = make(q1, s1)
+    assert torch.equal(lin(x), ref1)
+    cached = lin._w_bf16
+    assert cached is not None and torch.equal(cached, ops.q4_dequantize(q1, s1, N, K, 128, 0))
+    assert torch.equal(lin(x), ref1) and lin._w_bf16 is cached  # reused, not re-made
+    lin.qweight.copy_(q2)
+    lin.scales.copy_(s2)
+    assert torch.equal(lin(x), ref2)
+
+
 # ------------------------------------------------------------------------------------------------ bf16 weights
 # BASELINE config 2: unquantized nn.Linear in bf16-true. Reference: fp64 product of the same bf16 x and W.
 @pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 11008), (32000, 4096), (1000, 256), (77, 1376), (40, 8),
