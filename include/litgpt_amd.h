@@ -192,6 +192,11 @@ int lga_allreduce_bf16(const void* x, const void* residual, void* y, int n, void
  *    writes the token (int32) and advances *pos_inout by one (generate/base.py:92) -------------------------- */
 int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
                lga_stream_t stream);
+/* lga_argmax, then the same launch gathers row `token` of the embedding table (vocab x n_embd bf16) into emb_out
+ * (n_embd bf16): the next decode step's transformer.wte(idx) (lit_gpt/model.py:515, an nn.Embedding gather),
+ * bit-identical to lga_embedding of the token — one launch per step fewer. */
+int lga_argmax_embed(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
+                     const void* table, int n_embd, int vocab, void* emb_out, lga_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -27,10 +27,14 @@ __device__ __forceinline__ void take(float v, int i, float& bv, int& bi) {
 // comparing, so a 32000-entry vocabulary costs one memory round trip instead of one per element.
 constexpr int kVec = 8;
 
-template <bool VEC>
+// EMB: the same workgroup then gathers row `token` of the embedding table into emb_out — the next decode step's
+// transformer.wte(idx) (lit_gpt/model.py:515), so that step needs no embedding launch of its own.
+template <bool VEC, bool EMB = false>
 __global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict__ logits, int n,
                                                       int64_t* __restrict__ out_idx, int32_t* __restrict__ token_out,
-                                                      int64_t* __restrict__ pos_inout) {
+                                                      int64_t* __restrict__ pos_inout,
+                                                      const uint16_t* __restrict__ table = nullptr, int C = 0,
+                                                      int V = 0, uint16_t* __restrict__ emb_out = nullptr) {
   float bv = -INFINITY;
   int bi = 0x7FFFFFFF;
   int done = 0;
@@ -65,6 +69,7 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict
   }
   __shared__ float sv[16];
   __shared__ int si[16];
+  __shared__ int s_tok;
   const int wave = threadIdx.x >> 6;
   if ((threadIdx.x & 63) == 0) {
     sv[wave] = bv;
@@ -78,6 +83,13 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict
     if (out_idx) *out_idx = bi;
     if (token_out) *token_out = bi;
     if (pos_inout) *pos_inout += 1;
+    s_tok = bi;
+  }
+  if (EMB) {
+    __syncthreads();
+    const long id = min(max(s_tok, 0), V - 1);  // as lga_embedding: the gather stays in bounds
+    const uint4* src = (const uint4*)(table + (size_t)id * C);
+    for (int i = threadIdx.x; i < C / 8; i += blockDim.x) ((uint4*)emb_out)[i] = src[i];
   }
 }
 
@@ -90,5 +102,20 @@ extern "C" int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* 
     lga::argmax_kernel<true><<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, out_idx, token_out, pos_inout);
   else
     lga::argmax_kernel<false><<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, out_idx, token_out, pos_inout);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_argmax_embed(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
+                                const void* table, int n_embd, int vocab, void* emb_out, hipStream_t stream) {
+  LGA_CHECK_ARG(logits && n > 0 && table && emb_out && n_embd > 0 && n_embd % 8 == 0 && vocab > 0,
+                "lga_argmax_embed: bad arguments");
+  LGA_CHECK_ARG(((uintptr_t)table & 15) == 0 && ((uintptr_t)emb_out & 15) == 0,
+                "lga_argmax_embed: table and emb_out must be 16-B aligned");
+  if (((uintptr_t)logits & 15) == 0 && n >= 8)
+    lga::argmax_kernel<true, true><<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, out_idx, token_out, pos_inout,
+                                                           (const uint16_t*)table, n_embd, vocab, (uint16_t*)emb_out);
+  else
+    lga::argmax_kernel<false, true><<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, out_idx, token_out, pos_inout,
+                                                            (const uint16_t*)table, n_embd, vocab, (uint16_t*)emb_out);
   LGA_LAUNCH_RETURN();
 }

@@ -149,9 +149,11 @@ class GPT(nn.Module):
         return self.cos, self.sin
 
     def forward(self, idx: torch.Tensor, input_pos: Optional[torch.Tensor] = None, *,
-                last_token_only: bool = False) -> torch.Tensor:
+                last_token_only: bool = False, embedded: Optional[torch.Tensor] = None) -> torch.Tensor:
         """(B=1, T) ids -> (1, T, padded_vocab) logits; ``last_token_only`` computes only the last row (1, 1, V)
-        — all that ``generate`` samples from (generate/base.py:31)."""
+        — all that ``generate`` samples from (generate/base.py:31). ``embedded`` (T * n_embd bf16) is
+        ``transformer.wte(idx)`` already gathered — by the previous decode step's ``ops.argmax_embed`` in
+        ``DecodeGraph`` — and replaces the embedding launch."""
         B, T = idx.shape
         if self.max_seq_length < T:
             raise ValueError(f"Cannot forward sequence of length {T}, max seq length is only {self.max_seq_length}.")
@@ -164,7 +166,12 @@ class GPT(nn.Module):
         cos, sin = self._rope_tables()
         if input_pos is not None:
             input_pos = input_pos.to(device=idx.device, dtype=torch.int64).contiguous()
-        x = ops.embedding(idx.reshape(-1).contiguous(), self.transformer.wte.weight).view(1, T, -1)
+        if embedded is not None:
+            if embedded.numel() != T * self.config.n_embd or embedded.dtype != torch.bfloat16:
+                raise ValueError("embedded must hold T * n_embd bf16 values (the gathered wte rows of idx)")
+            x = embedded.view(1, T, -1)
+        else:
+            x = ops.embedding(idx.reshape(-1).contiguous(), self.transformer.wte.weight).view(1, T, -1)
         for block in self.transformer.h:
             x = block(x, cos, sin, None, input_pos)
         if last_token_only:

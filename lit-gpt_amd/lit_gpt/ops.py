@@ -60,6 +60,7 @@ SIGNATURES = {
     "lga_attention_decode_fused": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_attention_decode_split": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_argmax": [_P, _I, _P, _P, _P, _P],
+    "lga_argmax_embed": [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P],
     "lga_moe_route": [_P, _I, _I, _I, _P, _P, _P],
     "lga_q4_gemv_experts": [_P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _I, _P, _I, _I, _I, _I,
                             _I, _P],
@@ -466,6 +467,21 @@ def argmax(logits, out_idx=None, token_out=None, pos_inout=None):
     _check(load_library().lga_argmax(_dev(logits, "logits", torch.bfloat16), n, _dev(idx, "out_idx", torch.int64),
                                      _opt(token_out, "token_out", torch.int32),
                                      _opt(pos_inout, "pos_inout", torch.int64), _stream()))
+    return idx
+
+
+def argmax_embed(logits, table, emb_out, out_idx=None, token_out=None, pos_inout=None):
+    """argmax (as ``argmax``) + the embedding row of the chosen token written to ``emb_out`` (n_embd,) bf16 in
+    the same launch (the next decode step's input)."""
+    n = logits.numel()
+    V, C = table.shape
+    if emb_out.numel() != C:
+        raise ValueError(f"argmax_embed: emb_out holds {emb_out.numel()} elements, the table rows {C}")
+    idx = out_idx if out_idx is not None else torch.empty(1, dtype=torch.int64, device=logits.device)
+    _check(load_library().lga_argmax_embed(_dev(logits, "logits", torch.bfloat16), n, _dev(idx, "out_idx", torch.int64),
+                                           _opt(token_out, "token_out", torch.int32),
+                                           _opt(pos_inout, "pos_inout", torch.int64), _dev(table, "table", torch.bfloat16),
+                                           C, V, _dev(emb_out, "emb_out", torch.bfloat16), _stream()))
     return idx
 
 

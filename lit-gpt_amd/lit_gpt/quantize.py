@@ -178,7 +178,10 @@ class QuantLinear(nn.Module):
         """bf16(dequant(W)) for the library GEMM: the cached copy when it is current (same packed weights and
         scales as when it was made), else a fresh dequantize — into a cache buffer if the device budget admits one,
         into the shared scratch otherwise."""
-        key = (self.qweight.data_ptr(), self.qweight._version, self.scales.data_ptr(), self.scales._version)
+        try:
+            key = (self.qweight.data_ptr(), self.qweight._version, self.scales.data_ptr(), self.scales._version)
+        except RuntimeError:  # inference tensors keep no version counter: an in-place change would go unseen
+            key = None
         cached = getattr(self, "_w_bf16", None)
         if cached is not None and self._w_key == key:
             return cached
@@ -186,7 +189,7 @@ class QuantLinear(nn.Module):
             _CACHED_BYTES[cached.device] = _CACHED_BYTES.get(cached.device, 0) - cached.numel() * 2
             self._w_bf16 = None
         N, K = self.out_features, self.in_features
-        if _cache_admits(N * K * 2, device):
+        if key is not None and _cache_admits(N * K * 2, device):
             out = torch.empty(N, K, dtype=torch.bfloat16, device=device)
             _CACHED_BYTES[device] = _CACHED_BYTES.get(device, 0) + N * K * 2
             self._w_bf16, self._w_key = out, key

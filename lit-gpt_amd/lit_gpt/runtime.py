@@ -5,8 +5,9 @@ The reference gets launch-overhead relief from ``torch.compile(next_token, mode=
 chain of hand-written HIP kernels (per layer: fused RMSNorm+qkv GEMV, RoPE+KV append, split attention +
 combine, proj GEMV+residual, fused RMSNorm+SwiGLU GEMV, down GEMV+residual; then RMSNorm+lm_head GEMV and
 argmax). ``DecodeGraph`` captures that chain once with static input buffers — the token id and ``input_pos``
-live on the device, the argmax kernel writes the next token and advances ``input_pos`` — so a decode step is a
-single ``hipGraphLaunch`` with no host<->device synchronisation (or, with ``chunk``, several steps are).
+live on the device, the argmax kernel writes the next token, advances ``input_pos`` and gathers the token's
+embedding row for the next step (so the step has no embedding launch) — so a decode step is a single
+``hipGraphLaunch`` with no host<->device synchronisation (or, with ``chunk``, several steps are).
 """
 
 from __future__ import annotations
@@ -31,6 +32,12 @@ class DecodeGraph:
         self.pos = torch.tensor([first_pos], dtype=torch.int64, device=dev)
         self.chunk = max(1, int(chunk))
         self.history = torch.zeros(self.chunk, dtype=torch.int64, device=dev)
+        # the argmax launch also gathers the new token's embedding row (ops.argmax_embed) into x_emb, which the
+        # next step's forward takes instead of running its own embedding launch
+        wte = model.transformer.wte.weight
+        self.fuse_embedding = (wte.is_cuda and wte.dtype == torch.bfloat16 and wte.is_contiguous()
+                               and wte.shape[1] % 8 == 0)
+        self.x_emb = torch.empty(wte.shape[1], dtype=torch.bfloat16, device=dev) if self.fuse_embedding else None
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.chunk_graph: Optional[torch.cuda.CUDAGraph] = None
         self._step_eager()
@@ -46,12 +53,17 @@ class DecodeGraph:
                     self._step_body(self.history[i:i + 1])
             self.chunk_graph = gc
 
-    def _step_body(self, idx_out: Optional[torch.Tensor] = None) -> None:
-        logits = self.model(self.token, self.pos, last_token_only=True)
-        ops.argmax(logits.reshape(-1), out_idx=idx_out, token_out=self.token.view(-1), pos_inout=self.pos)
+    def _step_body(self, idx_out: Optional[torch.Tensor] = None, embedded: bool = True) -> None:
+        if not self.fuse_embedding:
+            logits = self.model(self.token, self.pos, last_token_only=True)
+            ops.argmax(logits.reshape(-1), out_idx=idx_out, token_out=self.token.view(-1), pos_inout=self.pos)
+            return
+        logits = self.model(self.token, self.pos, last_token_only=True, embedded=self.x_emb if embedded else None)
+        ops.argmax_embed(logits.reshape(-1), self.model.transformer.wte.weight, self.x_emb, out_idx=idx_out,
+                         token_out=self.token.view(-1), pos_inout=self.pos)
 
     def _step_eager(self) -> None:
-        self._step_body()
+        self._step_body(embedded=False)  # embeds first_token itself; its argmax leaves x_emb for the graphs
 
     def step(self) -> torch.Tensor:
         """One decode step; returns the (device) token buffer holding the new token."""

@@ -516,6 +516,39 @@ def test_argmax_matches_torch_random(ops, n, offset):
     assert ops.argmax(neg.to(DEV)).item() == 0
 
 
+@pytest.mark.parametrize("n,offset", [(32000, 0), (1001, 1), (7, 0)])
+def test_argmax_embed_is_argmax_then_embedding(ops, n, offset):
+    """lga_argmax_embed == lga_argmax followed by lga_embedding of the chosen token: same token, same token /
+    position bookkeeping, the same embedding row bit for bit (ties, NaN, and a token past the table clamp as the
+    embedding does)."""
+    C = 4096
+    V = max(n - 3, 1)  # the last logits index past the table: clamped to row V - 1 like lga_embedding
+    table = to_dev_bf16(synth.normal((V, C), "aemb", 5, 1.0))
+    g = torch.Generator().manual_seed(n)
+    x = (torch.randint(-50, 50, (n + offset,), generator=g).float() / 4).bfloat16()
+    cases = [x]
+    if n > 3:
+        x2 = x.clone()
+        x2[offset + n // 3] = float("nan")
+        cases.append(x2)
+        x3 = x.clone()
+        x3[offset + n - 1] = 100.0  # winner beyond the table's last row
+        cases.append(x3)
+    for xc in cases:
+        lg = xc.to(DEV)[offset:]
+        tok_a = torch.zeros(1, dtype=torch.int32, device=DEV)
+        pos_a = torch.tensor([7], device=DEV)
+        ia = ops.argmax(lg, token_out=tok_a, pos_inout=pos_a)
+        emb_a = ops.embedding(tok_a, table).view(-1)
+        tok_b = torch.zeros(1, dtype=torch.int32, device=DEV)
+        pos_b = torch.tensor([7], device=DEV)
+        emb_b = torch.empty(C, dtype=torch.bfloat16, device=DEV)
+        ib = ops.argmax_embed(lg, table, emb_b, token_out=tok_b, pos_inout=pos_b)
+        assert ia.item() == ib.item() == int(torch.argmax(xc[offset:].float()))
+        assert tok_a.item() == tok_b.item() and pos_a.item() == pos_b.item() == 8
+        assert torch.equal(emb_a, emb_b)
+
+
 def test_embedding_and_add(ops):
     V, C = 500, 256
     table = bf16_np(synth.normal((V, C), "emb", 5, 1.0))
