@@ -354,7 +354,7 @@ def main():
     from functools import partial
 
     model = build_model(cfg, quantize=None if dense else args.quantize, device=dev, max_seq_length=max_seq,
-                        fabric=fabric if world > 1 else None)
+                        fabric=fabric if world > 1 else None, prefill_rows=T)
     load_s = time.perf_counter() - t0
     g = torch.Generator(device="cpu").manual_seed(1234)
     prompt = torch.randint(0, cfg.vocab_size, (T,), generator=g, dtype=torch.int32).to(dev)

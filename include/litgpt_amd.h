@@ -78,6 +78,11 @@ int lga_q4_dequantize(const uint8_t* qweight, const void* scales, void* w, int N
  * `workspace` (may be NULL) of `workspace_bytes` is caller-owned scratch for split-K algorithms. */
 int lga_gemm_bf16_blaslt(const void* x, const void* weight, const void* bias, const void* residual, void* y, int M,
                          int N, int K, void* workspace, size_t workspace_bytes, lga_stream_t stream);
+/* The same GEMM, and the (M, N, K, bias, workspace) plan is tuned: hipBLASLt's top heuristic candidates are timed
+ * on these operands and the fastest is kept for every later lga_gemm_bf16_blaslt of the shape (synchronises the
+ * stream; call at load, outside graph capture). */
+int lga_gemm_bf16_blaslt_tune(const void* x, const void* weight, const void* bias, const void* residual, void* y,
+                              int M, int N, int K, void* workspace, size_t workspace_bytes, lga_stream_t stream);
 
 /* -- unquantized bf16 Linears (BASELINE config 2: no --quantize, precision bf16-true; the reference runs
  *    F.linear on the bf16 nn.Linear weight, lit_gpt/model.py:619, :656, :712-716, :519) ------------------- */

@@ -113,7 +113,7 @@ def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temp
 
 def build_model(config: Config, *, quantize: Optional[str], device: torch.device, seed: int = 1234,
                 checkpoint_path: Optional[Path] = None, max_seq_length: Optional[int] = None,
-                fabric=None, rope_positions: str = "reference") -> GPT:
+                fabric=None, rope_positions: str = "reference", prefill_rows: Optional[int] = None) -> GPT:
     """Instantiate on the meta device, then materialise (load, or random-init as GPT._init_weights) the float
     weights on the GPU in the model's parameter order; with ``fabric`` (world_size / global_rank, generate/tp.py)
     every block is sharded (``tensor_parallel_block``) and quantized as soon as its weights exist, so a rank holds
@@ -123,7 +123,9 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
 
     ``rope_positions="reference"`` builds the rope tables under a bf16 default dtype, as the reference's
     ``with fabric.init_tensor(): model.max_seq_length = ...`` does under bf16-true / bnb precision
-    (generate/base.py:153-157): positions above 256 round to bf16. ``"exact"`` keeps fp32 positions."""
+    (generate/base.py:153-157): positions above 256 round to bf16. ``"exact"`` keeps fp32 positions.
+    ``prefill_rows``: the prompt length about to be served — its prefill GEMM plans are tuned at load
+    (ops.tune_prefill_gemms)."""
     if rope_positions not in ("reference", "exact"):
         raise ValueError(f"rope_positions must be 'reference' or 'exact', got {rope_positions!r}")
     from lit_gpt.quantize import QuantizedPrecision
@@ -199,6 +201,8 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
     from lit_gpt import ops
 
     ops.warm_gemm_library(device, K=config.n_embd)
+    if prefill_rows:  # the served prompt length is known: tune its prefill GEMMs now, not in the first prompt
+        ops.tune_prefill_gemms(model, prefill_rows)
     return model.eval()
 
 
@@ -232,7 +236,7 @@ def main(prompt: str = "What food do llamas eat?", *, num_samples: int = 1, max_
     print(f"Loading model {str(checkpoint_path or synthetic)!r} with {config.__dict__}", file=sys.stderr)
     t0 = time.perf_counter()
     model = build_model(config, quantize=quantize, device=device, checkpoint_path=checkpoint_path,
-                        max_seq_length=max_returned_tokens)
+                        max_seq_length=max_returned_tokens, prefill_rows=prompt_length)
     print(f"Time to load the model weights: {time.perf_counter() - t0:.02f} seconds.", file=sys.stderr)
     torch.manual_seed(1234)
     eos_id = tokenizer.eos_id if tokenizer is not None else None

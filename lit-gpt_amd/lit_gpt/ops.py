@@ -48,6 +48,7 @@ SIGNATURES = {
     "lga_bf16_gemv_attn": [_P, _I, _I, _P, _P, _P, _P, _I, _I, _P],
     "lga_bf16_gemm": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lga_gemm_bf16_blaslt": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P],
+    "lga_gemm_bf16_blaslt_tune": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P],
     "lga_rmsnorm": [_P, _P, _P, _I, _I, _F, _P],
     "lga_rope_kv_append": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lga_embedding": [_P, _I, _P, _P, _I, _I, _I, _P],
@@ -255,6 +256,38 @@ def warm_gemm_library(device, K: int = 4096) -> None:
     not pay the library's start-up."""
     x = torch.zeros(LIB_GEMM_MIN_M, K, dtype=torch.bfloat16, device=device)
     bf16_gemm(x, torch.zeros(64, K, dtype=torch.bfloat16, device=device), impl="blaslt")
+
+
+def tune_prefill_gemms(model, rows: int) -> int:
+    """Tune the hipBLASLt plan of every distinct (N, K, bias) prefill GEMM of ``model``'s blocks for ``rows``-token
+    prompts (lga_gemm_bf16_blaslt_tune on random operands of that shape), so the first prompt of that length runs
+    the fastest candidate without paying the search. Returns the number of shapes tuned; no-op below
+    LIB_GEMM_MIN_M rows (those prompts do not reach hipBLASLt)."""
+    if rows < LIB_GEMM_MIN_M:
+        return 0
+    shapes = set()
+    for name, mod in model.named_modules():
+        if name.endswith("lm_head") or not hasattr(mod, "in_features") or not hasattr(mod, "out_features"):
+            continue  # lm_head sees one row in a prefill (last_token_only)
+        if mod.out_features % 8 or mod.in_features % 8:
+            continue
+        shapes.add((mod.out_features, mod.in_features, getattr(mod, "bias", None) is not None))
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ws = _GEMM_WS.get(dev)
+    if ws is None:
+        ws = _GEMM_WS[dev] = torch.empty(LIB_GEMM_WORKSPACE, dtype=torch.uint8, device=dev)
+    g = torch.Generator(device=dev).manual_seed(0)
+    for N, K, has_bias in sorted(shapes):
+        x = torch.randn(rows, K, generator=g, device=dev).to(torch.bfloat16)
+        w = (torch.randn(N, K, generator=g, device=dev) * 0.02).to(torch.bfloat16)
+        b = torch.zeros(N, dtype=torch.bfloat16, device=dev) if has_bias else None
+        y = torch.empty(rows, N, dtype=torch.bfloat16, device=dev)
+        _check(load_library().lga_gemm_bf16_blaslt_tune(
+            _dev(x, "x", torch.bfloat16), _dev(w, "weight", torch.bfloat16), _opt(b, "bias", torch.bfloat16), None,
+            _dev(y, "y", torch.bfloat16), rows, N, K, _dev(ws, "workspace", torch.uint8), ws.numel(), _stream()))
+        del x, w, y
+    torch.cuda.synchronize(dev)
+    return len(shapes)
 
 
 def bf16_gemm(x, weight, *, bias=None, residual=None, out=None, impl=None):

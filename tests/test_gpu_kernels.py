@@ -198,6 +198,30 @@ def test_dequantize_then_bf16_gemm_is_q4_gemm(ops, fmt, group, M, N, K):
     assert np.max(np.abs(y - exp) - (np.abs(exp) + np.abs(h)) * 2 ** -7) <= 2e-3
 
 
+def test_tuned_library_gemm(ops):
+    """A tuned hipBLASLt plan (lga_gemm_bf16_blaslt_tune: fastest of the heuristic's candidates on these operands)
+    is kept for the shape: later calls reproduce the tuning call's output bit for bit and stay within bf16 rounding
+    of the fp64 product; tune_prefill_gemms covers a model's block Linears."""
+    M, N, K = 1024, 1536, 4096
+    w = bf16_np(_weights(N, K, "tg"))
+    x = bf16_np(synth.normal((M, K), "tgx", 5, 1.0))
+    xd, wd = to_dev_bf16(x), to_dev_bf16(w)
+    ws = torch.empty(ops.LIB_GEMM_WORKSPACE, dtype=torch.uint8, device=DEV)
+    y0 = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops._check(ops.load_library().lga_gemm_bf16_blaslt_tune(xd.data_ptr(), wd.data_ptr(), None, None, y0.data_ptr(),
+                                                            M, N, K, ws.data_ptr(), ws.numel(), ops._stream()))
+    y1 = ops.bf16_gemm(xd, wd, impl="blaslt")
+    assert torch.equal(y0, y1)
+    h = _ref_linear(x, w)
+    assert np.max(np.abs(y1.float().cpu().numpy() - h) - np.abs(h) * 2 ** -7) <= 1e-3
+    from lit_gpt import GPT, Config
+
+    model = GPT(Config.from_name("Llama-2-7b-hf", n_layer=1, n_embd=256, n_head=4, n_query_groups=2,
+                                 intermediate_size=640, vocab_size=1000, padding_multiple=64))
+    assert ops.tune_prefill_gemms(model, 600) == 4  # qkv, attn.proj, fc_1 / fc_2 (one shape), mlp.proj
+    assert ops.tune_prefill_gemms(model, 8) == 0
+
+
 def test_prefill_weight_cache(ops, monkeypatch):
     """QuantLinear's prefill weight cache: the cached bf16 weight is the dequantized weight bit for bit, later
     prefills reuse it (same output as the uncached path), and an in-place weight change (load_state_dict's copy_)
