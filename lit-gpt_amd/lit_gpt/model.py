@@ -167,7 +167,7 @@ class GPT(nn.Module):
         if input_pos is not None:
             input_pos = input_pos.to(device=idx.device, dtype=torch.int64).contiguous()
         if embedded is not None:
-            if embedded.numel() != T * self.config.n_embd or embedded.dtype != torch.bfloat16:
+            if embedded.numel() != T * self.transformer.wte.weight.shape[1] or embedded.dtype != torch.bfloat16:
                 raise ValueError("embedded must hold T * n_embd bf16 values (the gathered wte rows of idx)")
             x = embedded.view(1, T, -1)
         else:
