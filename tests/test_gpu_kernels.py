@@ -336,6 +336,18 @@ def test_rmsnorm_matches_oracle(ops, golden):
     assert (y == ref).float().mean() > 0.97
 
 
+@pytest.mark.parametrize("rows,n", [(2048, 4096), (3, 8192), (5, 1000), (7, 4100), (2, 11008)])
+def test_rmsnorm_vector_and_scalar_forms(ops, rows, n):
+    """16-B form (n % 8 == 0, n <= 8192) and the scalar fallback (n = 4100, and 11008 > 8192) vs the oracle's
+    RMSNorm, one bf16 ulp (fp32 sums of squares in different orders)."""
+    x = torch.from_numpy(synth.normal((rows, n), f"rmx{n}", 5, 2.0)).bfloat16()
+    w = torch.from_numpy(1.0 + synth.normal((n,), f"rmw{n}", 5, 0.2)).bfloat16()
+    y = ops.rmsnorm(x.to(DEV), w.to(DEV), 1e-5).float().cpu()
+    ref = om.rms_norm(x, w, 1e-5).float()
+    assert torch.all((y - ref).abs() <= ref.abs() * 2 ** -7 + 1e-6)
+    assert (y == ref).float().mean() > 0.97
+
+
 @pytest.mark.parametrize("H,G,hs,n_elem", [(32, 32, 128, 128), (8, 2, 128, 128), (4, 1, 64, 64), (12, 12, 64, 16),
                                            (4, 2, 80, 20)])  # the last: scalar kernel (half not a multiple of 8)
 def test_rope_kv_append_bit_exact(ops, H, G, hs, n_elem):
