@@ -11,9 +11,12 @@ are resident in HBM before the timed region. Timed region: barrier + synchronize
 barrier; the max over ranks is reported.
 
 Extra objects in the JSON line:
-  roofline      the dominant kernel (fused RMSNorm + fc_1/fc_2 int4 GEMV + SwiGLU of one block, 46.5 MB of
-                algorithmic bytes per launch) timed with HIP events on the launch stream (all 32 blocks back to
-                back in a HIP graph); peak 8 TB/s; traffic = HBM bytes per launch from a rocprofv3 FETCH_SIZE pass
+  roofline      the dominant kernel = the one with the most device time per decode step, chosen in the run
+                between the decode attention (RoPE + KV append + split attention, K/V bytes at the timed
+                position) and the fused RMSNorm + fc_1/fc_2 int4 GEMV + SwiGLU (46.5 MB per launch); each is
+                timed with HIP events on the launch stream (all 32 blocks back to back in a HIP graph); peak
+                8 TB/s; traffic = HBM bytes per launch from a rocprofv3 FETCH_SIZE pass at the same position.
+                roofline_secondary = the other one
   step_roofline the whole decode step: algorithmic bytes per token (weights + KV read/write) x tok/s
   cpu_baseline  the CPU oracle (restatement of the reference's bf16 math) timed on this host on a bounded sample
 """
@@ -79,8 +82,7 @@ def prefill_flops(cfg, T: int, tp: int = 1) -> float:
     return L * (2.0 * T * per_tok + attn) + 2.0 * cfg.padded_vocab_size * C
 
 
-DOMINANT = ("gemv_q4s_kernel<.., DUAL> (streaming form: RMSNorm + fc_1/fc_2 int4 GEMV + SwiGLU of one block; the "
-            "largest per-step kernel)")
+DOMINANT = "gemv_q4s_kernel<.., DUAL> (streaming form: RMSNorm + fc_1/fc_2 int4 GEMV + SwiGLU of one block)"
 
 
 def time_attention(model, pos: int, replays: int = 5):
@@ -186,10 +188,11 @@ def time_dominant_kernel(model, replays: int = 5):
     return avg_ms, _dual_gemv_bytes(f1, C) * (2 if moe else 1)
 
 
-def pmc_child() -> None:
+def pmc_child(att_pos: int) -> None:
     """Run under `rocprofv3 --pmc FETCH_SIZE` by measure_traffic(): the fc_1||fc_2 GEMV at Llama-2-7B shape over
     24 distinct weight sets (1.1 GB, beyond the 256 MB Infinity Cache), one launch each, then the decode attention
-    over 24 distinct K/V caches."""
+    over 24 distinct K/V caches at position ``att_pos`` (the position time_attention() times, so traffic and
+    bytes_per_launch describe the same launch)."""
     from lit_gpt import ops
 
     C, N, copies = 4096, 11008, 24
@@ -209,8 +212,8 @@ def pmc_child() -> None:
     del sets
     # the decode attention over 24 distinct layers' K/V caches at the bench's last position (0.9 GB)
     H = G = 32
-    hs, S = 128, PROMPT_LEN + 256
-    pos = torch.tensor([PROMPT_LEN + 254], device=dev)
+    hs, S = 128, max(PROMPT_LEN + 256, att_pos + 2)
+    pos = torch.tensor([att_pos], device=dev)
     cos, sin = torch.ones(S, hs, device=dev), torch.zeros(S, hs, device=dev)
     qkv = torch.randn(1, (H + 2 * G) * hs, device=dev).to(torch.bfloat16)
     splits = ops.decode_splits(G, H // G, hs, S)
@@ -223,7 +226,7 @@ def pmc_child() -> None:
     torch.cuda.synchronize()
 
 
-def measure_traffic(timeout_s: float = 240.0):
+def measure_traffic(att_pos: int, timeout_s: float = 240.0):
     """HBM bytes per launch of the dominant kernel from the PMC counters, collected as MI355X_MICROARCH.md's HBM
     section prescribes: FETCH_SIZE (KiB, TCC_EA0_RDREQ x 64 B) in its own rocprofv3 pass, doubled (gfx950 tallies
     128-B requests of a 16-B/lane streaming read at 64 B). Runs in a child process started BEFORE this process
@@ -239,7 +242,7 @@ def measure_traffic(timeout_s: float = 240.0):
         return None, "rocprofv3 not found"
     out = Path(tempfile.mkdtemp(prefix="lga_pmc_"))
     cmd = [exe, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", str(out), "-o", "pmc", "--",
-           sys.executable, str(Path(__file__).resolve()), "--pmc-child"]
+           sys.executable, str(Path(__file__).resolve()), "--pmc-child", "--pmc-pos", str(att_pos)]
     try:
         subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=timeout_s, check=True)
         files = list(out.rglob("*counter_collection.csv"))
@@ -327,15 +330,17 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC pass for roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-pos", type=int, default=PROMPT_LEN + 254, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
-        return pmc_child()
+        return pmc_child(args.pmc_pos)
     traffic = {k: (None, "skipped") for k in ("gemv", "attention")}
     under_profiler = any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ)
     headline = args.model == MODEL and args.quantize == "int4-g128"
     dense = args.quantize in ("bf16", "none")
     if int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_traffic and not under_profiler and headline:
-        traffic = measure_traffic()  # before this process initialises the GPU
+        # before this process initialises the GPU; the attention at the position time_attention() uses below
+        traffic = measure_traffic(args.prompt_len + args.warmup + args.steps)
 
     import torch.distributed as dist
 
@@ -419,6 +424,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
+        gtp.comm.check_errors()  # TP: a timed-out xGMI all-reduce voids the run (raises on every rank)
         if world > 1:
             t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -429,10 +435,34 @@ def main():
         att_ms, att_bytes = time_attention(model, T + args.warmup + args.steps)
 
     cfg_full = Config.from_name(args.model)
+    pf_flops = prefill_flops(cfg_full, T, tp=world)
     mean_pos = T + args.warmup + 1 + (args.steps - 1) / 2
     step_bytes = algorithmic_bytes_per_token(cfg_full, mean_pos, tp=world, dense=dense)
     step_gbs = step_bytes * tok_s / 1e9
     kern_gbs = kbytes / (avg_ms * 1e-3) / 1e9
+    gemv_line = {"bound": "hbm", "kernel": (
+                 "gemv_bf16_kernel<.., DUAL> (RMSNorm + fc_1/fc_2 bf16 GEMV + SwiGLU of one block)" if dense else
+                 DOMINANT if not cfg._mlp_class == "LLaMAMoE" else
+                 "gemv_q4_kernel<.., DUAL> routed (RMSNorm + fc_1/fc_2 of 2 experts + SwiGLU of one block)"),
+                 "achieved": round(kern_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                 "frac": round(kern_gbs / HBM_PEAK_GBS, 4),
+                 "traffic": None if traffic["gemv"][0] is None else int(traffic["gemv"][0]),
+                 "traffic_note": traffic["gemv"][1],
+                 "bytes_per_launch": int(kbytes), "avg_launch_us": round(avg_ms * 1e3, 2),
+                 "us_per_step": round(avg_ms * 1e3 * cfg.n_layer, 1)}
+    att_line = None if att_ms is None else {
+        "bound": "hbm", "kernel": "attn_kernel<..,FUSED> (RoPE + KV append + split decode attention of one block)",
+        "achieved": round(att_bytes / (att_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "frac": round(att_bytes / (att_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": int(att_bytes),
+        "traffic": None if traffic["attention"][0] is None else int(traffic["attention"][0]),
+        "traffic_note": traffic["attention"][1], "avg_launch_us": round(att_ms * 1e3, 2),
+        "us_per_step": round(att_ms * 1e3 * cfg.n_layer, 1), "position": T + args.warmup + args.steps}
+    # the roofline object reports the kernel with the most device time per decode step (one launch per block
+    # each); the other one rides along as roofline_secondary
+    lines = sorted([l for l in (gemv_line, att_line) if l is not None], key=lambda l: -l["us_per_step"])
+    for l in lines:
+        l["note"] = ("the largest per-step kernel (most us per decode step)" if l is lines[0] else
+                     "second-largest per-step kernel")
     result = {
         "metric": ("decode tokens/s/GPU (Llama-2-7B int4, seq=2048) + % HBM roofline" if headline else
                    f"decode tokens/s/GPU ({args.model} {args.quantize}, seq={T}) + % HBM roofline"),
@@ -455,33 +485,22 @@ def main():
                    **({"graph_note": graph_note} if graph_note else {}),
                    **({"allreduce": "xgmi one-shot" if gtp.comm.get_default() is not None else
                        f"rccl ({gtp.comm.fallback_reason or 'LGA_TP_ALLREDUCE=rccl'})"} if world > 1 else {})},
-        "roofline": {"bound": "hbm", "kernel": (
-                     "gemv_bf16_kernel<.., DUAL> (RMSNorm + fc_1/fc_2 bf16 GEMV + SwiGLU of one block)" if dense else
-                     DOMINANT if not cfg._mlp_class == "LLaMAMoE" else
-                     "gemv_q4_kernel<.., DUAL> routed (RMSNorm + fc_1/fc_2 of 2 experts + SwiGLU of one block)"),
-                     "achieved": round(kern_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(kern_gbs / HBM_PEAK_GBS, 4),
-                     "traffic": None if traffic["gemv"][0] is None else int(traffic["gemv"][0]),
-                     "traffic_note": traffic["gemv"][1],
-                     "bytes_per_launch": int(kbytes), "avg_launch_us": round(avg_ms * 1e3, 2)},
-        "roofline_attention": None if att_ms is None else {
-            "bound": "hbm", "kernel": "attn_kernel<..,FUSED> (RoPE + KV append + split decode attention of one block)",
-            "achieved": round(att_bytes / (att_ms * 1e-3) / 1e9, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(att_bytes / (att_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bytes_per_launch": int(att_bytes),
-            "traffic": None if traffic["attention"][0] is None else int(traffic["attention"][0]),
-            "traffic_note": traffic["attention"][1], "avg_launch_us": round(att_ms * 1e3, 2),
-            "position": T + args.warmup + args.steps},
+        "roofline": lines[0],
+        "roofline_secondary": lines[1] if len(lines) > 1 else None,
         "step_roofline": {"bytes_per_token": int(step_bytes), "achieved": round(step_gbs, 1),
                           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(step_gbs / HBM_PEAK_GBS, 4),
                           "roofline_tokens_per_s": round(HBM_PEAK_GBS * 1e9 / step_bytes, 1)},
         "prefill_s": round(prefill_s, 4),
-        "prefill_roofline": {"bound": "mfma", "flops": prefill_flops(cfg_full, T, tp=world),
-                             "seconds": round(prefill_warm_s, 5),
-                             "achieved": round(prefill_flops(cfg_full, T, tp=world) / prefill_warm_s / 1e12, 1),
+        "prefill_roofline": {"bound": "mfma", "flops": pf_flops,
+                             "seconds": round(prefill_s, 5),
+                             "achieved": round(pf_flops / prefill_s / 1e12, 1),
                              "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                             "frac": round(prefill_flops(cfg_full, T, tp=world) / prefill_warm_s / 1e12
-                                           / MFMA_BF16_PEAK_TFLOPS, 4),
-                             "note": "whole warm prefill (GEMMs + flash attention + norms), wall clock"},
+                             "frac": round(pf_flops / prefill_s / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+                             "warm_seconds": round(prefill_warm_s, 5),
+                             "warm_frac": round(pf_flops / prefill_warm_s / 1e12 / MFMA_BF16_PEAK_TFLOPS, 4),
+                             "note": "the FIRST (cold) prefill of the process, wall clock, the one reference-style "
+                                     "tok/s counts: every Linear's int4 weights dequantized inside the GEMM, "
+                                     "flash attention, norms; warm_* = the same prompt again"},
         "reference_style_tokens_per_s": round((args.steps + args.warmup + 1) / (prefill_s + elapsed * (
             args.steps + args.warmup + 1) / args.steps), 2),
         "load_s": round(load_s, 2),

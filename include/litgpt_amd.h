@@ -58,12 +58,6 @@ int lga_q4_gemv(const void* x, const uint8_t* qweight, const void* scales, const
 int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const void* scales1, const uint8_t* qweight2,
                        const void* scales2, const void* norm_weight, float norm_eps, void* y, int N, int K,
                        int group, int fmt, int variant, lga_stream_t stream);
-/* Attention out-projection (CausalSelfAttention.proj, lit_gpt/model.py:656) whose activation is merged in the
- * prologue from the split partials of lga_attention_decode_split (the SDPA output, model.py:651, rounded to bf16
- * once — bit-identical to lga_attention_decode_fused + lga_q4_gemv): K = n_head * head_size. */
-int lga_q4_gemv_attn(const float* partials, int n_splits, int head_size, const uint8_t* qweight, const void* scales,
-                     const void* bias, const void* residual, void* y, int N, int K, int group, int fmt, int variant,
-                     lga_stream_t stream);
 
 /* -- prefill GEMM, M > 1 (bnb dequantize_4bit + cuBLAS GEMM) -------------------------------------------- */
 int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const void* bias, const void* residual,
@@ -92,9 +86,6 @@ int lga_bf16_gemv(const void* x, const void* weight, const void* bias, const voi
 /* y = bf16(silu(bf16(x W1^T))) * bf16(x W2^T) (LLaMAMLP, model.py:715), optional fused RMSNorm of x */
 int lga_bf16_gemv_swiglu(const void* x, const void* weight1, const void* weight2, const void* norm_weight,
                          float norm_eps, void* y, int N, int K, lga_stream_t stream);
-/* bf16 form of lga_q4_gemv_attn */
-int lga_bf16_gemv_attn(const float* partials, int n_splits, int head_size, const void* weight, const void* bias,
-                       const void* residual, void* y, int N, int K, lga_stream_t stream);
 /* prefill GEMM Y (M, N) = X (M, K) . W (N, K)^T [+bias] [+residual] on MFMA; K % 32 == 0 */
 int lga_bf16_gemm(const void* x, const void* weight, const void* bias, const void* residual, void* y, int M, int N,
                   int K, lga_stream_t stream);
@@ -144,14 +135,6 @@ int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, co
                                const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, void* y,
                                float* workspace, unsigned* counters, int n_head, int n_query_groups, int head_size,
                                int rope_n_elem, int max_seq, int n_splits, float scale, lga_stream_t stream);
-/* The same decode attention without the in-launch split merge: every split writes its (m, l, o) to `partials`
- * (lga_attention_workspace_bytes(1, H, hs, n_splits) bytes; per head row h and split s, hs + 4 floats at
- * (h * n_splits + s) * (hs + 4): max score, sum of exp, -, -, unnormalised output) for lga_q4_gemv_attn /
- * lga_bf16_gemv_attn to merge. No counters; caches as lga_attention_decode_fused. */
-int lga_attention_decode_split(const void* qkv, void* k_cache, void* v_cache, const int64_t* cache_pos,
-                               const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows,
-                               float* partials, int n_head, int n_query_groups, int head_size, int rope_n_elem,
-                               int max_seq, int n_splits, float scale, lga_stream_t stream);
 
 /* -- sparse MoE (LLaMAMoE.forward, lit_gpt/model.py:727-743; Mixtral) ------------------------------------------
  * lga_moe_route: per token row of router logits [T][n_expert] bf16 -> expert_ids [T][k] int32 and probs [T][k]

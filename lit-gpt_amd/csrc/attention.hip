@@ -15,9 +15,6 @@
 // With splits > 1 every workgroup publishes (m, l, o) write-through (sc1) and bumps a per-(t, group) counter;
 // the workgroup that arrives last merges the splits and writes the bf16 output (flash-decoding combine inside
 // the same launch; MI355X_MICROARCH.md "Valid forms" row 1), then re-arms the counter for the next launch.
-// lga_attention_decode_split instead stops after the per-split (m, l, o) (plain stores): the out-projection GEMV
-// merges them while its weights stream (gemv_body.h xpart_*), which takes the publish -> counter -> combine round
-// trips (~4 us per launch at Llama-2-7B decode) off the step's critical path.
 #include "decode_ops.h"
 
 namespace lga {
@@ -57,15 +54,13 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
                                                    uint16_t* __restrict__ y, float* __restrict__ ws,
                                                    unsigned* __restrict__ cnt, int n_head, int max_seq, float scale,
                                                    const int64_t* __restrict__ rope_pos, const float* __restrict__ cos,
-                                                   const float* __restrict__ sin, int rope_rows, int part_only) {
+                                                   const float* __restrict__ sin, int rope_rows) {
   constexpr int LPR = HS / 8;    // lanes per key row
   constexpr int RGW = 64 / LPR;  // row groups per wave
   constexpr int RG = NW * RGW;   // row groups per workgroup
   constexpr int NT = NW * 64;
   const int split = blockIdx.x, g = blockIdx.y, t = blockIdx.z;
   const int n_splits = gridDim.x, G = gridDim.y;
-  // partials-only launch (workspace, no counters): every split leaves its (m, l, o) for the out-projection GEMV,
-  // which merges them in its activation prologue (lga_q4_gemv_attn / lga_bf16_gemv_attn) — no in-launch combine
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int rg = wave * RGW + lane / LPR;
   const int sub = lane % LPR;
@@ -238,11 +233,7 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
       lt += sl[w][h] * c;
       ot += so[w][h][d] * c;
     }
-    if (part_only) {  // (m, l, o) of this split for the consumer GEMV's combine (a kernel boundary away)
-      float* wsr = ws + ((row0 + h) * n_splits + split) * (HS + 4);
-      wsr[4 + d] = ot;
-      if (d == 0) *(float2*)wsr = make_float2(mx, lt);
-    } else if (n_splits == 1) {
+    if (n_splits == 1) {
       y[(row0 + h) * HS + d] = f2bf(ot / lt);
     } else {
       float* wsr = ws + ((row0 + h) * n_splits + split) * (HS + 4);
@@ -254,7 +245,7 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
     }
   }
   LGA_TRACE(4);
-  if (n_splits == 1 || part_only) return;
+  if (n_splits == 1) return;
   // ---- publish, then the last-arriving split of this (t, group) merges all splits ----
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
@@ -533,20 +524,20 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(const uint16_t* __
 template <int HS, int QPK, int UNR, int NW, bool FUSED>
 static void launch_one(dim3 grid, hipStream_t stream, const void* q, void* kc, void* vc, const int64_t* pos, void* y,
                        float* ws, unsigned* cnt, int H, int max_seq, float scale, const int64_t* rope_pos,
-                       const float* cos, const float* sin, int rope_rows, int part_only) {
+                       const float* cos, const float* sin, int rope_rows) {
   attn_kernel<HS, QPK, UNR, NW, FUSED, LGA_ATTN_PIPE != 0><<<grid, NW * 64, 0, stream>>>((const uint16_t*)q, (uint16_t*)kc, (uint16_t*)vc,
                                                                      pos, (uint16_t*)y, ws, cnt, H, max_seq, scale,
-                                                                     rope_pos, cos, sin, rope_rows, part_only);
+                                                                     rope_pos, cos, sin, rope_rows);
 }
 
 template <int HS, bool FUSED>
 static int launch_hs(const void* q, void* kc, void* vc, const int64_t* pos, void* y, float* ws, unsigned* cnt, int T,
                      int H, int G, int max_seq, int n_splits, float scale, const int64_t* rope_pos, const float* cos,
-                     const float* sin, int rope_rows, hipStream_t stream, int part_only = 0) {
+                     const float* sin, int rope_rows, hipStream_t stream) {
   const dim3 grid(n_splits, G, T);
 #define LGA_ATTN(QPK, CFG)                                                                                        \
   launch_one<HS, QPK, CFG, FUSED>(grid, stream, q, kc, vc, pos, y, ws, cnt, H, max_seq, scale, rope_pos, cos, sin, \
-                                  rope_rows, part_only)
+                                  rope_rows)
   switch (H / G) {
     case 1: LGA_ATTN(1, LGA_ATTN_Q1); break;
     case 2: LGA_ATTN(2, LGA_ATTN_Q2); break;
@@ -621,24 +612,6 @@ extern "C" int lga_attention_decode_fused(const void* qkv, void* k_cache, void* 
   LGA_LAUNCH_RETURN();
 }
 
-extern "C" int lga_attention_decode_split(const void* qkv, void* k_cache, void* v_cache, const int64_t* cache_pos,
-                                          const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows,
-                                          float* partials, int n_head, int n_query_groups, int head_size,
-                                          int rope_n_elem, int max_seq, int n_splits, float scale,
-                                          hipStream_t stream) {
-  LGA_CHECK_ARG(qkv && k_cache && v_cache && cache_pos && rope_pos && cos && sin && partials,
-                "lga_attention_decode_split: null pointer");
-  LGA_CHECK_ARG(n_query_groups > 0 && n_head % n_query_groups == 0, "lga_attention_decode_split: bad head geometry");
-  LGA_CHECK_ARG(head_size == 128 && rope_n_elem == 128, "lga_attention_decode_split: needs head_size == rope_n_elem == 128");
-  LGA_CHECK_ARG(rope_rows > 0 && max_seq > 0, "lga_attention_decode_split: empty rope cache or kv cache");
-  LGA_CHECK_ARG(n_splits >= 1 && n_splits <= 256, "lga_attention_decode_split: n_splits must be in [1, 256]");
-  const int rc = lga::launch_hs<128, true>(qkv, k_cache, v_cache, cache_pos, nullptr, partials, nullptr, 1, n_head,
-                                           n_query_groups, max_seq, n_splits, scale, rope_pos, cos, sin, rope_rows,
-                                           stream, /*part_only=*/1);
-  if (rc) return rc;
-  LGA_LAUNCH_RETURN();
-}
-
 #ifdef LGA_ATTN_TRACE
 extern "C" int lga_attn_trace_read(unsigned long long* host, int n) {
   hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(lga::g_attn_trace), (size_t)n * sizeof(unsigned long long));
@@ -652,6 +625,5 @@ extern "C" int lga_attn_trace_read(unsigned long long* host, int n) {
 
 // fp32 partials (T * H * n_splits * (hs + 4)); the counters (T * G * 64 uint32) must be zeroed once at allocation
 extern "C" size_t lga_attention_workspace_bytes(int T, int n_head, int head_size, int n_splits) {
-  // sized for n_splits >= 1: lga_attention_decode_split writes its (m, l, o) partials even for one split
   return (size_t)T * n_head * (n_splits < 1 ? 1 : n_splits) * (head_size + 4) * sizeof(float);
 }

@@ -50,12 +50,16 @@ __global__ void __launch_bounds__(kCommThreads) allreduce_kernel(const uint16_t*
     for (int i = t; i < n8; i += kCommThreads) dst[i] = ((const uint4*)x)[i];
   }
   // 2. release: every storing thread's writes are complete and visible system-wide before any flag
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  //    (each storing wave drains its stores, the workgroup barrier orders them before the flag writers, and each
+  //    flag writer publishes with a system-scope RELEASE store behind an explicit drain: MI355X_MICROARCH.md
+  //    "Compiler hazard" — the asm wait keeps the release's write-back wait from being dropped)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (t < world && t != rank) {
     unsigned* f = (unsigned*)peers.mb[t] + rank * kFlagStride;
-    __hip_atomic_store(f, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // 3. wait for every peer's flag in this rank's own mailbox (bounded: 5 s of the 100 MHz real-time clock — far
   //    beyond any host-side skew between live ranks — then the error word is set and the kernel finishes with

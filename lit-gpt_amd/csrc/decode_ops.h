@@ -230,57 +230,4 @@ __device__ __forceinline__ uint4 rope8(const uint4 raw, const float* cr, const f
   return make_uint4(out[0], out[1], out[2], out[3]);
 }
 
-// ---- split-attention combine as a GEMV activation prologue (lga_q4_gemv_attn / lga_bf16_gemv_attn) ----
-// Workspace of lga_attention_decode_split: per head row h and split s, (HS + 4) floats at (h * S + s) * (HS + 4):
-// m, l, -, -, o[0..HS). x chunk u (the 8 values x[8u .. 8u+7], one head) is the flash-decoding merge of the S
-// splits in rounds of 8, exactly as attn_kernel's in-launch combine (same max / exp / fmaf order, one bf16 cast),
-// so the two paths are bit-identical.
-struct XPartRound {
-  float2 ml[8];
-  float4 o0[8], o1[8];
-};
-
-__device__ __forceinline__ void xpart_load(const float* ws, int S, int HS, int u, int s0, XPartRound& r) {
-  const int e = u * 8, h = e / HS, d0 = e % HS;
-  const float* base = ws + (size_t)h * S * (HS + 4);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const float* row = base + (size_t)min(s0 + k, S - 1) * (HS + 4);
-    r.ml[k] = *(const float2*)row;
-    r.o0[k] = *(const float4*)(row + 4 + d0);
-    r.o1[k] = *(const float4*)(row + 8 + d0);
-  }
-}
-
-__device__ __forceinline__ uint4 xpart_combine(const float* ws, int S, int HS, int u, XPartRound& r) {
-  float mx = -INFINITY, lt = 0.0f, ot[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) ot[j] = 0.0f;
-  for (int s0 = 0; s0 < S; s0 += 8) {
-    if (s0 > 0) xpart_load(ws, S, HS, u, s0, r);
-    float mv[8];
-    float nm = mx;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      mv[k] = s0 + k < S ? r.ml[k].x : -INFINITY;
-      nm = fmaxf(nm, mv[k]);
-    }
-    const float c = expf(mx - nm);  // round 0: exp(-inf) = 0
-    lt *= c;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) ot[j] *= c;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      const float e = expf(mv[k] - nm);
-      lt = fmaf(r.ml[k].y, e, lt);
-      const float ov[8] = {r.o0[k].x, r.o0[k].y, r.o0[k].z, r.o0[k].w, r.o1[k].x, r.o1[k].y, r.o1[k].z, r.o1[k].w};
-#pragma unroll
-      for (int j = 0; j < 8; ++j) ot[j] = fmaf(ov[j], e, ot[j]);
-    }
-    mx = nm;
-  }
-  return make_uint4(pack2(ot[0] / lt, ot[1] / lt), pack2(ot[2] / lt, ot[3] / lt), pack2(ot[4] / lt, ot[5] / lt),
-                    pack2(ot[6] / lt, ot[7] / lt));
-}
-
 }  // namespace lga

@@ -34,10 +34,10 @@ namespace lga {
 #endif
 constexpr int kGemvNW = LGA_GEMV_NW;
 
-template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, bool XC = false>
+template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES>
 __global__ void __launch_bounds__(kGemvNW * 64) gemv_q4_kernel(GemvArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  gemv_q4_body<RPR, CPT, FMT, DUAL, NORM, RES, kGemvNW, XC>(a, blockIdx.x, smem);
+  gemv_q4_body<RPR, CPT, FMT, DUAL, NORM, RES, kGemvNW>(a, blockIdx.x, smem);
 }
 
 template <int RPR, int CPT, int FMT, bool DUAL>
@@ -50,10 +50,7 @@ static void launch(const GemvArgs& a, hipStream_t stream) {
 #endif
   constexpr int NT = kGemvNW * 64;
   const bool norm = a.norm_w != nullptr, res = a.residual != nullptr;
-  if (!DUAL && a.xpart) {  // attention out-projection: activation merged from the split partials, no norm
-    if (res) gemv_q4_kernel<RPR, CPT, FMT, false, false, true, true><<<blocks, NT, lds, stream>>>(a);
-    else gemv_q4_kernel<RPR, CPT, FMT, false, false, false, true><<<blocks, NT, lds, stream>>>(a);
-  } else if (DUAL) {
+  if (DUAL) {
     if (norm) gemv_q4_kernel<RPR, CPT, FMT, DUAL, true, false><<<blocks, NT, lds, stream>>>(a);
     else gemv_q4_kernel<RPR, CPT, FMT, DUAL, false, false><<<blocks, NT, lds, stream>>>(a);
   } else if (norm) {
@@ -126,7 +123,7 @@ static bool stream_default(int N, int K, bool dual) {
 template <int FMT, bool DUAL>
 static int dispatch(const GemvArgs& a, int variant, hipStream_t stream) {
   const int cpt = (a.K / 32 + 63) / 64;  // chunks per lane (== uint4 of x per thread)
-  if (!a.eidx && !a.xpart && a.K <= 4096 &&
+  if (!a.eidx && a.K <= 4096 &&
       ((variant >= 0 && (variant & 4)) || (variant < 0 && stream_default(a.N, a.K, DUAL))))
     return dispatch_stream<FMT, DUAL>(a, variant < 0 ? 4 : variant, stream);
   if (variant < 0) {
@@ -173,22 +170,6 @@ extern "C" int lga_q4_gemv(const void* x, const uint8_t* qweight, const void* sc
   LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv: fmt must be 0 (int4-g) or 1 (nf4)");
   lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, (const uint16_t*)bias,
                   (const uint16_t*)residual, (const uint16_t*)norm_weight, (uint16_t*)y, N, K, group, norm_eps};
-  const int rc = fmt == 0 ? lga::dispatch<0, false>(a, variant, stream) : lga::dispatch<1, false>(a, variant, stream);
-  if (rc) return rc;
-  LGA_LAUNCH_RETURN();
-}
-
-extern "C" int lga_q4_gemv_attn(const float* partials, int n_splits, int head_size, const uint8_t* qweight,
-                                const void* scales, const void* bias, const void* residual, void* y, int N, int K,
-                                int group, int fmt, int variant, hipStream_t stream) {
-  LGA_CHECK_ARG(partials && qweight && scales && y, "lga_q4_gemv_attn: null pointer");
-  LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0, "lga_q4_gemv_attn: K must be a positive multiple of 32");
-  LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv_attn: bad group");
-  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv_attn: fmt must be 0 (int4-g) or 1 (nf4)");
-  LGA_CHECK_ARG(head_size % 8 == 0 && head_size > 0 && K % head_size == 0 && n_splits >= 1 && n_splits <= 256,
-                "lga_q4_gemv_attn: K must be a whole number of heads, 1 <= n_splits <= 256");
-  lga::GemvArgs a{nullptr, qweight, scales, nullptr, nullptr, (const uint16_t*)bias, (const uint16_t*)residual,
-                  nullptr, (uint16_t*)y, N, K, group, 0.0f, nullptr, 0, 0, 0, 0, 0, partials, n_splits, head_size};
   const int rc = fmt == 0 ? lga::dispatch<0, false>(a, variant, stream) : lga::dispatch<1, false>(a, variant, stream);
   if (rc) return rc;
   LGA_LAUNCH_RETURN();

@@ -29,14 +29,12 @@ struct GemvBArgs {
   uint16_t* y;               // [N]
   int N, K;
   float eps;
-  const float* xpart;        // XC (lga_bf16_gemv_attn): x merged from split-attention partials (decode_ops.h)
-  int xsplits, xhs;
 };
 
 constexpr int BCPT = 8;                 // 16-B chunks per lane per pass
 constexpr int BPASS = 64 * BCPT;        // chunks per pass (4096 columns)
 
-template <int RPR, bool DUAL, bool NORM, bool RES, int XPT, bool MULTI, bool XC = false>
+template <int RPR, bool DUAL, bool NORM, bool RES, int XPT, bool MULTI>
 __global__ void __launch_bounds__(256) gemv_bf16_kernel(GemvBArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint4* xl = (uint4*)smem;                     // K/8 uint4 (plain bf16 order)
@@ -51,16 +49,11 @@ __global__ void __launch_bounds__(256) gemv_bf16_kernel(GemvBArgs a) {
 
   // 1. activation (and norm weight) share of this thread: uint4 t, t+256, ... (clamped, branch-free)
   uint4 xr[XPT], nr[XPT];
-  XPartRound xp[XC ? XPT : 1];
 #pragma unroll
   for (int i = 0; i < XPT; ++i) {
     const int u = min(t + 256 * i, n8 - 1);
-    if (XC) {
-      xpart_load(a.xpart, a.xsplits, a.xhs, u, 0, xp[i]);
-    } else {
-      xr[i] = ((const uint4*)a.x)[u];
-      if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
-    }
+    xr[i] = ((const uint4*)a.x)[u];
+    if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
   }
   // 2. pass-0 weight loads of every row of this wave (rows past N re-read row N-1; never stored)
   static_assert(R >= 1 && R <= 8, "row partials per lane");
@@ -84,12 +77,7 @@ __global__ void __launch_bounds__(256) gemv_bf16_kernel(GemvBArgs a) {
   if (RES) res = a.residual[min(row0 + (lane & (RPR - 1)), a.N - 1)];
   __builtin_amdgcn_sched_barrier(0);  // nothing that waits on x may move above the weight loads
 
-  // 3. stage x into LDS (RMS-normalised when NORM, merged from the attention splits when XC) while the weights
-  //    stream
-  if (XC) {
-#pragma unroll
-    for (int i = 0; i < XPT; ++i) xr[i] = xpart_combine(a.xpart, a.xsplits, a.xhs, min(t + 256 * i, n8 - 1), xp[i]);
-  }
+  // 3. stage x into LDS (RMS-normalised when NORM) while the weights stream
   float rs = 1.0f;
   if (NORM) {
     float ss = 0.0f;
@@ -191,10 +179,7 @@ static void launch_b(const GemvBArgs& a, hipStream_t stream) {
   const dim3 blocks((waves + 3) / 4);
   const size_t lds = (size_t)a.K * 2 + 4 * 4;
   const bool norm = a.norm_w != nullptr, res = a.residual != nullptr;
-  if (!DUAL && a.xpart) {
-    if (res) gemv_bf16_kernel<RPR, false, false, true, XPT, MULTI, true><<<blocks, 256, lds, stream>>>(a);
-    else gemv_bf16_kernel<RPR, false, false, false, XPT, MULTI, true><<<blocks, 256, lds, stream>>>(a);
-  } else if (DUAL) {
+  if (DUAL) {
     if (norm) gemv_bf16_kernel<RPR, DUAL, true, false, XPT, MULTI><<<blocks, 256, lds, stream>>>(a);
     else gemv_bf16_kernel<RPR, DUAL, false, false, XPT, MULTI><<<blocks, 256, lds, stream>>>(a);
   } else if (norm) {
@@ -237,21 +222,6 @@ extern "C" int lga_bf16_gemv(const void* x, const void* weight, const void* bias
                 "lga_bf16_gemv: x, weight and norm_weight must be 16-B aligned");
   lga::GemvBArgs a{(const uint16_t*)x, (const uint16_t*)weight, nullptr, (const uint16_t*)bias,
                    (const uint16_t*)residual, (const uint16_t*)norm_weight, (uint16_t*)y, N, K, norm_eps};
-  const int rc = lga::dispatch_b<false>(a, stream);
-  if (rc) return rc;
-  LGA_LAUNCH_RETURN();
-}
-
-extern "C" int lga_bf16_gemv_attn(const float* partials, int n_splits, int head_size, const void* weight,
-                                  const void* bias, const void* residual, void* y, int N, int K, hipStream_t stream) {
-  LGA_CHECK_ARG(partials && weight && y, "lga_bf16_gemv_attn: null pointer");
-  LGA_CHECK_ARG(N > 0 && K > 0 && K % 8 == 0, "lga_bf16_gemv_attn: K must be a positive multiple of 8");
-  LGA_CHECK_ARG(((uintptr_t)weight % 16 == 0) && ((uintptr_t)partials % 16 == 0),
-                "lga_bf16_gemv_attn: weight and partials must be 16-B aligned");
-  LGA_CHECK_ARG(head_size % 8 == 0 && head_size > 0 && K % head_size == 0 && n_splits >= 1 && n_splits <= 256,
-                "lga_bf16_gemv_attn: K must be a whole number of heads, 1 <= n_splits <= 256");
-  lga::GemvBArgs a{nullptr, (const uint16_t*)weight, nullptr, (const uint16_t*)bias, (const uint16_t*)residual,
-                   nullptr, (uint16_t*)y, N, K, 0.0f, partials, n_splits, head_size};
   const int rc = lga::dispatch_b<false>(a, stream);
   if (rc) return rc;
   LGA_LAUNCH_RETURN();

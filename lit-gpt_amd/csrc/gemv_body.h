@@ -44,14 +44,11 @@ struct GemvArgs {
   const int32_t* eidx;
   long long ew, es;
   int xs, n_expert, slots;
-  // XC (lga_q4_gemv_attn): x is not stored; it is the split-attention merge of these partials (decode_ops.h)
-  const float* xpart;
-  int xsplits, xhs;
 };
 
 // One wave of a decode GEMV (see gemv.hip for the design). NW waves per workgroup (each its own row slot); the
 // workgroup stages x once for all of them.
-template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, int NW = 4, bool XC = false>
+template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, int NW = 4>
 __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char* smem) {
   if (a.eidx) {  // wave-uniform: one scalar load of the routed expert id, then plain pointer offsets
     const long long e = min(max(a.eidx[blockIdx.y], 0), a.n_expert - 1);
@@ -79,23 +76,17 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
   LGA_GTRACE_NOWAIT(0);
 
   // 1. activation (and norm weight) share of this thread: uint4 t, t+NT, ... (clamped, branch-free)
-  //    (XC: the first round of split-attention partials x is merged from, issued just as early)
   uint4 xr[XI], nr[XI];
-  XPartRound xp[XC ? XI : 1];
 #pragma unroll
   for (int i = 0; i < XI; ++i) {
     const int u = min(t + NT * i, n8 - 1);
-    if (XC) {
-      xpart_load(a.xpart, a.xsplits, a.xhs, u, 0, xp[i]);
-    } else {
 #ifdef LGA_LAB_NOX  // lab builds only: cost of the activation fetch
-      xr[i] = make_uint4(0x3F803F80u + u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
-      if (NORM) nr[i] = xr[i];
+    xr[i] = make_uint4(0x3F803F80u + u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
+    if (NORM) nr[i] = xr[i];
 #else
-      xr[i] = ((const uint4*)a.x)[u];
-      if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
+    xr[i] = ((const uint4*)a.x)[u];
+    if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
 #endif
-    }
   }
   // 2. every weight / scale / residual load of this wave (rows past N re-read row N-1; never stored), issued in
   //    the order step 4 consumes them (chunk-major, each scale right after its weights): vmcnt retires in order,
@@ -130,12 +121,7 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
   __builtin_amdgcn_sched_barrier(0);  // nothing that waits on x may move above the weight loads
   LGA_GTRACE_NOWAIT(1);
 
-  // 3. stage x into LDS (RMS-normalised when NORM, merged from the attention splits when XC) while the weights
-  //    stream
-  if (XC) {
-#pragma unroll
-    for (int i = 0; i < XI; ++i) xr[i] = xpart_combine(a.xpart, a.xsplits, a.xhs, min(t + NT * i, n8 - 1), xp[i]);
-  }
+  // 3. stage x into LDS (RMS-normalised when NORM) while the weights stream
   float rs = 1.0f;
   if (NORM) {
     float ss = 0.0f;

@@ -100,6 +100,7 @@ def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temp
                         break
                 i += n
         tokens.append(out[:produced])
+        _check_collectives()
         return torch.cat(tokens)
     input_pos = torch.tensor([T], device=device)
     for _ in range(n_steps):
@@ -108,7 +109,17 @@ def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temp
         if eos_id is not None and int(token) == eos_id:
             break
         input_pos = input_pos.add_(1)
+    _check_collectives()
     return torch.cat(tokens)
+
+
+def _check_collectives() -> None:
+    """Under tensor parallelism with the xGMI all-reduce: raise (on every rank) if any decode all-reduce of this
+    run gave up waiting for a peer — its logits were summed from partial data (lit_gpt/comm.py check_errors)."""
+    from lit_gpt import comm
+
+    if comm.get_default() is not None:
+        comm.check_errors()
 
 
 def build_model(config: Config, *, quantize: Optional[str], device: torch.device, seed: int = 1234,

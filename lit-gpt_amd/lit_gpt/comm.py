@@ -139,6 +139,28 @@ class XgmiAllReduce:
             self._own = None
 
 
+class AllReduceTimeout(RuntimeError):
+    """An xGMI all-reduce gave up waiting for a peer (5 s bound in the kernel): the logits of that step were
+    summed from partial data, so the run is void. Raised on every rank (the outcome is agreed over the group)."""
+
+
+def check_errors(comm: Optional["XgmiAllReduce"] = None) -> None:
+    """Collective: every rank reports whether any of its all-reduce calls since the last check timed out, the
+    ranks agree (MAX over the group) and all of them raise ``AllReduceTimeout`` if one did. Call it at the same
+    point on every rank (generate() does after each run, bench.py after the timed region). No-op without an
+    installed communicator."""
+    comm = comm or _default
+    if comm is None:
+        return
+    mine = comm.errors()
+    flag = torch.tensor([1 if mine else 0], dtype=torch.int32,
+                        device=comm.device if dist.get_backend(comm.group) == "nccl" else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=comm.group)
+    if int(flag.item()):
+        raise AllReduceTimeout(f"rank {comm.rank}: an xGMI all-reduce timed out waiting for a peer "
+                               f"({'this rank' if mine else 'another rank'}); the generated tokens are invalid")
+
+
 def set_default(comm: Optional[XgmiAllReduce]) -> None:
     """Install the communicator the TP hooks (generate/tp.py all_reduce_output) use for small messages."""
     global _default

@@ -74,21 +74,6 @@ def _dense(linear: nn.Linear, x: torch.Tensor, *, residual: Optional[torch.Tenso
     return y.view(*lead, N)
 
 
-def _lin_attn(linear: nn.Module, partials: torch.Tensor, n_splits: int, head_size: int,
-              residual: Optional[torch.Tensor]) -> torch.Tensor:
-    """The attention out-projection of one decode token fed from split-attention partials (the merge runs in the
-    GEMV prologue, ops.attention_decode_split); (1, 1, N)."""
-    from lit_gpt.quantize import QuantLinear
-
-    if isinstance(linear, QuantLinear):
-        return linear.forward_attn(partials, n_splits, head_size, residual=residual)
-    w = _dense_weight(linear)
-    b = None if linear.bias is None else linear.bias.to(torch.bfloat16)
-    y = ops.bf16_gemv_attn(partials, n_splits, head_size, w, bias=b,
-                           residual=None if residual is None else residual.reshape(-1).contiguous())
-    return y.view(1, 1, w.shape[0])
-
-
 def _lin(linear: nn.Module, x: torch.Tensor, **kw) -> torch.Tensor:
     from lit_gpt.quantize import QuantLinear
 
@@ -273,11 +258,6 @@ class CausalSelfAttention(nn.Module):
     # decode tokens (T = 1) with full 128-dim rotary use lga_attention_decode_fused; False keeps the two-launch
     # rope_kv_append + attention path (bit-identical; tests compare the two)
     fuse_decode = True
-    # ...and with split_proj the attention leaves its per-split partials to the out-projection GEMV, which merges
-    # them in its prologue (lga_attention_decode_split + lga_q4_gemv_attn; bit-identical to fused + gemv). Off by
-    # default: at Llama-2-7B decode the attention gets 1.5 us faster but the GEMV reads 4x its weight bytes in
-    # partials and gets 1.6-2.2 us slower (profiles/r02_*). LGA_SPLIT_PROJ=1 turns it on.
-    split_proj = os.environ.get("LGA_SPLIT_PROJ", "0") == "1"
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
                 input_pos: Optional[torch.Tensor] = None, *, norm: Optional["RMSNorm"] = None,
@@ -317,12 +297,6 @@ class CausalSelfAttention(nn.Module):
             ws = getattr(self, "_attn_ws", None)
             if ws is None or ws.key != (1, H, G, hs, n_splits) or ws.counters.device != dev:
                 ws = self._attn_ws = ops.AttentionWorkspace(1, H, G, hs, n_splits, dev)
-        if (T == 1 and self.fuse_decode and self.split_proj and ops.decode_fusable(hs, c.rope_n_elem)
-                and ws is not None and not self.proj._forward_hooks and not self.proj._forward_pre_hooks):
-            # decode token: RoPE + KV-append + split attention in one launch, the split merge in the proj GEMV
-            part = ops.attention_decode_split(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem,
-                                              1.0 / math.sqrt(hs), n_splits, workspace=ws)
-            return _lin_attn(self.proj, part, n_splits, hs, residual).view(B, T, -1)
         if T == 1 and self.fuse_decode and ops.decode_fusable(hs, c.rope_n_elem):
             # decode token: RoPE + KV-append + attention in a single launch
             y = ops.attention_decode_fused(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem,

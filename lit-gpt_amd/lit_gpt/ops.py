@@ -40,12 +40,10 @@ SIGNATURES = {
     "lga_nf4_double_quant": [_P, _L, _P, _P, _P],
     "lga_q4_gemv": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemv_swiglu": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
-    "lga_q4_gemv_attn": [_P, _I, _I, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemm": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_dequantize": [_P, _P, _P, _I, _I, _I, _I, _P],
     "lga_bf16_gemv": [_P, _P, _P, _P, _P, _F, _P, _I, _I, _P],
     "lga_bf16_gemv_swiglu": [_P, _P, _P, _P, _F, _P, _I, _I, _P],
-    "lga_bf16_gemv_attn": [_P, _I, _I, _P, _P, _P, _P, _I, _I, _P],
     "lga_bf16_gemm": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lga_gemm_bf16_blaslt": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P],
     "lga_gemm_bf16_blaslt_tune": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P],
@@ -59,7 +57,6 @@ SIGNATURES = {
     "lga_attention": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_attention_workspace_bytes": [_I, _I, _I, _I],
     "lga_attention_decode_fused": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
-    "lga_attention_decode_split": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_argmax": [_P, _I, _P, _P, _P, _P],
     "lga_argmax_embed": [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P],
     "lga_moe_route": [_P, _I, _I, _I, _P, _P, _P],
@@ -176,19 +173,6 @@ def q4_gemv_swiglu(x, qw1, sc1, qw2, sc2, N, K, group, fmt, *, norm_weight=None,
     return y
 
 
-def q4_gemv_attn(partials, n_splits, head_size, qweight, scales, N, K, group, fmt, *, bias=None, residual=None,
-                 out=None, variant=-1):
-    """y (N,) = merge(partials) (K = heads * head_size, the split attention's output) . dequant(W)^T [+bias]
-    [+residual]: the attention out-projection fed straight from lga_attention_decode_split."""
-    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=partials.device)
-    _check(load_library().lga_q4_gemv_attn(_dev(partials, "partials", torch.float32), int(n_splits), int(head_size),
-                                           _dev(qweight, "qweight", torch.uint8), _dev(scales, "scales"),
-                                           _opt(bias, "bias", torch.bfloat16),
-                                           _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16),
-                                           N, K, group, fmt, variant, _stream()))
-    return y
-
-
 def q4_gemm(x, qweight, scales, N, K, group, fmt, *, bias=None, residual=None, out=None):
     """Y (M, N) = X (M, K) . dequant(W)^T [+bias] [+residual] with MFMA tiles."""
     M = x.shape[0]
@@ -231,18 +215,6 @@ def bf16_gemv_swiglu(x, w1, w2, *, norm_weight=None, eps=1e-5, out=None):
                                                _dev(w2, "w2", torch.bfloat16),
                                                _opt(norm_weight, "norm_weight", torch.bfloat16), float(eps),
                                                _dev(y, "y", torch.bfloat16), N, K, _stream()))
-    return y
-
-
-def bf16_gemv_attn(partials, n_splits, head_size, weight, *, bias=None, residual=None, out=None):
-    """bf16-weight form of q4_gemv_attn."""
-    N, K = weight.shape
-    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=partials.device)
-    _check(load_library().lga_bf16_gemv_attn(_dev(partials, "partials", torch.float32), int(n_splits),
-                                             int(head_size), _dev(weight, "weight", torch.bfloat16),
-                                             _opt(bias, "bias", torch.bfloat16),
-                                             _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16),
-                                             N, K, _stream()))
     return y
 
 
@@ -398,25 +370,6 @@ def attention_decode_fused(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin,
         cos.shape[0], _dev(y, "y", torch.bfloat16), ws, cnt, n_head, n_query_groups, head_size, rope_n_elem, max_seq,
         n_splits, float(scale), _stream()))
     return y
-
-
-def attention_decode_split(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin, n_head, n_query_groups,
-                           head_size, rope_n_elem, scale, n_splits, workspace: AttentionWorkspace):
-    """attention_decode_fused without the split merge: returns ``workspace.partials`` holding every split's
-    (m, l, o) for q4_gemv_attn / bf16_gemv_attn (the out-projection merges them in its prologue)."""
-    if qkv.shape[0] != 1:
-        raise ValueError("attention_decode_split handles exactly one token (T = 1)")
-    if workspace is None or workspace.key != (1, n_head, n_query_groups, head_size, n_splits):
-        raise ValueError("attention_decode_split needs an AttentionWorkspace of this geometry")
-    if workspace.partials.numel() * 4 < load_library().lga_attention_workspace_bytes(1, n_head, head_size, n_splits):
-        raise ValueError("attention_decode_split: workspace too small for the split partials")
-    _check(load_library().lga_attention_decode_split(
-        _dev(qkv, "qkv", torch.bfloat16), _dev(k_cache, "k_cache", torch.bfloat16),
-        _dev(v_cache, "v_cache", torch.bfloat16), _dev(cache_pos, "cache_pos", torch.int64),
-        _dev(rope_pos, "rope_pos", torch.int64), _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32),
-        cos.shape[0], _dev(workspace.partials, "partials", torch.float32), n_head, n_query_groups, head_size,
-        rope_n_elem, k_cache.shape[-2], n_splits, float(scale), _stream()))
-    return workspace.partials
 
 
 _N_CU = None

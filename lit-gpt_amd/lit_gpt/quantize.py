@@ -197,15 +197,6 @@ class QuantLinear(nn.Module):
             out = _dequant_scratch(N * K, device)
         return ops.q4_dequantize(self.qweight, self.scales, N, K, self.group, self.fmt, out=out)
 
-    def forward_attn(self, partials: torch.Tensor, n_splits: int, head_size: int, *,
-                     residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """One decode token of the attention out-projection, its input merged from split-attention partials
-        (ops.attention_decode_split) inside the GEMV: same bits as forward(attention output)."""
-        res = None if residual is None else residual.reshape(-1).contiguous()
-        y = ops.q4_gemv_attn(partials, n_splits, head_size, self.qweight, self.scales, self.out_features,
-                             self.in_features, self.group, self.fmt, bias=self.bias, residual=res)
-        return y.view(1, 1, self.out_features)
-
     def extra_repr(self) -> str:
         kind = "int4" if self.fmt == ops.FMT_Q4G else "nf4"
         return f"in_features={self.in_features}, out_features={self.out_features}, {kind}, group={self.group}"

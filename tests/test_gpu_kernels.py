@@ -458,42 +458,6 @@ def test_attention_decode_fused_matches_two_launch_path(ops, H, G, p, splits):
     assert torch.max((yb - ref).abs() - ref.abs() * 2 ** -7) <= 1e-4
 
 
-@pytest.mark.parametrize("H,G,splits", [(32, 32, 8), (16, 4, 16), (8, 1, 16), (64, 8, 5), (32, 32, 1), (16, 8, 23)])
-@pytest.mark.parametrize("p", [0, 3, 2047, 2303])
-@pytest.mark.parametrize("wfmt", ["q4g", "nf4", "bf16"])
-def test_attention_split_then_merging_proj_is_bit_exact(ops, H, G, splits, p, wfmt):
-    """lga_attention_decode_split + the out-projection GEMV that merges the split partials in its prologue
-    (lga_q4_gemv_attn / lga_bf16_gemv_attn) == lga_attention_decode_fused + lga_q4_gemv / lga_bf16_gemv with the
-    same residual: bit-identical output and caches (the decode step's attention -> proj seam)."""
-    hs, S = 128, 2304
-    C = H * hs
-    qkv = to_dev_bf16(synth.normal((1, (H + 2 * G) * hs), "sq", 3, 1.0))
-    k0 = to_dev_bf16(synth.normal((G, S, hs), "sk", 3, 1.0))
-    v0 = to_dev_bf16(synth.normal((G, S, hs), "sv", 3, 1.0))
-    res = to_dev_bf16(synth.normal((C,), "sr", 3, 1.0))
-    cos, sin = om.build_rope_cache(S, hs, 10000)
-    cos, sin = cos.to(DEV), sin.to(DEV)
-    pos = torch.tensor([p], device=DEV)
-    scale = 1.0 / math.sqrt(hs)
-    w = torch.from_numpy(synth.normal((C, C), "sw", 3)).to(DEV)
-    ka, va = k0.clone(), v0.clone()
-    y = ops.attention_decode_fused(qkv, ka, va, pos, pos, cos, sin, H, G, hs, hs, scale, n_splits=splits)
-    kb, vb = k0.clone(), v0.clone()
-    ws = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
-    part = ops.attention_decode_split(qkv, kb, vb, pos, pos, cos, sin, H, G, hs, hs, scale, splits, ws)
-    assert torch.equal(ka, kb) and torch.equal(va, vb)
-    if wfmt == "bf16":
-        wb = w.bfloat16().contiguous()
-        ref = ops.bf16_gemv(y.view(-1), wb, residual=res)
-        got = ops.bf16_gemv_attn(part, splits, hs, wb, residual=res)
-    else:
-        fmt, group = (0, 128) if wfmt == "q4g" else (1, 64)
-        qw, sc = ops.quantize(w, fmt, group)
-        ref = ops.q4_gemv(y.view(-1), qw, sc, C, C, group, fmt, residual=res)
-        got = ops.q4_gemv_attn(part, splits, hs, qw, sc, C, C, group, fmt, residual=res)
-    assert torch.equal(ref, got)
-
-
 def test_attention_decode_fused_rejects_unsupported_geometry(ops):
     qkv = torch.zeros(1, 3 * 64 * 4, dtype=torch.bfloat16, device=DEV)
     kc = torch.zeros(4, 16, 64, dtype=torch.bfloat16, device=DEV)

@@ -165,37 +165,6 @@ def test_teacher_forced_logits_match_oracle(key, mode):
         check_step(g, exp[torch.bfloat16][s], exp[torch.float64][s], f"{key} {mode} step {s}")
 
 
-@pytest.mark.parametrize("key", ["mha", "gqa", "mqa", "moe"])
-@pytest.mark.parametrize("mode", ["int4-g128", "bf16"])
-@torch.inference_mode()
-def test_split_attention_proj_path_is_bit_identical(key, mode):
-    """Decode with the attention split merged inside the out-projection GEMV (CausalSelfAttention.split_proj,
-    LGA_SPLIT_PROJ=1) == decode with the in-launch merge + plain GEMV (the default): identical logits at every
-    step."""
-    from lit_gpt.model import CausalSelfAttention
-
-    if mode == "bf16" and key == "moe":
-        pytest.skip("sparse-MoE experts run 4-bit weights only")
-    cfg = _cfg(key)
-    sd = synth.state_dict(cfg, seed=23)
-    T, N = 9, 10
-    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=23)).to(DEV)
-    stream = torch.from_numpy(synth.token_ids(N, cfg.vocab_size, seed=24)).to(DEV)
-    outs = {}
-    default = CausalSelfAttention.split_proj
-    for split in (True, False):
-        CausalSelfAttention.split_proj = split
-        try:
-            model = build_gpu_model(cfg, sd, mode, T + N)
-            lg = [model(prompt.view(1, -1), torch.arange(T, device=DEV))[0, -1]]
-            for i in range(N - 1):
-                lg.append(model(stream[i:i + 1].view(1, 1), torch.tensor([T + i], device=DEV))[0, -1])
-            outs[split] = torch.stack(lg).cpu()
-        finally:
-            CausalSelfAttention.split_proj = default
-    assert torch.equal(outs[True], outs[False])
-
-
 @pytest.mark.parametrize("key,mode", [("mha", "int4-g128"), ("gqa", "int4-g128"), ("moe", "int4-g128"),
                                       ("gqa", "bf16")])
 @torch.inference_mode()

@@ -51,10 +51,21 @@ def _check_logits(d):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("nproc", [2, 4])
+@pytest.mark.parametrize("nproc", [2, 4, 8])
 def test_xgmi_allreduce_bit_exact_vs_ordered_sum(nproc, tmp_path):
+    """Eager, graph-captured and back-to-back calls at 2, 4 and 8 ranks (8 = BASELINE config 4's rank count: the
+    8-slot mailboxes and flags all in use), each bit-exact vs the ordered fp32 sum over ranks."""
     out = tmp_path / "status.txt"
     _launch("allreduce_worker.py", nproc, [out], timeout=280)
+    assert out.read_text() == "ok", out.read_text()
+
+
+@pytest.mark.timeout(120)
+def test_xgmi_allreduce_late_peer_raises_on_every_rank(tmp_path):
+    """A peer later than the kernel's 5 s bound: the call finishes (no GPU hang) and comm.check_errors raises
+    AllReduceTimeout on every rank instead of letting the partial sum through."""
+    out = tmp_path / "status.txt"
+    _launch("allreduce_worker.py", 2, [out, "--late-peer"], timeout=100)
     assert out.read_text() == "ok", out.read_text()
 
 
@@ -62,21 +73,25 @@ def test_xgmi_allreduce_bit_exact_vs_ordered_sum(nproc, tmp_path):
 def test_tp8_llama2_70b_rank_geometry(tmp_path):
     """BASELINE config 4 per rank: Llama-2-70B at TP=8 (C 8192, 8 query heads + 1 KV group per rank, qkv 1280 rows,
     attn.proj K 1024, fc 3584 rows, mlp.proj K 3584), two full-width blocks, int4-g128, a 16-token prefill + 7 decode
-    steps; gloo all-reduce (eight ranks on one device)."""
+    steps, then the greedy HIP-graph decode; the xGMI one-shot all-reduce at its real rank count (eight ranks on one
+    device, every mailbox slot and flag in use, captured in the decode graph)."""
     out = tmp_path / "r.npz"
-    _launch("tp_geometry_worker.py", 8, [out, "--model", "Llama-2-70b-hf", "--layers", "2", "--allreduce", "gloo",
-                                         "--tmp", tmp_path], timeout=580)
+    _launch("tp_geometry_worker.py", 8, [out, "--model", "Llama-2-70b-hf", "--layers", "2", "--allreduce", "xgmi",
+                                         "--graph", "--tmp", tmp_path], timeout=580)
     print(f"worst {_check_logits(np.load(out)):.3%}")
 
 
 @pytest.mark.timeout(600)
 def test_tp8_llama2_7b_ragged_int4_group(tmp_path):
     """Llama-2-7B at TP=8: mlp.proj shards have K = 11008 / 8 = 1376 (not a multiple of 128), quantized with the
-    largest fitting group (32) per shard; the oracle dequantizes exactly those shards."""
+    largest fitting group (32) per shard; the oracle dequantizes exactly those shards. xGMI all-reduce at 8 ranks,
+    eager and graph-captured (the graph's greedy tokens must equal the eager argmaxes where margins are clear)."""
     out = tmp_path / "r.npz"
-    _launch("tp_geometry_worker.py", 8, [out, "--model", "Llama-2-7b-hf", "--layers", "2", "--allreduce", "gloo",
-                                         "--tmp", tmp_path], timeout=580)
-    print(f"worst {_check_logits(np.load(out)):.3%}")
+    _launch("tp_geometry_worker.py", 8, [out, "--model", "Llama-2-7b-hf", "--layers", "2", "--allreduce", "xgmi",
+                                         "--graph", "--tmp", tmp_path], timeout=580)
+    d = np.load(out)
+    print(f"worst {_check_logits(d):.3%}")
+    assert len(d["graph_tokens"]) > 0
 
 
 @pytest.mark.timeout(600)

@@ -38,6 +38,8 @@ def main():
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
     c = comm.XgmiAllReduce(device=DEV)
+    if "--late-peer" in sys.argv:
+        return late_peer(c, out, world, rank)
     bad = []
     it = 0
     for n in (4096, 8192, 32768, 8):
@@ -88,6 +90,33 @@ def main():
     c.close()
     if rank == 0:
         Path(out).write_text("ok" if not bad and err == 0 else f"FAIL err={err} {bad[:5]}")
+    dist.destroy_process_group()
+
+
+def late_peer(c, out, world, rank):
+    """The last rank reaches the all-reduce 6 s after the others (past the kernel's 5 s peer bound): the early
+    ranks' kernels give up and set the error word; comm.check_errors must then raise AllReduceTimeout on EVERY
+    rank, the late one included (a lost peer must not yield silent partial sums)."""
+    import time
+
+    x = partial(rank, 4096, 1).to(DEV)
+    torch.cuda.synchronize()
+    dist.barrier()
+    if rank == world - 1:
+        time.sleep(6.0)
+    c.all_reduce(x)
+    torch.cuda.synchronize()
+    raised = 0
+    try:
+        comm.check_errors(c)
+    except comm.AllReduceTimeout:
+        raised = 1
+    flags = [None] * world
+    dist.all_gather_object(flags, raised)
+    dist.barrier()
+    c.close()
+    if rank == 0:
+        Path(out).write_text("ok" if all(flags) else f"FAIL raised per rank: {flags}")
     dist.destroy_process_group()
 
 
