@@ -62,6 +62,17 @@ int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const void* scale
 /* -- prefill GEMM, M > 1 (bnb dequantize_4bit + cuBLAS GEMM) -------------------------------------------- */
 int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const void* bias, const void* residual,
                 void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
+/* The same product with the dequantization fused into a 256 x 128 MFMA tile (csrc/gemm_q4f.hip): the weight
+ * is never written out in bf16. fmt 0 int4-g / 1 nf4 / 2 bf16 weights [N][K]; needs N % 8 == 0, K % 64 == 0 and
+ * (4-bit) a power-of-two group >= 64 dividing K (lga_q4f_fits). Numerically the bnb path: bf16(value * scale)
+ * weights, fp32 accumulation, one bf16 rounding (+bias), then + residual. */
+int lga_q4f_fits(int M, int N, int K, int group, int fmt);
+int lga_q4_gemm_fused(const void* x, const void* weight, const void* scales, const void* bias, const void* residual,
+                      void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
+/* LLaMAMLP prefill (lit_gpt/model.py:712-716): y (M, N) = bf16(silu(bf16(x W1^T))) * bf16(x W2^T), fc_1 and fc_2
+ * in one launch (each tile computes 64 columns of both and applies the product in its epilogue). */
+int lga_q4_gemm_swiglu(const void* x, const void* qweight1, const void* scales1, const void* qweight2,
+                       const void* scales2, void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
 /* bnb dequantize_4bit (the first half of the reference's M > 1 Linear4bit path): w (N, K) bf16 =
  * bf16(value(nibble) * scale) — the same bits lga_q4_gemm stages, so lga_bf16_gemm over w == lga_q4_gemm.
  * QuantLinear uses it for long prefills (M >= 512), where the bf16 GEMM's rate pays for the extra pass. */

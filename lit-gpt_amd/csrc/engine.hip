@@ -224,7 +224,7 @@ __device__ __forceinline__ void glds_line(const void* src, unsigned lds_dst) {
 struct Ctl {
   unsigned* w;  // [1] x_ready (op + 1), [2] gathering, [3] done_local, [4] abort, [5] split-last flag,
                 // [6] trace op, [7] RMSNorm partials, [8 + cw] consumer position, [24 + lw] lines landed by loader
-                // lw, [32 + 2 cw] argmax candidates, [60] gather waves finished
+                // lw, [32 + 2 cw] argmax candidates, [60] gather waves finished, [61] GEMV ops finished (x waves)
   __device__ unsigned* landed(int lw) const { return w + 24 + lw; }
   __device__ unsigned* xready() const { return w + 1; }
   __device__ unsigned* gathering() const { return w + 2; }
@@ -638,7 +638,8 @@ __device__ bool poll_granules(const Args& a, const Ctl& ctl, const Clock& clk, c
 // The wave that completes the staging raises x_ready.
 template <int FMT, int CPT, bool NORM, bool RES, bool DUAL>
 __device__ __attribute__((noinline)) bool gather_gemv(const Args& a, const Ctl& ctl, const Clock& clk, const Lds& s,
-                                                      int cw, int k, unsigned ng, unsigned tag, unsigned char* scl,
+                                                      int cw, int k, unsigned ng, unsigned ngemv, unsigned tag,
+                                                      unsigned char* scl,
                                                       const void* sc, const void* sc2, int n0, int rows, int groups,
                                                       const void* x, bool x_plain, const uint16_t* normw,
                                                       const void* res, bool res_plain, int K) {
@@ -689,6 +690,12 @@ __device__ __attribute__((noinline)) bool gather_gemv(const Args& a, const Ctl& 
 #ifdef LGA_ENGINE_TRACE
   if (cw == 0 && lane == 0) g_eng_trace[((size_t)blockIdx.x * TR_OPS + (unsigned)k) * TR_EV + 1] = __builtin_amdgcn_s_memrealtime();
 #endif
+  // this wave's slice being complete says nothing of this CU's own units of the previous GEMV, which read the whole
+  // staged vector: wait until every consumer wave has finished them before overwriting it
+  while (lds_ld(ctl.w + 61) < NCW * ngemv) {
+    if (lds_ld(ctl.abort()) || clk.expired()) return false;
+    __builtin_amdgcn_s_sleep(0);
+  }
   float rs = 1.0f;
   if (NORM) {
     uint4 nr[XI];
@@ -751,7 +758,7 @@ __device__ __attribute__((noinline)) bool gather_gemv(const Args& a, const Ctl& 
 
 template <int FMT, int QPK, int CPT_C, int CPT_I>
 __device__ bool gather(const Args& a, const Ctl& ctl, const Clock& clk, const Lds& s, const OpInfo& o, long p,
-                       unsigned tag, int k, int cw, unsigned ng) {
+                       unsigned tag, int k, int cw, unsigned ng, unsigned ngemv) {
   unsigned char* scl = s.scl + scale_buf(o.kind) * SCALE_BYTES;
   const Geo& g = a.g;
   const int lane = threadIdx.x & 63;
@@ -769,23 +776,23 @@ __device__ bool gather(const Args& a, const Ctl& ctl, const Clock& clk, const Ld
   const void* xl_in = o.l == 0 ? (const void*)x0 : (const void*)(xg + (o.l - 1) * hC);  // block input x_l
   switch (o.kind) {
     case K_QKV:
-      return gather_gemv<FMT, CPT_C, true, false, false>(a, ctl, clk, s, cw, k, ng, tag, scl, Lp->qkv_s, nullptr, n0,
+      return gather_gemv<FMT, CPT_C, true, false, false>(a, ctl, clk, s, cw, k, ng, ngemv, tag, scl, Lp->qkv_s, nullptr, n0,
                                                          rows, g.gC, xl_in, o.l == 0, (const uint16_t*)Lp->norm1,
                                                          nullptr, false, g.C);
     case K_O:
-      return gather_gemv<FMT, CPT_C, false, true, false>(a, ctl, clk, s, cw, k, ng, tag, scl, Lp->o_s, nullptr, n0,
+      return gather_gemv<FMT, CPT_C, false, true, false>(a, ctl, clk, s, cw, k, ng, ngemv, tag, scl, Lp->o_s, nullptr, n0,
                                                          rows, g.gC, yg + o.l * hC, false, nullptr, xl_in, o.l == 0,
                                                          g.C);
     case K_FC:
-      return gather_gemv<FMT, CPT_C, true, false, true>(a, ctl, clk, s, cw, k, ng, tag, scl, Lp->fc1_s, Lp->fc2_s,
+      return gather_gemv<FMT, CPT_C, true, false, true>(a, ctl, clk, s, cw, k, ng, ngemv, tag, scl, Lp->fc1_s, Lp->fc2_s,
                                                         n0, rows, g.gC, xpg + o.l * hC, false,
                                                         (const uint16_t*)Lp->norm2, nullptr, false, g.C);
     case K_DN:
-      return gather_gemv<FMT, CPT_I, false, true, false>(a, ctl, clk, s, cw, k, ng, tag, scl, Lp->dn_s, nullptr, n0,
+      return gather_gemv<FMT, CPT_I, false, true, false>(a, ctl, clk, s, cw, k, ng, ngemv, tag, scl, Lp->dn_s, nullptr, n0,
                                                          rows, g.gI, gg + o.l * ((size_t)g.I / 2), false, nullptr,
                                                          xpg + o.l * hC, false, g.I);
     case K_LM:
-      return gather_gemv<FMT, CPT_C, true, false, false>(a, ctl, clk, s, cw, k, ng, tag, scl, a.lm_s, nullptr, n0,
+      return gather_gemv<FMT, CPT_C, true, false, false>(a, ctl, clk, s, cw, k, ng, ngemv, tag, scl, a.lm_s, nullptr, n0,
                                                          rows, g.gC, g.L == 0 ? (const void*)x0 : (const void*)(xg + (g.L - 1) * hC),
                                                          g.L == 0, a.ln_f, nullptr, false, g.C);
     default: {  // attention (wave 0): the group's q heads, k, v granules; RoPE; the new key/value appended
@@ -1036,6 +1043,7 @@ __device__ void run_consumer(const Args& a, const Ctl& ctl, const Clock& clk, co
   int best_i = 0x7FFFFFFF;
   const unsigned tag = epoch + 1u;  // this launch's granule tag
   unsigned ng = 0;                   // RMSNorm gathers so far
+  unsigned ngemv = 0;                // GEMV ops finished by this wave
   for (int k = 0; k < nops; ++k) {
     const OpInfo o = op_info<CPT_C, CPT_I>(g, k, c, p);
     const bool norm = o.kind == K_QKV || o.kind == K_FC || o.kind == K_LM;
@@ -1047,7 +1055,7 @@ __device__ void run_consumer(const Args& a, const Ctl& ctl, const Clock& clk, co
 #endif
     }
     if (cw < NGW && (o.kind != K_ATTN || cw == 0)) {
-      if (!gather<FMT, QPK, CPT_C, CPT_I>(a, ctl, clk, s, o, p, tag, k, cw, ng)) {
+      if (!gather<FMT, QPK, CPT_C, CPT_I>(a, ctl, clk, s, o, p, tag, k, cw, ng, ngemv)) {
         lds_st(ctl.abort(), 1u);
         break;
       }
@@ -1116,6 +1124,9 @@ __device__ void run_consumer(const Args& a, const Ctl& ctl, const Clock& clk, co
         break;
       }
       lds_st(ctl.posw(cw), line_base + (unsigned)(o.n_units * o.lines));
+      // this wave is done reading the op's staged x / scales / residual rows
+      if (lane == 0) __hip_atomic_fetch_add(ctl.w + 61, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      ++ngemv;
       if (o.kind == K_LM) {
         if (lane == 0) {
           ctl.cand(cw)[0] = __float_as_uint(best_v);

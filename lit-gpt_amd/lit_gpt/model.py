@@ -70,8 +70,17 @@ def _dense(linear: nn.Linear, x: torch.Tensor, *, residual: Optional[torch.Tenso
     else:
         if norm_weight is not None:
             x2 = ops.rmsnorm(x2, norm_weight, norm_eps)
-        y = ops.bf16_gemm(x2, w, bias=b, residual=res)
+        if _fused_prefill(M, N, K, 64, 2):  # MFMA tiles with the weight DMA'd as stored (csrc/gemm_q4f.hip)
+            y = ops.q4_gemm_fused(x2, w, None, N, K, 64, 2, bias=b, residual=res)
+        else:
+            y = ops.bf16_gemm(x2, w, bias=b, residual=res)
     return y.view(*lead, N)
+
+
+def _fused_prefill(M: int, N: int, K: int, group: int, fmt: int) -> bool:
+    from lit_gpt import quantize
+
+    return quantize.PREFILL_GEMM == "fused" and M >= quantize.FUSED_GEMM_MIN_M and ops.q4f_fits(M, N, K, group, fmt)
 
 
 def _lin(linear: nn.Module, x: torch.Tensor, **kw) -> torch.Tensor:
@@ -384,7 +393,17 @@ class LLaMAMLP(nn.Module):
                                    eps=1e-5 if norm is None else norm.eps).view(1, -1)
         else:
             n = x2 if norm is None else norm(x2)
-            g = ops.swiglu(_lin(f1, n).contiguous(), _lin(f2, n).contiguous())
+            g = None
+            if f1.bias is None and f2.bias is None:  # fc_1 || fc_2 + SwiGLU in one fused GEMM launch
+                I = f1.out_features
+                if (isinstance(f1, QuantLinear) and isinstance(f2, QuantLinear)
+                        and (f1.fmt, f1.group) == (f2.fmt, f2.group) and _fused_prefill(M, I, C, f1.group, f1.fmt)):
+                    g = ops.q4_gemm_swiglu(n, f1.qweight, f1.scales, f2.qweight, f2.scales, I, C, f1.group, f1.fmt)
+                elif (type(f1) is nn.Linear and type(f2) is nn.Linear and f1.weight.is_cuda
+                      and f1.weight.shape == f2.weight.shape and _fused_prefill(M, I, C, 64, 2)):
+                    g = ops.q4_gemm_swiglu(n, _dense_weight(f1), None, _dense_weight(f2), None, I, C, 64, 2)
+            if g is None:
+                g = ops.swiglu(_lin(f1, n).contiguous(), _lin(f2, n).contiguous())
         out = _lin(self.proj, g, residual=residual)
         return out.view(*lead, -1)
 

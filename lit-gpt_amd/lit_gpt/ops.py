@@ -41,6 +41,9 @@ SIGNATURES = {
     "lga_q4_gemv": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemv_swiglu": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemm": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lga_q4f_fits": [_I, _I, _I, _I, _I],
+    "lga_q4_gemm_fused": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lga_q4_gemm_swiglu": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_dequantize": [_P, _P, _P, _I, _I, _I, _I, _P],
     "lga_bf16_gemv": [_P, _P, _P, _P, _P, _F, _P, _I, _I, _P],
     "lga_bf16_gemv_swiglu": [_P, _P, _P, _P, _F, _P, _I, _I, _P],
@@ -188,6 +191,35 @@ def q4_gemm(x, qweight, scales, N, K, group, fmt, *, bias=None, residual=None, o
                                       _dev(scales, "scales"), _opt(bias, "bias", torch.bfloat16),
                                       _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16),
                                       M, N, K, group, fmt, _stream()))
+    return y
+
+
+def q4f_fits(M, N, K, group, fmt) -> bool:
+    """Whether lga_q4_gemm_fused / lga_q4_gemm_swiglu take this shape (fmt 2 = bf16 weights)."""
+    return bool(load_library().lga_q4f_fits(int(M), int(N), int(K), int(group), int(fmt)))
+
+
+def q4_gemm_fused(x, weight, scales, N, K, group, fmt, *, bias=None, residual=None, out=None):
+    """Y (M, N) = X (M, K) . dequant(W)^T [+bias] [+residual], dequantization fused into the MFMA tiles
+    (fmt 2: ``weight`` is the bf16 (N, K) matrix, ``scales`` None)."""
+    M = x.shape[0]
+    y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    wdt = torch.bfloat16 if fmt == 2 else torch.uint8
+    _check(load_library().lga_q4_gemm_fused(_dev(x, "x", torch.bfloat16), _dev(weight, "weight", wdt),
+                                            _opt(scales, "scales"), _opt(bias, "bias", torch.bfloat16),
+                                            _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16),
+                                            M, N, K, group, fmt, _stream()))
+    return y
+
+
+def q4_gemm_swiglu(x, w1, s1, w2, s2, N, K, group, fmt, *, out=None):
+    """G (M, N) = bf16(silu(bf16(X W1^T))) * bf16(X W2^T) in one launch (LLaMAMLP fc_1 / fc_2 / silu*mul)."""
+    M = x.shape[0]
+    y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
+    wdt = torch.bfloat16 if fmt == 2 else torch.uint8
+    _check(load_library().lga_q4_gemm_swiglu(_dev(x, "x", torch.bfloat16), _dev(w1, "w1", wdt), _opt(s1, "s1"),
+                                             _dev(w2, "w2", wdt), _opt(s2, "s2"), _dev(y, "y", torch.bfloat16),
+                                             M, N, K, group, fmt, _stream()))
     return y
 
 

@@ -73,6 +73,11 @@ def _fit_group(K: int, group: int) -> int:
     raise ValueError(f"in_features={K} is not a multiple of 32; no 4-bit group layout fits")
 
 
+# Prefill GEMM for M > 1 rows: "fused" = lga_q4_gemm_fused (dequantization inside the MFMA tiles) from
+# FUSED_GEMM_MIN_M rows; "blaslt" = dequantize + hipBLASLt (LGA_PREFILL_GEMM=blaslt, for A/B runs).
+PREFILL_GEMM = os.environ.get("LGA_PREFILL_GEMM", "blaslt")
+FUSED_GEMM_MIN_M = 16
+
 # prefill rows from which dequantize + the library bf16 GEMM beats the fused int4 GEMM (tools/gemm_rates.py, Llama-2-7B
 # layer: 0.21 vs 0.44 ms at M = 64, 0.63 vs 1.04 ms at M = 2048; gemm.hip's 128-row tiles idle most CUs below M = 256)
 DEQUANT_GEMM_MIN_M = 16
@@ -164,7 +169,13 @@ class QuantLinear(nn.Module):
         else:
             if norm_weight is not None:
                 x2 = ops.rmsnorm(x2, norm_weight, norm_eps)
-            if M >= DEQUANT_GEMM_MIN_M:
+            if PREFILL_GEMM == "fused" and M >= FUSED_GEMM_MIN_M and ops.q4f_fits(M, self.out_features,
+                                                                                  self.in_features, self.group,
+                                                                                  self.fmt):
+                # dequantization fused into the MFMA tiles (csrc/gemm_q4f.hip): no bf16 weight in HBM
+                y = ops.q4_gemm_fused(x2, self.qweight, self.scales, self.out_features, self.in_features,
+                                      self.group, self.fmt, bias=self.bias, residual=res)
+            elif M >= DEQUANT_GEMM_MIN_M:
                 # long prefill: dequantize to bf16 once (bnb's dequantize_4bit, the reference's own M > 1 path),
                 # then the library bf16 GEMM (hipBLASLt): 1.1-1.25 PFLOP/s vs 0.5-0.7 for the fused int4 GEMM at
                 # M = 2048, the dequantize pass included (tools/gemm_rates.py)

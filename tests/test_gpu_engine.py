@@ -52,14 +52,16 @@ def test_engine_ops_match_per_op_kernels(T):
 
     model, cfg, first = _model(T)
     eng = DecodeEngine(model)
-    blk = model.transformer.h[0]
-    a, m = blk.attn, blk.mlp
     emb = ops.embedding(torch.tensor([first], device=DEV, dtype=torch.int32), model.transformer.wte.weight).view(-1)
-    kc0, vc0 = a.kv_cache.k.clone(), a.kv_cache.v.clone()
+    kv0 = [(b.attn.kv_cache.k.clone(), b.attn.kv_cache.v.clone()) for b in model.transformer.h]
+
+    def restore():
+        for b, (k, v) in zip(model.transformer.h, kv0):
+            b.attn.kv_cache.k.copy_(k)
+            b.attn.kv_cache.v.copy_(v)
 
     def run(limit):
-        a.kv_cache.k.copy_(kc0)
-        a.kv_cache.v.copy_(vc0)
+        restore()
         eng.reset()
         eng.set_embedding(emb)
         pos = torch.tensor([T], device=DEV)
@@ -68,49 +70,51 @@ def test_engine_ops_match_per_op_kernels(T):
         assert eng.errors() == 0
         return pos
 
-    # 1. RMSNorm + qkv GEMV
-    run(1)
-    qkv = eng.buffer("qkv", 0).clone()
-    ref = ops.q4_gemv(emb, a.attn.qweight, a.attn.scales, a.attn.out_features, cfg.n_embd, a.attn.group, a.attn.fmt,
-                      norm_weight=blk.norm_1.weight, eps=blk.norm_1.eps)
-    assert torch.equal(qkv, ref), "qkv GEMV differs from lga_q4_gemv"
-    # 2. RoPE + KV append + attention (the per-op fused kernel on the engine's qkv, same caches)
-    run(2)
-    y = eng.buffer("y", 0).clone()
-    k_eng, v_eng = a.kv_cache.k.clone(), a.kv_cache.v.clone()
-    a.kv_cache.k.copy_(kc0)
-    a.kv_cache.v.copy_(vc0)
     cos, sin = model._rope_tables()
-    p = torch.tensor([T], device=DEV)
     H, G, hs = cfg.n_head, cfg.n_query_groups, cfg.head_size
-    splits = ops.decode_splits(G, H // G, hs, a.kv_cache.k.size(-2))
-    y_ref = ops.attention_decode_fused(qkv.view(1, -1), a.kv_cache.k, a.kv_cache.v, p, p, cos, sin, H, G, hs, hs,
-                                       1.0 / math.sqrt(hs), splits)
-    assert torch.equal(k_eng, a.kv_cache.k) and torch.equal(v_eng, a.kv_cache.v), "KV append differs"
-    assert _ulps_close(y, y_ref.view(-1)), (y.float() - y_ref.view(-1).float()).abs().max()
-    # 3. o_proj + residual on the engine's attention output
-    run(3)
-    xp = eng.buffer("xp", 0).clone()
-    ref = ops.q4_gemv(eng.buffer("y", 0), a.proj.qweight, a.proj.scales, cfg.n_embd, cfg.n_embd, a.proj.group,
-                      a.proj.fmt, residual=emb)
-    assert torch.equal(xp, ref), "o_proj GEMV differs"
-    # 4. RMSNorm + fc_1 || fc_2 + SwiGLU
-    run(4)
-    g = eng.buffer("g", 0).clone()
-    ref = ops.q4_gemv_swiglu(eng.buffer("xp", 0), m.fc_1.qweight, m.fc_1.scales, m.fc_2.qweight, m.fc_2.scales,
-                             cfg.intermediate_size, cfg.n_embd, m.fc_1.group, m.fc_1.fmt,
-                             norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps)
-    assert torch.equal(g, ref), "fc_1/fc_2 SwiGLU GEMV differs"
-    # 5. mlp.proj + residual
-    run(5)
-    x1 = eng.buffer("x", 1).clone()
-    ref = ops.q4_gemv(eng.buffer("g", 0), m.proj.qweight, m.proj.scales, cfg.n_embd, cfg.intermediate_size,
-                      m.proj.group, m.proj.fmt, residual=eng.buffer("xp", 0))
-    assert torch.equal(x1, ref), "mlp.proj GEMV differs"
+    for l, blk in enumerate(model.transformer.h):
+        a, m = blk.attn, blk.mlp
+        k0 = 5 * l
+        # 1. RMSNorm + qkv GEMV on the engine's block input x_l
+        run(k0 + 1)
+        xl = eng.buffer("x", l).clone()
+        qkv = eng.buffer("qkv", l).clone()
+        ref = ops.q4_gemv(xl, a.attn.qweight, a.attn.scales, a.attn.out_features, cfg.n_embd, a.attn.group,
+                          a.attn.fmt, norm_weight=blk.norm_1.weight, eps=blk.norm_1.eps)
+        assert torch.equal(qkv, ref), f"layer {l}: qkv GEMV differs from lga_q4_gemv"
+        # 2. RoPE + KV append + attention (the per-op fused kernel on the engine's qkv, same caches)
+        run(k0 + 2)
+        y = eng.buffer("y", l).clone()
+        k_eng, v_eng = a.kv_cache.k.clone(), a.kv_cache.v.clone()
+        restore()
+        p = torch.tensor([T], device=DEV)
+        splits = ops.decode_splits(G, H // G, hs, a.kv_cache.k.size(-2))
+        y_ref = ops.attention_decode_fused(qkv.view(1, -1), a.kv_cache.k, a.kv_cache.v, p, p, cos, sin, H, G, hs, hs,
+                                           1.0 / math.sqrt(hs), splits)
+        assert torch.equal(k_eng, a.kv_cache.k) and torch.equal(v_eng, a.kv_cache.v), f"layer {l}: KV append differs"
+        assert _ulps_close(y, y_ref.view(-1)), (l, (y.float() - y_ref.view(-1).float()).abs().max())
+        # 3. o_proj + residual on the engine's attention output
+        run(k0 + 3)
+        xp = eng.buffer("xp", l).clone()
+        ref = ops.q4_gemv(eng.buffer("y", l), a.proj.qweight, a.proj.scales, cfg.n_embd, cfg.n_embd, a.proj.group,
+                          a.proj.fmt, residual=xl)
+        assert torch.equal(xp, ref), f"layer {l}: o_proj GEMV differs"
+        # 4. RMSNorm + fc_1 || fc_2 + SwiGLU
+        run(k0 + 4)
+        g = eng.buffer("g", l).clone()
+        ref = ops.q4_gemv_swiglu(eng.buffer("xp", l), m.fc_1.qweight, m.fc_1.scales, m.fc_2.qweight,
+                                 m.fc_2.scales, cfg.intermediate_size, cfg.n_embd, m.fc_1.group, m.fc_1.fmt,
+                                 norm_weight=blk.norm_2.weight, eps=blk.norm_2.eps)
+        assert torch.equal(g, ref), f"layer {l}: fc_1/fc_2 SwiGLU GEMV differs"
+        # 5. mlp.proj + residual
+        run(k0 + 5)
+        x1 = eng.buffer("x", l + 1).clone()
+        ref = ops.q4_gemv(eng.buffer("g", l), m.proj.qweight, m.proj.scales, cfg.n_embd, cfg.intermediate_size,
+                          m.proj.group, m.proj.fmt, residual=eng.buffer("xp", l))
+        assert torch.equal(x1, ref), f"layer {l}: mlp.proj GEMV differs"
     # 6. the whole step: ln_f + lm_head bit-exact on the engine's last activation, argmax, pos, next embedding
     tok = torch.zeros(1, dtype=torch.int32, device=DEV)
-    a.kv_cache.k.copy_(kc0)
-    a.kv_cache.v.copy_(vc0)
+    restore()
     eng.reset()
     eng.set_embedding(emb)
     pos = torch.tensor([T], device=DEV)

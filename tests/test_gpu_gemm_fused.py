@@ -1,0 +1,156 @@
+"""The prefill GEMM with the 4-bit dequantization fused in (lga_q4_gemm_fused / lga_q4_gemm_swiglu,
+csrc/gemm_q4f.hip) against the oracle.
+
+The reference's M > 1 Linear4bit path is dequantize_4bit to a bf16 weight, then the GEMM (bitsandbytes, reached
+through BitsandbytesPrecision, reference generate/base.py:128-136): the kernel stages exactly those bf16 weights
+(bf16(value(nibble) * scale), oracle/quant.py), so the product is compared with the fp64 product of the oracle's
+dequantized weights, within bf16 rounding (tolerance in each test). LLaMAMLP's fc_1 / fc_2 / silu*mul
+(reference model.py:712-716) is checked against bf16(bf16(silu(bf16(h1))) * bf16(h2)) of the fp64 products.
+Shapes: ragged M (1, 17, 300, 513), N tails (136, 392: not multiples of the 128-column tile), K of one K-step
+(64) up to Llama-2-7B's 11008, the 7B layer shapes at M = 2048 (fp32 GPU reference there).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import quant, synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def bf16_np(x):
+    return quant.bf16_bits_to_f32(quant.f32_to_bf16_bits(x))
+
+
+def to_dev(x):
+    return torch.from_numpy(np.ascontiguousarray(x, dtype=np.float32)).to(DEV).to(torch.bfloat16)
+
+
+@pytest.fixture(scope="module")
+def ops():
+    from lit_gpt import ops as _ops
+
+    _ops.load_library()
+    return _ops
+
+
+def _w(N, K, tag, std=0.02):
+    rng = np.random.default_rng(abs(hash((N, K, tag))) % (2 ** 31))
+    return rng.standard_normal((N, K), dtype=np.float32) * std
+
+
+def _quant(ops, w, fmt, group):
+    qw, sc = ops.quantize(torch.from_numpy(w).to(DEV), fmt, group)
+    p, s = quant.quantize_q4g(w, group) if fmt == 0 else quant.quantize_nf4(w, group)
+    wd = quant.dequantize_q4g(p, s, group) if fmt == 0 else quant.dequantize_nf4(p, s, group)
+    return qw, sc, bf16_np(wd)
+
+
+def _silu(v):
+    return v / (1.0 + np.exp(-v))
+
+
+def _swiglu_tol(a, b, g):
+    """Bound on |g - g_ref| when the two products' bf16 roundings may each differ by one ulp (different fp32
+    summation orders): |silu'| <= 1.1, so 2^-7 (1.1 |a| |b| + |silu(a)| |b|), + the final rounding + slack."""
+    sa = a / (1.0 + (-a).exp()) if isinstance(a, torch.Tensor) else _silu(a)
+    return 2 ** -7 * (1.1 * abs(a) * abs(b) + abs(sa) * abs(b)) + 2 ** -8 * abs(g) + 2e-3
+
+
+@pytest.mark.parametrize("fmt,group", [(0, 128), (0, 64), (1, 64)])
+@pytest.mark.parametrize("M,N,K", [(1, 128, 64), (17, 136, 256), (300, 392, 1024), (513, 256, 704)])
+@pytest.mark.parametrize("epi", ["none", "residual", "bias+residual"])
+def test_fused_gemm_matches_oracle(ops, fmt, group, M, N, K, epi):
+    if K % group:
+        pytest.skip("group must divide K")
+    assert ops.q4f_fits(M, N, K, group, fmt)
+    w = _w(N, K, "fg")
+    qw, sc, wd = _quant(ops, w, fmt, group)
+    x = bf16_np(synth.normal((M, K), f"fgx{M}x{K}", 5, 1.0))
+    res = bf16_np(synth.normal((M, N), "fgres", 5, 1.0)) if "residual" in epi else None
+    bias = bf16_np(synth.normal((N,), "fgb", 5, 0.1)) if "bias" in epi else None
+    y = ops.q4_gemm_fused(to_dev(x), qw, sc, N, K, group, fmt, bias=None if bias is None else to_dev(bias),
+                          residual=None if res is None else to_dev(res)).float().cpu().numpy()
+    h = x.astype(np.float64) @ wd.astype(np.float64).T
+    if bias is not None:
+        h = h + bias
+    ref = bf16_np(h.astype(np.float32))
+    if res is not None:
+        ref = ref + res
+    err = np.abs(y - ref) - (np.abs(ref) + np.abs(h)) * 2 ** -7
+    assert np.max(err) <= 2e-3, float(np.max(err))
+
+
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
+@pytest.mark.parametrize("M,N,K", [(1, 64, 128), (40, 200, 512), (300, 392, 1024)])
+def test_fused_swiglu_matches_oracle(ops, fmt, group, M, N, K):
+    w1, w2 = _w(N, K, "s1"), _w(N, K, "s2")
+    q1, s1, d1 = _quant(ops, w1, fmt, group)
+    q2, s2, d2 = _quant(ops, w2, fmt, group)
+    x = bf16_np(synth.normal((M, K), f"sx{M}x{K}", 5, 1.0))
+    g = ops.q4_gemm_swiglu(to_dev(x), q1, s1, q2, s2, N, K, group, fmt).float().cpu().numpy()
+    h1 = x.astype(np.float64) @ d1.astype(np.float64).T
+    h2 = x.astype(np.float64) @ d2.astype(np.float64).T
+    a = bf16_np(h1.astype(np.float32))
+    ref = bf16_np(bf16_np(_silu(a.astype(np.float64)).astype(np.float32)) * bf16_np(h2.astype(np.float32)))
+    err = np.abs(g - ref) - _swiglu_tol(a, bf16_np(h2.astype(np.float32)), ref)
+    assert np.max(err) <= 0.0, float(np.max(err))
+
+
+@pytest.mark.parametrize("M,N,K", [(2048, 4096, 4096), (2048, 4096, 11008), (257, 12288, 4096)])
+def test_fused_gemm_llama7b_shapes(ops, M, N, K):
+    """Full-size layer shapes: vs the fp32 product of the bit-exact dequantized weight (lga_q4_dequantize)."""
+    g = torch.Generator(device=DEV).manual_seed(M + N + K)
+    w = torch.randn(N, K, generator=g, device=DEV) * 0.02
+    qw, sc = ops.quantize(w, 0, 128)
+    wd = ops.q4_dequantize(qw, sc, N, K, 128, 0)
+    x = torch.randn(M, K, generator=g, device=DEV).to(torch.bfloat16)
+    res = torch.randn(M, N, generator=g, device=DEV).to(torch.bfloat16)
+    y = ops.q4_gemm_fused(x, qw, sc, N, K, 128, 0, residual=res).float()
+    h = x.float() @ wd.float().t()
+    ref = h.to(torch.bfloat16).float() + res.float()
+    err = (y - ref).abs() - (ref.abs() + h.abs()) * 2 ** -7
+    assert float(err.max()) <= 2e-3
+    # fc_1 || fc_2 + SwiGLU at the MLP shape
+    if K == 4096 and N == 4096:
+        I = 11008
+        w1 = torch.randn(I, K, generator=g, device=DEV) * 0.02
+        w2 = torch.randn(I, K, generator=g, device=DEV) * 0.02
+        q1, s1 = ops.quantize(w1, 0, 128)
+        q2, s2 = ops.quantize(w2, 0, 128)
+        gg = ops.q4_gemm_swiglu(x, q1, s1, q2, s2, I, K, 128, 0).float()
+        h1 = (x.float() @ ops.q4_dequantize(q1, s1, I, K, 128, 0).float().t()).to(torch.bfloat16)
+        h2 = (x.float() @ ops.q4_dequantize(q2, s2, I, K, 128, 0).float().t()).to(torch.bfloat16)
+        ref = ops.swiglu(h1.contiguous(), h2.contiguous()).float()
+        assert float((gg - ref).abs().sub(_swiglu_tol(h1.float(), h2.float(), ref)).max()) <= 0.0
+
+
+@pytest.mark.parametrize("M,N,K", [(17, 136, 256), (300, 392, 1024), (2048, 640, 4096)])
+def test_fused_bf16_weights(ops, M, N, K):
+    """fmt 2 (unquantized bf16 Linear, BASELINE config 2): the weight tile DMA'd as stored."""
+    w = to_dev(bf16_np(_w(N, K, "bw")))
+    x = to_dev(bf16_np(synth.normal((M, K), f"bwx{M}", 5, 1.0)))
+    bias = to_dev(bf16_np(synth.normal((N,), "bwb", 5, 0.1)))
+    y = ops.q4_gemm_fused(x, w, None, N, K, 64, 2, bias=bias).float()
+    h = x.float() @ w.float().t() + bias.float()
+    err = (y - h.to(torch.bfloat16).float()).abs() - h.abs() * 2 ** -7
+    assert float(err.max()) <= 2e-3
+    w2 = to_dev(bf16_np(_w(N, K, "bw2")))
+    g = ops.q4_gemm_swiglu(x, w, None, w2, None, N, K, 64, 2).float()
+    h1 = (x.float() @ w.float().t()).to(torch.bfloat16)
+    h2 = (x.float() @ w2.float().t()).to(torch.bfloat16)
+    ref = ops.swiglu(h1.contiguous(), h2.contiguous()).float()
+    assert float((g - ref).abs().sub(_swiglu_tol(h1.float(), h2.float(), ref)).max()) <= 0.0
+
+
+def test_fused_gemm_rejects_unsupported_shapes(ops):
+    assert not ops.q4f_fits(16, 128, 96, 32, 0)   # K % 64
+    assert not ops.q4f_fits(16, 132, 128, 64, 0)  # N % 8
+    assert not ops.q4f_fits(16, 128, 128, 32, 0)  # group < 64
+    x = torch.zeros(16, 96, dtype=torch.bfloat16, device=DEV)
+    qw = torch.zeros(128, 48, dtype=torch.uint8, device=DEV)
+    sc = torch.zeros(128, 3, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(RuntimeError, match="K % 64"):
+        ops.q4_gemm_fused(x, qw, sc, 128, 96, 32, 0)

@@ -37,14 +37,20 @@ for name, (N, K) in SHAPES.items():
     wb = ops.q4_dequantize(qw, sc, N, K, 128, 0)
     x = torch.randn(M, K, device=dev).bfloat16()
     fl = 2.0 * M * N * K
-    r = {"q4_gemm": timed(lambda: ops.q4_gemm(x, qw, sc, N, K, 128, 0)),
+    r = {"q4f": timed(lambda: ops.q4_gemm_fused(x, qw, sc, N, K, 128, 0)),
+         "q4_gemm": timed(lambda: ops.q4_gemm(x, qw, sc, N, K, 128, 0)),
          "dequant": timed(lambda: ops.q4_dequantize(qw, sc, N, K, 128, 0, out=wb)),
          "bf16_gemm": timed(lambda: ops.bf16_gemm(x, wb, impl="mfma")),
          "blaslt": timed(lambda: ops.bf16_gemm(x, wb, impl="blaslt")),
+         "q4f_bf16w": timed(lambda: ops.q4_gemm_fused(x, wb, None, N, K, 64, 2)),
          "torch_mm": timed(lambda: torch.matmul(x, wb.t()))}
+    if name == "fc":  # fc_1 || fc_2 + SwiGLU in one launch (counts as both GEMMs of the layer)
+        r["q4f_swiglu/2"] = timed(lambda: ops.q4_gemm_swiglu(x, qw, sc, qw, sc, N, K, 128, 0)) / 2
     for k, v in r.items():
-        tot[k] = tot.get(k, 0.0) + v
+        tot[k] = tot.get(k, 0.0) + v * (2 if name == "fc" else 1)
     print(f"{name:5s} N={N:6d} K={K:6d}  " + "  ".join(
         f"{k} {v:8.1f} us" + (f" ({fl / v / 1e6:6.1f} TF/s)" if k != "dequant" else
                               f" ({(N * K * 2.5) / v / 1e3:6.1f} GB/s)") for k, v in r.items()), flush=True)
-print("per layer: " + "  ".join(f"{k} {v:8.1f} us" for k, v in tot.items()) + "  (fc counted once; x2 in a layer)")
+print("per layer: " + "  ".join(f"{k} {v:8.1f} us" for k, v in tot.items()) + "  (fc counted twice)")
+fl_layer = 2.0 * M * sum(N * K * (2 if n == "fc" else 1) for n, (N, K) in SHAPES.items())
+print("per-layer TF/s: " + "  ".join(f"{k} {fl_layer / v / 1e6:6.1f}" for k, v in tot.items()), flush=True)
