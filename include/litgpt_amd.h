@@ -67,27 +67,22 @@ int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const
  * (4-bit) a power-of-two group >= 64 dividing K (lga_q4f_fits). Numerically the bnb path: bf16(value * scale)
  * weights, fp32 accumulation, one bf16 rounding (+bias), then + residual. */
 int lga_q4f_fits(int M, int N, int K, int group, int fmt);
+/* Short prompts split K across workgroups: the caller passes a zero-initialised workspace of at least this many
+ * bytes (0 = none needed) and keeps it for later calls (its per-tile counters are left zeroed). */
+size_t lga_q4f_workspace_bytes(int M, int N, int K, int swiglu);
 int lga_q4_gemm_fused(const void* x, const void* weight, const void* scales, const void* bias, const void* residual,
-                      void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
+                      void* y, int M, int N, int K, int group, int fmt, void* workspace, size_t workspace_bytes,
+                      lga_stream_t stream);
 /* LLaMAMLP prefill (lit_gpt/model.py:712-716): y (M, N) = bf16(silu(bf16(x W1^T))) * bf16(x W2^T), fc_1 and fc_2
  * in one launch (each tile computes 64 columns of both and applies the product in its epilogue). */
 int lga_q4_gemm_swiglu(const void* x, const void* qweight1, const void* scales1, const void* qweight2,
-                       const void* scales2, void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
+                       const void* scales2, void* y, int M, int N, int K, int group, int fmt, void* workspace,
+                       size_t workspace_bytes, lga_stream_t stream);
 /* bnb dequantize_4bit (the first half of the reference's M > 1 Linear4bit path): w (N, K) bf16 =
- * bf16(value(nibble) * scale) — the same bits lga_q4_gemm stages, so lga_bf16_gemm over w == lga_q4_gemm.
- * QuantLinear uses it for long prefills (M >= 512), where the bf16 GEMM's rate pays for the extra pass. */
+ * bf16(value(nibble) * scale) — the same bits lga_q4_gemm / lga_q4_gemm_fused stage, so lga_bf16_gemm over w ==
+ * lga_q4_gemm (tests, tools). */
 int lga_q4_dequantize(const uint8_t* qweight, const void* scales, void* w, int N, int K, int group, int fmt,
                       lga_stream_t stream);
-/* Long-prefill bf16 GEMM (the cuBLAS GEMM behind F.linear / after dequantize_4bit) on hipBLASLt: y (M, N) =
- * x (M, K) . W (N, K)^T [+bias] [+residual, added after the bf16 rounding of the product]. N, K multiples of 8;
- * `workspace` (may be NULL) of `workspace_bytes` is caller-owned scratch for split-K algorithms. */
-int lga_gemm_bf16_blaslt(const void* x, const void* weight, const void* bias, const void* residual, void* y, int M,
-                         int N, int K, void* workspace, size_t workspace_bytes, lga_stream_t stream);
-/* The same GEMM, and the (M, N, K, bias, workspace) plan is tuned: hipBLASLt's top heuristic candidates are timed
- * on these operands and the fastest is kept for every later lga_gemm_bf16_blaslt of the shape (synchronises the
- * stream; call at load, outside graph capture). */
-int lga_gemm_bf16_blaslt_tune(const void* x, const void* weight, const void* bias, const void* residual, void* y,
-                              int M, int N, int K, void* workspace, size_t workspace_bytes, lga_stream_t stream);
 
 /* -- unquantized bf16 Linears (BASELINE config 2: no --quantize, precision bf16-true; the reference runs
  *    F.linear on the bf16 nn.Linear weight, lit_gpt/model.py:619, :656, :712-716, :519) ------------------- */

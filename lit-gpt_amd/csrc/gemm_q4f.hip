@@ -3,26 +3,33 @@
 //
 // Replaces bitsandbytes' M > 1 path of `Linear4bit.forward` (dequantize_4bit into a bf16 weight, then the cuBLAS
 // GEMM; reached through BitsandbytesPrecision, reference generate/base.py:128-136) for the prefill pass
-// (next_token(model, arange(0, T), prompt), generate/base.py:83-85), and LLaMAMLP's fc_1 / fc_2 / silu product
-// (reference lit_gpt/model.py:712-716). The weight is never materialised in bf16 in HBM: each workgroup
-// dequantizes its [128 x 64] weight tile into LDS once per K-step, to exactly the bits bnb's dequantize_4bit
-// writes (bf16(value(nibble) * scale)), and every one of its 256 rows reads it from there.
+// (next_token(model, arange(0, T), prompt), generate/base.py:83-85), the bf16 F.linear of unquantized models
+// (lit_gpt/model.py:619,656), and LLaMAMLP's fc_1 / fc_2 / silu product (model.py:712-716). The weight is never
+// materialised in bf16 in HBM: each workgroup dequantizes its weight tile into LDS once per K-step, to exactly the
+// bits bnb's dequantize_4bit writes (bf16(value(nibble) * scale)), and every row of its tile reads it from there.
 //
 // MI355X design (CDNA4 playbook §5, "Pipelining across barriers"):
-//  * 256 x 128 output tile per 512-thread workgroup (8 waves as 4 (M) x 2 (N), 64 x 64 per wave =
-//    4 x 4 `v_mfma_f32_16x16x32_bf16` tiles, weight rows as the A operand so a lane's accumulators are 4
-//    consecutive output columns of one row: 8-byte stores). BM = 256 amortises the dequantization over 256 rows.
+//  * 8 waves per workgroup, 64 rows per wave; tiles <BM, BN> = <256, 128> for long prompts (4 (M) x 2 (N) waves,
+//    64 x 64 per wave = 4 x 4 `v_mfma_f32_16x16x32_bf16`) and <64, 128> / <64, 256> for short ones (1 x 8 waves);
+//    the weight rows are the A operand, so a lane's accumulators are 4 consecutive output columns of one row
+//    (8-byte stores).
 //  * X tiles and the packed weight / scale tiles reach LDS by LDS-DMA (`global_load_lds_dwordx4`, source-swizzled so
 //    the 128-B rows are XOR-swizzled for conflict-free `ds_read_b128`), X two K-steps ahead in 3 buffers, the packed
-//    weights three ahead in 4 (they are dequantized one K-step before use); one raw `s_barrier` per K-step after a
-//    COUNTED `s_waitcnt vmcnt`, so the DMAs stay in flight across the barrier (never `__syncthreads()`, whose
-//    vmcnt(0) would drain them); all LDS in one `__shared__` array; no other global loads inside the loop.
+//    weights three ahead in 4 (they are dequantized one K-step before use, between the MFMAs); one raw `s_barrier`
+//    per K-step after a COUNTED `s_waitcnt vmcnt`, so the DMAs stay in flight across the barrier (never
+//    `__syncthreads()`, whose vmcnt(0) would drain them); all LDS in one `__shared__` array; no other global loads
+//    inside the loop.
+//  * split-K for short prompts (few tiles): the K-slices of a tile write fp32 slabs, the last to arrive (agent
+//    release / acquire on a per-tile counter) sums them in slice order — deterministic — and runs the epilogue.
 //  * dequantization, int4-g: one `v_cvt_f32_ubyteN` per nibble, fma(n, s, -8 s) (exact: (n - 8) s needs 12
 //    significant bits) and `v_cvt_pk_bf16_f32` (round to nearest even) — the reference's bf16((n - 8) * s).
 //    nf4: bf16(NF4[n] * absmax) (fp32 product, as bnb's kernel) from an LDS table.
 //  * bf16 weights (unquantized Linear, BASELINE config 2): the weight tile is DMA'd like X (no dequantization).
 //  * tile order: m-tile fastest, so with 8 m-tiles (M = 2048) the blocks of one XCD (block id mod 8) share one
 //    X row panel in their L2 and stream distinct weight tiles.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 
 namespace lga {
@@ -30,34 +37,36 @@ namespace pf {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
-typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 64, NT = 512;
-// Tile shapes (8 waves, 64 x 64 outputs per wave either way): <BM, BN> = <256, 128> (4 (M) x 2 (N) waves) or
-// <128, 256> (2 x 4): the second halves the X bytes per FLOP — X (bf16) is the dominant on-chip traffic once the
-// weight is 4-bit — at twice the dequantization per FLOP.
-template <int BM_>
+
+template <int BM_, int BN_>
 struct Tile {
-  static constexpr int BM = BM_, BN = 32768 / BM_;
-  static constexpr int WM = BM / 64, WN = 8 / WM;          // wave grid
-  static constexpr int A_BYTES = BM * BK * 2;                // one X tile (BM rows x 128 B)
-  static constexpr int B_BYTES = BN * BK * 2;                // one bf16 weight tile
-  static constexpr int RAW_BYTES = BN * BK / 2;              // one packed weight tile (BN rows x 32 B)
-  static constexpr int SC_BYTES = 8 * 256;                   // one scale stage: a 256-B slot per wave
+  static constexpr int BM = BM_, BN = BN_;
+  static constexpr int WM = BM / 64, WN = 8 / WM;  // wave grid
+  static constexpr int WC = BN / WN;               // weight rows (output columns) per wave
+  static constexpr int FJ = WC / 16;               // 16-row weight fragments per wave
+  static constexpr int A_BYTES = BM * BK * 2;      // one X tile (BM rows x 128 B)
+  static constexpr int B_BYTES = BN * BK * 2;      // one bf16 weight tile
+  static constexpr int RAW_BYTES = BN * BK / 2;    // one packed weight tile (BN rows x 32 B)
+  static constexpr int SC_BYTES = 8 * 256;         // one scale stage: a 256-B slot per wave
   static constexpr int NA = 3, NRAW = 4, NWB = 2;
-  // LDS, 4-bit weights: A[3] | RAW[4] | SC[4] | WB[2] | nf4 table ; bf16 weights: A[3] | B[3]
+  // LDS, 4-bit weights: A[3] | RAW[4] | SC[4] | WB[2] | misc ; bf16 weights: A[3] | B[3] | misc
   static constexpr int OFF_RAW = NA * A_BYTES;
   static constexpr int OFF_SC = OFF_RAW + NRAW * RAW_BYTES;
   static constexpr int OFF_WB = OFF_SC + NRAW * SC_BYTES;
-  static constexpr int OFF_TAB = OFF_WB + NWB * B_BYTES;
-  static constexpr int LDS_Q4 = OFF_TAB + 64;
-  static constexpr int LDS_BF16 = NA * A_BYTES + NA * B_BYTES;
-  static constexpr int LDS_BYTES = LDS_Q4 > LDS_BF16 ? LDS_Q4 : LDS_BF16;
-  static constexpr int RAW_PER_THREAD = BN * BK / 2 / NT;    // packed bytes each thread dequantizes (8 or 16)
-  static constexpr int ROW_SHIFT = BN == 256 ? 1 : 2;        // dequant: thread -> weight-tile row tid >> ROW_SHIFT
+  static constexpr int END_Q4 = OFF_WB + NWB * B_BYTES;
+  static constexpr int END_BF16 = NA * A_BYTES + NA * B_BYTES;
+  static constexpr int OFF_MISC = END_Q4 > END_BF16 ? END_Q4 : END_BF16;  // nf4 table (64 B), last-arriver flag
+  static constexpr int LDS_BYTES = OFF_MISC + 128;
+  static constexpr int RPT = BN * BK / 2 / NT;     // packed bytes each thread dequantizes (8 or 16)
+  static constexpr int TPR = 32 / RPT;             // dequant threads per weight row
+  // DMAs per wave per stage: X pieces (8 rows x 128 B); bf16 weight pieces; packed weight + scale DMAs
+  static constexpr int APW = BM / 64, BPW = BN / 64, RAWPW = BN == 256 ? 2 : 1;
+  static_assert(WM * WN == 8 && FJ >= 1 && RPT >= 8, "tile shape");
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
-static_assert(Tile<256>::LDS_BYTES <= 163840 && Tile<128>::LDS_BYTES <= 163840, "LDS budget");
 
 __constant__ float kNF4f[16] = {
     -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
@@ -76,6 +85,9 @@ struct Args {
   uint16_t* y;               // [M][N]
   int M, N, K, G;
   int mt;                    // m-tiles
+  int splits;                // K-slices per tile (1: no split)
+  unsigned* counters;        // split-K: one per tile, zero between launches (the last arriver re-zeroes it)
+  float* slabs;              // split-K: [splits][M][N] fp32 partial products
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
@@ -93,9 +105,29 @@ __device__ __forceinline__ void cvt_ubytes(uint32_t w, float (&f)[4]) {
 
 template <int SIZE>
 __device__ __forceinline__ void glds(const void* src, unsigned char* lds) {
-  // the builtin's size must be a literal
+  // the builtin's size must be a literal; an LDS-DMA lane slot is 4 bytes wide for the sub-dword sizes
   if constexpr (SIZE == 16) __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
   else __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
+}
+
+// s_waitcnt vmcnt(N) / vmcnt(N) lgkmcnt(0) for a compile-time N (the count is an encoding field)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  static_assert(N >= 0 && N <= 8, "vmcnt");
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm() {
+  wait_vm<N>();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
 // 8 rows x 128 B of a row-major bf16 matrix into a swizzled tile: lane L lands at base + 16 L = row r0 + L/8,
@@ -107,25 +139,30 @@ __device__ __forceinline__ void glds_rows8(const uint16_t* src, int ld, int row,
   glds<16>(src + (size_t)min(r, row_max) * ld + k0 + lc * 8, lds_rows);
 }
 
-// FMT 0 int4-g (bf16 scales), 1 nf4 (fp32 absmax), 2 bf16 weights. DUAL: fc_1 || fc_2 + SwiGLU (tile = 64
-// columns of each; the weight tile's rows 0-63 are fc_1's, 64-127 fc_2's).
-template <int FMT, bool DUAL, int BM_>
+// FMT 0 int4-g (bf16 scales), 1 nf4 (fp32 absmax), 2 bf16 weights. DUAL: fc_1 || fc_2 + SwiGLU (tile = BN / 2
+// columns of each; the weight tile's rows [0, BN/2) are fc_1's, [BN/2, BN) fc_2's).
+template <int FMT, bool DUAL, int BM_, int BN_>
 __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
-  using T = Tile<BM_>;
-  constexpr int BM = T::BM, BN = T::BN, NA = T::NA, NRAW = T::NRAW;
+  using T = Tile<BM_, BN_>;
+  constexpr int BM = T::BM, BN = T::BN, NA = T::NA, NRAW = T::NRAW, FJ = T::FJ, WC = T::WC;
   constexpr int A_BYTES = T::A_BYTES, B_BYTES = T::B_BYTES, RAW_BYTES = T::RAW_BYTES, SC_BYTES = T::SC_BYTES;
-  constexpr int OFF_RAW = T::OFF_RAW, OFF_SC = T::OFF_SC, OFF_WB = T::OFF_WB, OFF_TAB = T::OFF_TAB;
+  constexpr int OFF_RAW = T::OFF_RAW, OFF_SC = T::OFF_SC, OFF_WB = T::OFF_WB, OFF_MISC = T::OFF_MISC;
+  static_assert(!DUAL || FJ % 2 == 0, "SwiGLU needs fc_1 and fc_2 fragments in pairs");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[T::LDS_BYTES];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int wm = wave % T::WM, wn = wave / T::WM;
-  const int m0 = (blockIdx.x % a.mt) * BM;
-  const int ntile = blockIdx.x / a.mt;
+  const int split = blockIdx.x % a.splits;
+  const int tile = blockIdx.x / a.splits;
+  const int m0 = (tile % a.mt) * BM;
   constexpr int TN = DUAL ? BN / 2 : BN;  // output columns per tile
-  const int n0 = ntile * TN;
-  const int nk = a.K / BK;
+  const int n0 = (tile / a.mt) * TN;
+  const int nk_all = a.K / BK;
+  const int per = (nk_all + a.splits - 1) / a.splits;
+  const int kt0 = split * per;
+  const int nk = max(0, min(nk_all, kt0 + per) - kt0);  // K-steps of this slice
   const int groups = a.K / (FMT == 2 ? 1 : a.G);
   const int gshift = FMT == 2 ? 0 : 31 - __builtin_clz((unsigned)a.G);
-  float* tab = (float*)(lds + OFF_TAB);
+  float* tab = (float*)(lds + OFF_MISC);
   if (FMT == 1 && tid < 16) tab[tid] = kNF4f[tid];
 
   // the weight tile's row r -> (matrix, row)
@@ -139,9 +176,9 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
     n = min(n, a.N - 1);
     return base + (size_t)n * (FMT == 2 ? (size_t)a.K * 2 : (size_t)a.K / 2);
   };
-  // scale index of weight-tile row r at K-step kt. The DMA moves 4 bytes per lane (an LDS-DMA lane slot is 4 bytes
-  // wide): a bf16 scale is fetched with its neighbour from the 4-byte-aligned pair holding it (in bounds: N * groups
-  // is even) and the reader picks the half by the index's parity.
+  // scale index of weight-tile row r at K-step kt (global). The DMA moves 4 bytes per lane: a bf16 scale is
+  // fetched with its neighbour from the 4-byte-aligned pair holding it (in bounds: N * groups is even) and the
+  // reader picks the half by the index's parity.
   auto sc_index = [&](int r, int kt) -> size_t {
     int n = n0 + r;
     if (DUAL && r >= BN / 2) n = n0 + r - BN / 2;
@@ -154,36 +191,33 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
     return base + (FMT == 0 ? (i & ~(size_t)1) * 2 : i * 4);
   };
 
-  // ---- stage issue (every wave issues the same number of DMAs per group, so one count serves all) ----
-  // X tile kt: BM / 64 pieces of 8 rows per wave
-  constexpr int APW = BM / 64;
-  auto issue_a = [&](int kt) {
-    unsigned char* A = lds + (kt % NA) * A_BYTES;
+  // ---- stage issue; `lk` is the slice-local K-step (buffer index), kt0 + lk the global one. Every wave issues
+  // the same number of DMAs per stage, so one count serves all ----
+  auto issue_a = [&](int lk) {
+    unsigned char* A = lds + (lk % NA) * A_BYTES;
 #pragma unroll
-    for (int i = 0; i < APW; ++i) {
-      const int r0 = (wave * APW + i) * 8;
-      glds_rows8(a.x, a.K, m0 + r0, a.M - 1, kt * BK, A + r0 * 128, lane);
+    for (int i = 0; i < T::APW; ++i) {
+      const int r0 = (wave * T::APW + i) * 8;
+      glds_rows8(a.x, a.K, m0 + r0, a.M - 1, (kt0 + lk) * BK, A + r0 * 128, lane);
     }
   };
-  // bf16 weight tile kt (FMT 2): BN / 64 pieces of 8 rows per wave
-  constexpr int BPW = BN / 64;
-  auto issue_b16 = [&](int kt) {
-    unsigned char* B = lds + NA * A_BYTES + (kt % NA) * B_BYTES;
+  auto issue_b16 = [&](int lk) {  // bf16 weight tile (FMT 2)
+    unsigned char* B = lds + NA * A_BYTES + (lk % NA) * B_BYTES;
 #pragma unroll
-    for (int i = 0; i < BPW; ++i) {
-      const int r0 = (wave * BPW + i) * 8;
+    for (int i = 0; i < T::BPW; ++i) {
+      const int r0 = (wave * T::BPW + i) * 8;
       const int r = r0 + (lane >> 3);
       const int lc = (lane & 7) ^ (r & 7);
-      glds<16>(wrow_ptr(r) + (size_t)kt * BK * 2 + lc * 16, B + r0 * 128);
+      glds<16>(wrow_ptr(r) + (size_t)(kt0 + lk) * BK * 2 + lc * 16, B + r0 * 128);
     }
   };
-  // packed weight tile kt (1 KB = 32 rows x 32 B per DMA) and its scales (256 B = 64 rows x 4 B per DMA).
+  // packed weight tile (1 KB = 32 rows x 32 B per DMA) and its scales (256 B = 64 rows x 4 B per DMA).
   // BN = 256: every wave one of each (waves 4-7 repeat the scales of 0-3 into their own slots);
   // BN = 128: waves 4-7 the packed rows, waves 0-3 the scales (2, 3 repeat 0, 1): one DMA per wave.
-  constexpr int RAW_DMAS = BN == 256 ? 2 : 1;
-  auto issue_raw = [&](int kt) {
-    unsigned char* R = lds + OFF_RAW + (kt % NRAW) * RAW_BYTES;
-    unsigned char* S = lds + OFF_SC + (kt % NRAW) * SC_BYTES + wave * 256;
+  auto issue_raw = [&](int lk) {
+    const int kt = kt0 + lk;
+    unsigned char* R = lds + OFF_RAW + (lk % NRAW) * RAW_BYTES;
+    unsigned char* S = lds + OFF_SC + (lk % NRAW) * SC_BYTES + wave * 256;
     const int sw = wave & (BN / 64 - 1);  // the 64-row scale block this wave fetches
     if (BN == 256) {
       const int r = wave * 32 + (lane >> 1);
@@ -197,26 +231,25 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
     }
   };
 
-  // ---- dequantization of packed tile kt into bf16 image buffer kt & 1: thread t -> row t / 4, 16 weights ----
-  // The LDS reads are inline asm: their data is ordered by the counted vmcnt + barrier of the loop, and hipcc would
-  // otherwise drain every LDS-DMA in flight (vmcnt(0)) before them, as it cannot tell the buffers apart.
-  // (split in three so the math can sit between the MFMAs: the reads are issued before the K-step's first MFMA
-  // group, the bf16 image is written after its last)
-  // thread -> weight-tile row dq_r, packed bytes [dq_q * RPT, +RPT) of its 32 (RPT = 8 or 16 weights' bytes)
-  constexpr int RPT = T::RAW_PER_THREAD, NDW = RPT / 4;
-  const int dq_r = tid >> T::ROW_SHIFT, dq_q = tid & ((1 << T::ROW_SHIFT) - 1);
+  // ---- dequantization of packed stage lk into bf16 image buffer lk & 1 ----
+  // thread -> weight-tile row dq_r, packed bytes [dq_q * RPT, +RPT) of its 32. The LDS reads / writes are inline
+  // asm: their data is ordered by the counted vmcnt + barrier of the loop, and hipcc would otherwise drain every
+  // LDS-DMA in flight (vmcnt(0)) before them, as it cannot tell the buffers apart. Split in three so the math can
+  // sit between the MFMAs: the reads are issued before the K-step's first MFMA group, the image written after.
+  constexpr int RPT = T::RPT, NDW = RPT / 4;
+  const int dq_r = tid / T::TPR, dq_q = tid % T::TPR;
   typedef uint32_t raw_t __attribute__((ext_vector_type(NDW)));
-  auto dq_load = [&](int kt, raw_t& wv, uint32_t& sb) {
-    const unsigned raw_a = lds_addr(lds + OFF_RAW + (kt % NRAW) * RAW_BYTES + dq_r * 32 + dq_q * RPT);
+  auto dq_load = [&](int lk, raw_t& wv, uint32_t& sb) {
+    const unsigned raw_a = lds_addr(lds + OFF_RAW + (lk % NRAW) * RAW_BYTES + dq_r * 32 + dq_q * RPT);
     // the scale of row r sits in the slot of the wave that fetched its 64-row block (wave r / 64)
-    const unsigned sc_a = lds_addr(lds + OFF_SC + (kt % NRAW) * SC_BYTES + (dq_r >> 6) * 256 + (dq_r & 63) * 4 +
-                                   (FMT == 0 ? (int)(sc_index(dq_r, kt) & 1) * 2 : 0));
-    if (NDW == 4) {
+    const unsigned sc_a = lds_addr(lds + OFF_SC + (lk % NRAW) * SC_BYTES + (dq_r >> 6) * 256 + (dq_r & 63) * 4 +
+                                   (FMT == 0 ? (int)(sc_index(dq_r, kt0 + lk) & 1) * 2 : 0));
+    if constexpr (NDW == 4) {
       if (FMT == 0)
         asm volatile("ds_read_b128 %0, %2\n\tds_read_u16 %1, %3" : "=&v"(wv), "=&v"(sb) : "v"(raw_a), "v"(sc_a) : "memory");
       else
         asm volatile("ds_read_b128 %0, %2\n\tds_read_b32 %1, %3" : "=&v"(wv), "=&v"(sb) : "v"(raw_a), "v"(sc_a) : "memory");
-    } else {
+    } else if constexpr (NDW == 2) {
       if (FMT == 0)
         asm volatile("ds_read_b64 %0, %2\n\tds_read_u16 %1, %3" : "=&v"(wv), "=&v"(sb) : "v"(raw_a), "v"(sc_a) : "memory");
       else
@@ -249,130 +282,173 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
       }
     }
   };
-  auto dq_store = [&](int kt, const uint32_t (&o)[4 * NDW]) {
-    unsigned char* WB = lds + OFF_WB + (kt & 1) * B_BYTES;
+  auto dq_store = [&](int lk, const uint32_t (&o)[4 * NDW]) {
+    unsigned char* WB = lds + OFF_WB + (lk & 1) * B_BYTES;
+    {
 #pragma unroll
-    for (int h = 0; h < NDW; ++h) {  // 16-B chunk (dq_q * NDW + h) of the 128-B bf16 row
-      const unsigned wa = lds_addr(WB + swz(dq_r, dq_q * NDW + h));
-      const u32x4 ov = {o[4 * h], o[4 * h + 1], o[4 * h + 2], o[4 * h + 3]};
-      asm volatile("ds_write_b128 %0, %1" :: "v"(wa), "v"(ov) : "memory");
+      for (int h = 0; h < NDW; ++h) {  // 16-B chunk (dq_q * NDW + h) of the 128-B bf16 row
+        const unsigned wa = lds_addr(WB + swz(dq_r, dq_q * NDW + h));
+        const u32x4 ov = {o[4 * h], o[4 * h + 1], o[4 * h + 2], o[4 * h + 3]};
+        asm volatile("ds_write_b128 %0, %1" :: "v"(wa), "v"(ov) : "memory");
+      }
     }
   };
-  auto dequant = [&](int kt) {
+  auto dequant = [&](int lk) {
     raw_t wv;
     uint32_t sb, o[4 * NDW];
-    dq_load(kt, wv, sb);
+    dq_load(lk, wv, sb);
     dq_wait(wv, sb);
     dq_math(wv, sb, o);
-    dq_store(kt, o);
+    dq_store(lk, o);
   };
 
-  // accumulators: acc[j][i] = weight rows (j) x X rows (i) of this wave
-  f32x4_t acc[4][4];
+  // accumulators: acc[j][i] = weight rows (fragment j) x X rows (fragment i) of this wave
+  f32x4_t acc[FJ][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
+  for (int j = 0; j < FJ; ++j)
 #pragma unroll
     for (int i = 0; i < 4; ++i) acc[j][i] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const int fr = lane & 15, fk = lane >> 4;
-  // weight-tile row of fragment j
-  // (SwiGLU: fragments 0, 1 are fc_1 columns wn * 32 .. + 32, fragments 2, 3 the same fc_2 columns)
-  auto brow = [&](int j) { return DUAL ? (j >> 1) * (BN / 2) + wn * 32 + (j & 1) * 16 : wn * 64 + j * 16; };
-
+  // weight-tile row of fragment j (SwiGLU: the first FJ/2 fragments are fc_1 rows, the rest the same fc_2 rows)
+  auto brow = [&](int j) {
+    return DUAL ? (j / (FJ / 2)) * (BN / 2) + wn * (WC / 2) + (j % (FJ / 2)) * 16 : wn * WC + j * 16;
+  };
   auto mfma_sub = [&](const unsigned char* A, const unsigned char* B, int sub) {
-    {
-      bf16x8_t af[4], bfr[4];
+    bf16x8_t af[4], bfr[FJ];
+#pragma unroll
+    for (int j = 0; j < FJ; ++j) bfr[j] = *(const bf16x8_t*)(B + swz(brow(j) + fr, sub * 4 + fk));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8_t*)(A + swz(wm * 64 + i * 16 + fr, sub * 4 + fk));
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[j][i], 0, 0, 0);
+  };
+
+  if (nk > 0) {
+    if (FMT == 2) {
+      // X and W both DMA'd two K-steps ahead into 3 buffers: G = APW + BPW DMAs per wave per stage
+      constexpr int G = T::APW + T::BPW;
+      issue_a(0);
+      issue_b16(0);
+      if (nk > 1) {
+        issue_a(1);
+        issue_b16(1);
+        wait_vm<G>();
+      } else {
+        wait_vm<0>();
+      }
+      __builtin_amdgcn_s_barrier();
+      for (int lk = 0; lk < nk; ++lk) {
+        const bool full = lk + 2 < nk;
+        if (full) {
+          issue_a(lk + 2);
+          issue_b16(lk + 2);
+        }
+        const unsigned char* A = lds + (lk % NA) * A_BYTES;
+        const unsigned char* B = lds + NA * A_BYTES + (lk % NA) * B_BYTES;
+        mfma_sub(A, B, 0);
+        mfma_sub(A, B, 1);
+        if (full) wait_vm_lgkm<G>();
+        else wait_vm_lgkm<0>();
+        __builtin_amdgcn_s_barrier();
+      }
+    } else {
+      // G = APW + RAWPW DMAs per wave per stage. Prologue: {A0, raw0, raw1} {A1, raw2}; raw0 -> WB0
+      constexpr int G = T::APW + T::RAWPW;
+      issue_a(0);
+      issue_raw(0);
+      if (nk > 1) issue_raw(1);
+      if (nk > 1) issue_a(1);
+      if (nk > 2) issue_raw(2);
+      if (nk > 2) wait_vm<G>();
+      else wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+      dequant(0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      // iteration lk: issue {A(lk+2), raw(lk+3)}; MFMA on A(lk), WB(lk) with raw(lk+1) dequantized between the
+      // two MFMA groups; wait for {A(lk+1), raw(lk+2)} (issued one iteration earlier); barrier
+      for (int lk = 0; lk < nk; ++lk) {
+        const bool full = lk + 3 < nk;
+        if (lk + 2 < nk) issue_a(lk + 2);
+        if (full) issue_raw(lk + 3);
+        // past the last stage this dequantizes a stale raw buffer into the bf16 buffer nobody reads again: no
+        // branch, so the math can interleave with the MFMAs
+        const unsigned char* A = lds + (lk % NA) * A_BYTES;
+        const unsigned char* B = lds + OFF_WB + (lk & 1) * B_BYTES;
+        raw_t wv;
+        uint32_t sb, o[4 * NDW];
+        dq_load(lk + 1, wv, sb);
+        mfma_sub(A, B, 0);
+        dq_wait(wv, sb);
+        dq_math(wv, sb, o);
+        mfma_sub(A, B, 1);
+        dq_store(lk + 1, o);
+        if (full) wait_vm_lgkm<G>();
+        else wait_vm_lgkm<0>();
+        __builtin_amdgcn_s_barrier();
+      }
+    }
+  }
+
+  // ---- split-K: slabs, then the tile's last slice sums them in slice order ----
+  if (a.splits > 1) {
+    constexpr int NJ = FJ;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      // column in the slab's [N] (SwiGLU: fc_1 and fc_2 partials side by side, [2][M][N])
+      const int jj = DUAL ? j % (FJ / 2) : j;
+      const int n = n0 + (DUAL ? wn * (WC / 2) : wn * WC) + jj * 16 + fk * 4;
+      if (n >= a.N) continue;
+      float* slab = a.slabs + ((size_t)split * (DUAL ? 2 : 1) + (DUAL ? j / (FJ / 2) : 0)) * a.M * a.N;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        bfr[i] = *(const bf16x8_t*)(B + swz(brow(i) + fr, sub * 4 + fk));
-        af[i] = *(const bf16x8_t*)(A + swz(wm * 64 + i * 16 + fr, sub * 4 + fk));
+        const int m = m0 + wm * 64 + i * 16 + fr;
+        if (m < a.M) *(f32x4_t*)(slab + (size_t)m * a.N + n) = acc[j][i];
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[j][i], 0, 0, 0);
     }
-  };
-
-  auto mfma_step = [&](const unsigned char* A, const unsigned char* B) {
-    mfma_sub(A, B, 0);
-    mfma_sub(A, B, 1);
-  };
-
-  static_assert(APW + BPW == 6 && APW + RAW_DMAS == 4 + (BN == 256 ? 0 : 1), "vmcnt counts below");
-  if (FMT == 2) {
-    // X and W both DMA'd two K-steps ahead into 3 buffers: APW + BPW = 6 DMAs per wave per stage
-    issue_a(0);
-    issue_b16(0);
-    if (nk > 1) {
-      issue_a(1);
-      issue_b16(1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* last = (unsigned*)(lds + OFF_MISC + 64);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool full = kt + 2 < nk;
-      if (full) {
-        issue_a(kt + 2);
-        issue_b16(kt + 2);
+      const unsigned old = __hip_atomic_fetch_add(a.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool is_last = old == (unsigned)a.splits - 1;
+      if (is_last) {
+        a.counters[tile] = 0u;  // ready for the next launch (stream-ordered after this one)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      mfma_step(lds + (kt % NA) * A_BYTES, lds + NA * A_BYTES + (kt % NA) * B_BYTES);
-      if (full) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      *last = is_last ? 1u : 0u;
     }
-  } else {
-    // prologue: {A0, raw0, raw1} {A1, raw2}; raw0 -> WB0
-    issue_a(0);
-    issue_raw(0);
-    if (nk > 1) issue_raw(1);
-    if (nk > 1) issue_a(1);
-    if (nk > 2) issue_raw(2);
-    // {A1, raw2} = APW + RAW_DMAS = 4 (BN 256) / 5 (BN 128) DMAs per wave may stay in flight
-    if (nk > 2) {
-      if (BN == 256) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    dequant(0);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    // iteration kt: issue {A(kt+2), raw(kt+3)}; MFMA on A(kt), WB(kt); dequant raw(kt+1); wait for
-    // {A(kt+1), raw(kt+2)} (issued one iteration earlier); barrier
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool full = kt + 3 < nk;
-      if (kt + 2 < nk) issue_a(kt + 2);
-      if (full) issue_raw(kt + 3);
-      // dequantize stage kt + 1 around this step's MFMAs (past the last stage it reads a stale raw buffer into the
-      // bf16 buffer nobody reads again: no branch, so the math can interleave with the MFMAs)
-      const unsigned char* A = lds + (kt % NA) * A_BYTES;
-      const unsigned char* B = lds + OFF_WB + (kt & 1) * B_BYTES;
-      raw_t wv;
-      uint32_t sb, o[4 * NDW];
-      dq_load(kt + 1, wv, sb);
-      mfma_sub(A, B, 0);
-      dq_wait(wv, sb);
-      dq_math(wv, sb, o);
-      mfma_sub(A, B, 1);
-      dq_store(kt + 1, o);
-      if (full) {
-        if (BN == 256) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(5) lgkmcnt(0)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (*last == 0u) return;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int jj = DUAL ? j % (FJ / 2) : j;
+      const int n = n0 + (DUAL ? wn * (WC / 2) : wn * WC) + jj * 16 + fk * 4;
+      if (n >= a.N) continue;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + wm * 64 + i * 16 + fr;
+        if (m >= a.M) continue;
+        f32x4_t t = f32x4_t{0.f, 0.f, 0.f, 0.f};
+        for (int s = 0; s < a.splits; ++s) {
+          const float* slab = a.slabs + ((size_t)s * (DUAL ? 2 : 1) + (DUAL ? j / (FJ / 2) : 0)) * a.M * a.N;
+          t += *(const f32x4_t*)(slab + (size_t)m * a.N + n);
+        }
+        acc[j][i] = t;
       }
-      __builtin_amdgcn_s_barrier();
     }
   }
 
   // ---- epilogue: lane holds columns (fk * 4 + r) of weight fragment j for X row fr of fragment i ----
   if (DUAL) {
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 32 + j * 16 + fk * 4;
+    for (int j = 0; j < FJ / 2; ++j) {
+      const int n = n0 + wn * (WC / 2) + j * 16 + fk * 4;
       if (n >= a.N) continue;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -385,7 +461,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
 #pragma unroll
           for (int e = 0; e < 2; ++e) {
             const float gate = round_bf(silu_f(round_bf(acc[j][i][r + e])));  // bf16(silu(bf16(fc_1 x)))
-            g[e] = __fmul_rn(gate, round_bf(acc[j + 2][i][r + e]));           // * bf16(fc_2 x)
+            g[e] = __fmul_rn(gate, round_bf(acc[j + FJ / 2][i][r + e]));      // * bf16(fc_2 x)
           }
           o[r / 2] = pack2(g[0], g[1]);
         }
@@ -394,8 +470,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
     }
   } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wn * 64 + j * 16 + fk * 4;
+    for (int j = 0; j < FJ; ++j) {
+      const int n = n0 + wn * WC + j * 16 + fk * 4;
       if (n >= a.N) continue;
       float b[4] = {0.f, 0.f, 0.f, 0.f};
       if (a.bias) {
@@ -426,6 +502,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
 }  // namespace lga
 
 namespace {
+using lga::pf::Args;
+
 // the fused kernel's shape contract (the callers fall back to gemm.hip's 128 x 128 tiles outside it)
 bool q4f_fits(int M, int N, int K, int group, int fmt) {
   if (M < 1 || N < 8 || N % 8 || K < lga::pf::BK || K % lga::pf::BK) return false;
@@ -433,66 +511,98 @@ bool q4f_fits(int M, int N, int K, int group, int fmt) {
   return group >= lga::pf::BK && (group & (group - 1)) == 0 && K % group == 0;
 }
 
-// tile choice: 128 x 256 for 4-bit weights (half the X traffic per FLOP), 256 x 128 for bf16 weights (whose tile
-// bytes are then balanced); LGA_Q4F_BM=256 / 128 overrides (lab A/B)
-int q4f_bm(int fmt) {
-  static const int env = [] {
-    const char* e = getenv("LGA_Q4F_BM");
-    return e ? atoi(e) : 0;
-  }();
-  if (env == 128 || env == 256) return env;
-  return fmt == 2 ? 256 : 128;
+// Launch plan: tile shape by M, then K-slices so the grid covers the CUs (>= 2 waves of tiles is left whole).
+struct Plan {
+  int bm, bn, mt, tn, tiles, splits;
+};
+Plan q4f_plan(int M, int N, int K, bool dual) {
+  Plan p;
+  p.bm = M <= 128 ? 64 : 256;
+  p.bn = p.bm == 64 ? (dual ? 256 : 128) : 128;
+  p.mt = (M + p.bm - 1) / p.bm;
+  p.tn = dual ? p.bn / 2 : p.bn;
+  p.tiles = p.mt * ((N + p.tn - 1) / p.tn);
+  const int nk = K / lga::pf::BK;
+  int s = 1;
+  // each slice keeps >= 4 K-steps; aim at ~256 workgroups
+  while (p.tiles * s * 2 <= 256 && nk / (s * 2) >= 4) s *= 2;
+  if (const char* e = getenv("LGA_Q4F_SPLITS")) s = std::max(1, std::min(atoi(e), nk));
+  p.splits = s;
+  return p;
 }
 
-template <int FMT, bool DUAL, int BM>
-int launch_q4f_bm(lga::pf::Args a, hipStream_t stream) {
-  using T = lga::pf::Tile<BM>;
-  a.mt = (a.M + BM - 1) / BM;
-  const int tn = DUAL ? T::BN / 2 : T::BN;
-  const unsigned grid = (unsigned)(a.mt * ((a.N + tn - 1) / tn));
-  lga::pf::gemm_q4f_kernel<FMT, DUAL, BM><<<grid, lga::pf::NT, 0, stream>>>(a);
+template <int FMT, bool DUAL, int BM, int BN>
+int launch_tile(Args a, const Plan& p, hipStream_t stream) {
+  a.mt = p.mt;
+  a.splits = p.splits;
+  const unsigned grid = (unsigned)(p.tiles * p.splits);
+  lga::pf::gemm_q4f_kernel<FMT, DUAL, BM, BN><<<grid, lga::pf::NT, 0, stream>>>(a);
   LGA_LAUNCH_RETURN();
 }
 
 template <int FMT, bool DUAL>
-int launch_q4f(const lga::pf::Args& a, hipStream_t stream) {
-  return q4f_bm(FMT) == 256 ? launch_q4f_bm<FMT, DUAL, 256>(a, stream) : launch_q4f_bm<FMT, DUAL, 128>(a, stream);
+int launch_q4f(Args a, const Plan& p, hipStream_t stream) {
+  if (p.bm == 256) return launch_tile<FMT, DUAL, 256, 128>(a, p, stream);
+  if (DUAL || p.bn == 256) return launch_tile<FMT, DUAL, 64, 256>(a, p, stream);
+  return launch_tile<FMT, false, 64, 128>(a, p, stream);
+}
+
+size_t ws_need(const Plan& p, int M, int N, bool dual) {
+  if (p.splits == 1) return 0;
+  return 4096 + (size_t)p.splits * (dual ? 2 : 1) * M * N * 4;
+}
+
+int run(Args a, int fmt, bool dual, void* ws, size_t ws_bytes, hipStream_t stream) {
+  const Plan p = q4f_plan(a.M, a.N, a.K, dual);
+  if (p.splits > 1) {
+    LGA_CHECK_ARG(ws && ws_bytes >= ws_need(p, a.M, a.N, dual) && p.tiles <= 1024,
+                  "lga_q4_gemm_fused: split-K needs the workspace lga_q4f_workspace_bytes reports");
+    a.counters = (unsigned*)ws;
+    a.slabs = (float*)((unsigned char*)ws + 4096);
+  }
+  switch (fmt * 2 + (dual ? 1 : 0)) {
+    case 0: return launch_q4f<0, false>(a, p, stream);
+    case 1: return launch_q4f<0, true>(a, p, stream);
+    case 2: return launch_q4f<1, false>(a, p, stream);
+    case 3: return launch_q4f<1, true>(a, p, stream);
+    case 4: return launch_q4f<2, false>(a, p, stream);
+    default: return launch_q4f<2, true>(a, p, stream);
+  }
 }
 }  // namespace
 
 extern "C" int lga_q4f_fits(int M, int N, int K, int group, int fmt) { return q4f_fits(M, N, K, group, fmt) ? 1 : 0; }
 
+extern "C" size_t lga_q4f_workspace_bytes(int M, int N, int K, int swiglu) {
+  if (M < 1 || N < 1 || K < lga::pf::BK) return 0;
+  const Plan p = q4f_plan(M, N, K, swiglu != 0);
+  return ws_need(p, M, N, swiglu != 0);
+}
+
 extern "C" int lga_q4_gemm_fused(const void* x, const void* weight, const void* scales, const void* bias,
                                  const void* residual, void* y, int M, int N, int K, int group, int fmt,
-                                 hipStream_t stream) {
+                                 void* workspace, size_t workspace_bytes, hipStream_t stream) {
   LGA_CHECK_ARG(x && weight && y && (fmt == 2 || scales), "lga_q4_gemm_fused: null pointer");
   LGA_CHECK_ARG(fmt >= 0 && fmt <= 2, "lga_q4_gemm_fused: fmt must be 0 (int4-g), 1 (nf4) or 2 (bf16)");
   LGA_CHECK_ARG(q4f_fits(M, N, K, group, fmt),
                 "lga_q4_gemm_fused: needs N % 8 == 0, K % 64 == 0 and a power-of-two group >= 64 dividing K");
   LGA_CHECK_ARG(((uintptr_t)x | (uintptr_t)weight | (uintptr_t)y | (uintptr_t)residual) % 16 == 0,
                 "lga_q4_gemm_fused: x, weight, residual and y must be 16-B aligned");
-  lga::pf::Args a{(const uint16_t*)x, weight, scales, nullptr, nullptr, (const uint16_t*)bias,
-                  (const uint16_t*)residual, (uint16_t*)y, M, N, K, fmt == 2 ? 64 : group, 1};
-  switch (fmt) {
-    case 0: return launch_q4f<0, false>(a, stream);
-    case 1: return launch_q4f<1, false>(a, stream);
-    default: return launch_q4f<2, false>(a, stream);
-  }
+  Args a{(const uint16_t*)x, weight, scales, nullptr, nullptr, (const uint16_t*)bias, (const uint16_t*)residual,
+         (uint16_t*)y, M, N, K, fmt == 2 ? 64 : group, 1, 1, nullptr, nullptr};
+  return run(a, fmt, false, workspace, workspace_bytes, stream);
 }
 
 extern "C" int lga_q4_gemm_swiglu(const void* x, const void* qw1, const void* sc1, const void* qw2, const void* sc2,
-                                  void* y, int M, int N, int K, int group, int fmt, hipStream_t stream) {
+                                  void* y, int M, int N, int K, int group, int fmt, void* workspace,
+                                  size_t workspace_bytes, hipStream_t stream) {
   LGA_CHECK_ARG(x && qw1 && qw2 && y && (fmt == 2 || (sc1 && sc2)), "lga_q4_gemm_swiglu: null pointer");
   LGA_CHECK_ARG(fmt >= 0 && fmt <= 2, "lga_q4_gemm_swiglu: fmt must be 0 (int4-g), 1 (nf4) or 2 (bf16)");
   LGA_CHECK_ARG(q4f_fits(M, N, K, group, fmt),
                 "lga_q4_gemm_swiglu: needs N % 8 == 0, K % 64 == 0 and a power-of-two group >= 64 dividing K");
   LGA_CHECK_ARG(((uintptr_t)x | (uintptr_t)qw1 | (uintptr_t)qw2 | (uintptr_t)y) % 16 == 0,
                 "lga_q4_gemm_swiglu: x, weights and y must be 16-B aligned");
-  lga::pf::Args a{(const uint16_t*)x, qw1, sc1, qw2, sc2, nullptr, nullptr, (uint16_t*)y, M, N, K,
-                  fmt == 2 ? 64 : group, 1};
-  switch (fmt) {
-    case 0: return launch_q4f<0, true>(a, stream);
-    case 1: return launch_q4f<1, true>(a, stream);
-    default: return launch_q4f<2, true>(a, stream);
-  }
+  Args a{(const uint16_t*)x, qw1, sc1, qw2, sc2, nullptr, nullptr, (uint16_t*)y, M, N, K, fmt == 2 ? 64 : group, 1,
+         1, nullptr, nullptr};
+  return run(a, fmt, true, workspace, workspace_bytes, stream);
 }

@@ -136,8 +136,8 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
     ``rope_positions="reference"`` builds the rope tables under a bf16 default dtype, as the reference's
     ``with fabric.init_tensor(): model.max_seq_length = ...`` does under bf16-true / bnb precision
     (generate/base.py:153-157): positions above 256 round to bf16. ``"exact"`` keeps fp32 positions.
-    ``prefill_rows``: the prompt length about to be served — its prefill GEMM plans are tuned at load
-    (ops.tune_prefill_gemms)."""
+    ``prefill_rows`` (the prompt length about to be served) is accepted for API stability; the prefill GEMMs are
+    hand-written (csrc/gemm_q4f.hip) and need no per-shape tuning or warm-up."""
     if rope_positions not in ("reference", "exact"):
         raise ValueError(f"rope_positions must be 'reference' or 'exact', got {rope_positions!r}")
     from lit_gpt.quantize import QuantizedPrecision
@@ -209,12 +209,6 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
     finally:
         torch.set_default_dtype(prev)
     model.set_kv_cache(batch_size=1, device=device)
-    # the prefill's library GEMM (hipBLASLt) loads its kernels on first use: do it here, at load, not in the prompt
-    from lit_gpt import ops
-
-    ops.warm_gemm_library(device, K=config.n_embd)
-    if prefill_rows:  # the served prompt length is known: tune its prefill GEMMs now, not in the first prompt
-        ops.tune_prefill_gemms(model, prefill_rows)
     return model.eval()
 
 

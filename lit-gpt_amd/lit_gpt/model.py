@@ -78,9 +78,7 @@ def _dense(linear: nn.Linear, x: torch.Tensor, *, residual: Optional[torch.Tenso
 
 
 def _fused_prefill(M: int, N: int, K: int, group: int, fmt: int) -> bool:
-    from lit_gpt import quantize
-
-    return quantize.PREFILL_GEMM == "fused" and M >= quantize.FUSED_GEMM_MIN_M and ops.q4f_fits(M, N, K, group, fmt)
+    return M > 1 and ops.q4f_fits(M, N, K, group, fmt)
 
 
 def _lin(linear: nn.Module, x: torch.Tensor, **kw) -> torch.Tensor:

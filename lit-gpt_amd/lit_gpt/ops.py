@@ -42,14 +42,13 @@ SIGNATURES = {
     "lga_q4_gemv_swiglu": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4_gemm": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
     "lga_q4f_fits": [_I, _I, _I, _I, _I],
-    "lga_q4_gemm_fused": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
-    "lga_q4_gemm_swiglu": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P],
+    "lga_q4f_workspace_bytes": [_I, _I, _I, _I],
+    "lga_q4_gemm_fused": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P],
+    "lga_q4_gemm_swiglu": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _P, _SZ, _P],
     "lga_q4_dequantize": [_P, _P, _P, _I, _I, _I, _I, _P],
     "lga_bf16_gemv": [_P, _P, _P, _P, _P, _F, _P, _I, _I, _P],
     "lga_bf16_gemv_swiglu": [_P, _P, _P, _P, _F, _P, _I, _I, _P],
     "lga_bf16_gemm": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
-    "lga_gemm_bf16_blaslt": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P],
-    "lga_gemm_bf16_blaslt_tune": [_P, _P, _P, _P, _P, _I, _I, _I, _P, _SZ, _P],
     "lga_rmsnorm": [_P, _P, _P, _I, _I, _F, _P],
     "lga_rope_kv_append": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lga_embedding": [_P, _I, _P, _P, _I, _I, _I, _P],
@@ -81,7 +80,7 @@ SIGNATURES = {
     "lga_engine_error": [_P, _P, _P],
     "lga_decode_engine": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
 }
-_RESTYPES = {"lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
+_RESTYPES = {"lga_q4f_workspace_bytes": ctypes.c_size_t, "lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
              "lga_comm_mailbox_bytes": ctypes.c_size_t, "lga_engine_scratch_bytes": ctypes.c_size_t,
              "lga_engine_x0": ctypes.c_void_p}
 
@@ -199,16 +198,32 @@ def q4f_fits(M, N, K, group, fmt) -> bool:
     return bool(load_library().lga_q4f_fits(int(M), int(N), int(K), int(group), int(fmt)))
 
 
+_Q4F_WS: dict = {}
+
+
+def _q4f_workspace(M, N, K, swiglu, device):
+    """The split-K workspace of a short-prompt fused GEMM: one zeroed buffer per device, grown as needed (its
+    per-tile counters are left zeroed by every launch). Returns (ptr, bytes) or (None, 0)."""
+    need = int(load_library().lga_q4f_workspace_bytes(int(M), int(N), int(K), int(bool(swiglu))))
+    if need == 0:
+        return None, 0
+    ws = _Q4F_WS.get(device)
+    if ws is None or ws.numel() < need:
+        ws = _Q4F_WS[device] = torch.zeros(need, dtype=torch.uint8, device=device)
+    return ws.data_ptr(), ws.numel()
+
+
 def q4_gemm_fused(x, weight, scales, N, K, group, fmt, *, bias=None, residual=None, out=None):
     """Y (M, N) = X (M, K) . dequant(W)^T [+bias] [+residual], dequantization fused into the MFMA tiles
     (fmt 2: ``weight`` is the bf16 (N, K) matrix, ``scales`` None)."""
     M = x.shape[0]
     y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
     wdt = torch.bfloat16 if fmt == 2 else torch.uint8
+    ws, nws = _q4f_workspace(M, N, K, False, x.device)
     _check(load_library().lga_q4_gemm_fused(_dev(x, "x", torch.bfloat16), _dev(weight, "weight", wdt),
                                             _opt(scales, "scales"), _opt(bias, "bias", torch.bfloat16),
                                             _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16),
-                                            M, N, K, group, fmt, _stream()))
+                                            M, N, K, group, fmt, ws, nws, _stream()))
     return y
 
 
@@ -217,9 +232,10 @@ def q4_gemm_swiglu(x, w1, s1, w2, s2, N, K, group, fmt, *, out=None):
     M = x.shape[0]
     y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
     wdt = torch.bfloat16 if fmt == 2 else torch.uint8
+    ws, nws = _q4f_workspace(M, N, K, True, x.device)
     _check(load_library().lga_q4_gemm_swiglu(_dev(x, "x", torch.bfloat16), _dev(w1, "w1", wdt), _opt(s1, "s1"),
                                              _dev(w2, "w2", wdt), _opt(s2, "s2"), _dev(y, "y", torch.bfloat16),
-                                             M, N, K, group, fmt, _stream()))
+                                             M, N, K, group, fmt, ws, nws, _stream()))
     return y
 
 
@@ -257,70 +273,12 @@ def bf16_gemv_swiglu(x, w1, w2, *, norm_weight=None, eps=1e-5, out=None):
     return y
 
 
-LIB_GEMM_MIN_M = 16  # rows from which the hipBLASLt bf16 GEMM replaces gemm.hip's tiles (tools/gemm_rates.py)
-LIB_GEMM_WORKSPACE = 32 << 20
-_GEMM_WS: dict = {}
-
-
-def warm_gemm_library(device, K: int = 4096) -> None:
-    """Load hipBLASLt and its gfx950 kernels before the first prefill (one small GEMM), so the first prompt does
-    not pay the library's start-up."""
-    x = torch.zeros(LIB_GEMM_MIN_M, K, dtype=torch.bfloat16, device=device)
-    bf16_gemm(x, torch.zeros(64, K, dtype=torch.bfloat16, device=device), impl="blaslt")
-
-
-def tune_prefill_gemms(model, rows: int) -> int:
-    """Tune the hipBLASLt plan of every distinct (N, K, bias) prefill GEMM of ``model``'s blocks for ``rows``-token
-    prompts (lga_gemm_bf16_blaslt_tune on random operands of that shape), so the first prompt of that length runs
-    the fastest candidate without paying the search. Returns the number of shapes tuned; no-op below
-    LIB_GEMM_MIN_M rows (those prompts do not reach hipBLASLt)."""
-    if rows < LIB_GEMM_MIN_M:
-        return 0
-    shapes = set()
-    for name, mod in model.named_modules():
-        if name.endswith("lm_head") or not hasattr(mod, "in_features") or not hasattr(mod, "out_features"):
-            continue  # lm_head sees one row in a prefill (last_token_only)
-        if mod.out_features % 8 or mod.in_features % 8:
-            continue
-        shapes.add((mod.out_features, mod.in_features, getattr(mod, "bias", None) is not None))
-    dev = torch.device("cuda", torch.cuda.current_device())
-    ws = _GEMM_WS.get(dev)
-    if ws is None:
-        ws = _GEMM_WS[dev] = torch.empty(LIB_GEMM_WORKSPACE, dtype=torch.uint8, device=dev)
-    g = torch.Generator(device=dev).manual_seed(0)
-    for N, K, has_bias in sorted(shapes):
-        x = torch.randn(rows, K, generator=g, device=dev).to(torch.bfloat16)
-        w = (torch.randn(N, K, generator=g, device=dev) * 0.02).to(torch.bfloat16)
-        b = torch.zeros(N, dtype=torch.bfloat16, device=dev) if has_bias else None
-        y = torch.empty(rows, N, dtype=torch.bfloat16, device=dev)
-        _check(load_library().lga_gemm_bf16_blaslt_tune(
-            _dev(x, "x", torch.bfloat16), _dev(w, "weight", torch.bfloat16), _opt(b, "bias", torch.bfloat16), None,
-            _dev(y, "y", torch.bfloat16), rows, N, K, _dev(ws, "workspace", torch.uint8), ws.numel(), _stream()))
-        del x, w, y
-    torch.cuda.synchronize(dev)
-    return len(shapes)
-
-
-def bf16_gemm(x, weight, *, bias=None, residual=None, out=None, impl=None):
-    """Y (M, N) = X (M, K) . W (N, K)^T [+bias] [+residual] with bf16 weights. impl "mfma" = gemm.hip's MFMA tiles
-    (bias and residual fused in its epilogue), "blaslt" = hipBLASLt (bias epilogue; residual added after the
-    product's bf16 rounding, as the reference Block adds it); default: hipBLASLt from LIB_GEMM_MIN_M rows."""
+def bf16_gemm(x, weight, *, bias=None, residual=None, out=None):
+    """Y (M, N) = X (M, K) . W (N, K)^T [+bias] [+residual] with bf16 weights on gemm.hip's MFMA tiles (bias and
+    residual fused in its epilogue; the residual added after the product's bf16 rounding, as Block adds it)."""
     M = x.shape[0]
     N, K = weight.shape
     y = out if out is not None else torch.empty(M, N, dtype=torch.bfloat16, device=x.device)
-    if impl is None:
-        impl = "blaslt" if M >= LIB_GEMM_MIN_M and N % 8 == 0 and K % 8 == 0 else "mfma"
-    if impl == "blaslt":
-        ws = _GEMM_WS.get(x.device)
-        if ws is None:
-            ws = _GEMM_WS[x.device] = torch.empty(LIB_GEMM_WORKSPACE, dtype=torch.uint8, device=x.device)
-        _check(load_library().lga_gemm_bf16_blaslt(
-            _dev(x, "x", torch.bfloat16), _dev(weight, "weight", torch.bfloat16), _opt(bias, "bias", torch.bfloat16),
-            _opt(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16), M, N, K,
-            _dev(ws, "workspace", torch.uint8), ws.numel(), _stream()))
-        return y
-    if impl != "mfma":
-        raise ValueError(f"bf16_gemm: unknown impl {impl!r}")
     _check(load_library().lga_bf16_gemm(_dev(x, "x", torch.bfloat16), _dev(weight, "weight", torch.bfloat16),
                                         _opt(bias, "bias", torch.bfloat16), _opt(residual, "residual", torch.bfloat16),
                                         _dev(y, "y", torch.bfloat16), M, N, K, _stream()))

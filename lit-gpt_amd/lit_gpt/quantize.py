@@ -73,51 +73,11 @@ def _fit_group(K: int, group: int) -> int:
     raise ValueError(f"in_features={K} is not a multiple of 32; no 4-bit group layout fits")
 
 
-# Prefill GEMM for M > 1 rows: "fused" = lga_q4_gemm_fused (dequantization inside the MFMA tiles) from
-# FUSED_GEMM_MIN_M rows; "blaslt" = dequantize + hipBLASLt (LGA_PREFILL_GEMM=blaslt, for A/B runs).
-PREFILL_GEMM = os.environ.get("LGA_PREFILL_GEMM", "blaslt")
-FUSED_GEMM_MIN_M = 16
-
-# prefill rows from which dequantize + the library bf16 GEMM beats the fused int4 GEMM (tools/gemm_rates.py, Llama-2-7B
-# layer: 0.21 vs 0.44 ms at M = 64, 0.63 vs 1.04 ms at M = 2048; gemm.hip's 128-row tiles idle most CUs below M = 256)
-DEQUANT_GEMM_MIN_M = 16
-_SCRATCH: dict = {}
-
-
-# Prefill weight cache: a Linear keeps the bf16 weight its first long prefill dequantized (the same bits
-# lga_q4_dequantize writes every time) and later prefills skip the dequantize pass — 0.13 ms of HBM-bound work per
-# Llama-2-7B layer, the largest non-GEMM cost of a warm 2048-token prefill. Decode keeps streaming the packed 4-bit
-# weights. Costs 2 bytes per weight of HBM: 13 GB for Llama-2-7B of an MI355X's 288 GB, so it is bounded per device
-# by PREFILL_CACHE_FRACTION of the device memory and by what is free (keeping PREFILL_CACHE_HEADROOM free); a Linear
-# that does not fit dequantizes into the shared scratch as before. LGA_PREFILL_CACHE=0 turns it off.
-PREFILL_CACHE = os.environ.get("LGA_PREFILL_CACHE", "1") != "0"
-PREFILL_CACHE_FRACTION = 0.25
-PREFILL_CACHE_HEADROOM = 16 << 30
-_CACHED_BYTES: dict = {}
-
-
-def _cache_admits(nbytes: int, device: torch.device) -> bool:
-    if not PREFILL_CACHE:
-        return False
-    free, total = torch.cuda.mem_get_info(device)
-    used = _CACHED_BYTES.get(device, 0)
-    return used + nbytes <= PREFILL_CACHE_FRACTION * total and free - nbytes >= PREFILL_CACHE_HEADROOM
-
-
-def _dequant_scratch(numel: int, device: torch.device) -> torch.Tensor:
-    """One growing bf16 buffer per device for dequantized weights: the Linears of a forward run one after
-    another on the device's stream, so one buffer serves them all."""
-    buf = _SCRATCH.get(device)
-    if buf is None or buf.numel() < numel:
-        buf = _SCRATCH[device] = torch.empty(numel, dtype=torch.bfloat16, device=device)
-    return buf
-
-
 class QuantLinear(nn.Module):
     """Packed 4-bit weight ``qweight`` (N, K/2) uint8 + ``scales`` (N, K/group) on the GPU.
 
     ``forward`` dispatches like bitsandbytes' ``matmul_4bit``: one token -> fused dequant-GEMV
-    (``lga_q4_gemv``), several -> MFMA GEMM (``lga_q4_gemm``). ``weight`` is kept as an alias of the packed
+    (``lga_q4_gemv``), several -> MFMA GEMM with the dequantization fused (``lga_q4_gemm_fused``). ``weight`` is kept as an alias of the packed
     buffer so code that inspects ``linear.weight`` (e.g. ``.device``/``.dtype``) keeps working.
     """
 
@@ -169,44 +129,15 @@ class QuantLinear(nn.Module):
         else:
             if norm_weight is not None:
                 x2 = ops.rmsnorm(x2, norm_weight, norm_eps)
-            if PREFILL_GEMM == "fused" and M >= FUSED_GEMM_MIN_M and ops.q4f_fits(M, self.out_features,
-                                                                                  self.in_features, self.group,
-                                                                                  self.fmt):
-                # dequantization fused into the MFMA tiles (csrc/gemm_q4f.hip): no bf16 weight in HBM
+            if ops.q4f_fits(M, self.out_features, self.in_features, self.group, self.fmt):
+                # several rows (prefill): the dequantization runs inside the MFMA tiles (csrc/gemm_q4f.hip) to the
+                # bits bnb's dequantize_4bit writes — the reference's M > 1 path without a bf16 weight in HBM
                 y = ops.q4_gemm_fused(x2, self.qweight, self.scales, self.out_features, self.in_features,
                                       self.group, self.fmt, bias=self.bias, residual=res)
-            elif M >= DEQUANT_GEMM_MIN_M:
-                # long prefill: dequantize to bf16 once (bnb's dequantize_4bit, the reference's own M > 1 path),
-                # then the library bf16 GEMM (hipBLASLt): 1.1-1.25 PFLOP/s vs 0.5-0.7 for the fused int4 GEMM at
-                # M = 2048, the dequantize pass included (tools/gemm_rates.py)
-                y = ops.bf16_gemm(x2, self._prefill_weight(x2.device), bias=self.bias, residual=res)
-            else:
+            else:  # group 32 / K % 64: gemm.hip's 128 x 128 tiles (same staged weight bits)
                 y = ops.q4_gemm(x2, self.qweight, self.scales, self.out_features, self.in_features, self.group,
                                 self.fmt, bias=self.bias, residual=res)
         return y.view(*lead, self.out_features)
-
-    def _prefill_weight(self, device: torch.device) -> torch.Tensor:
-        """bf16(dequant(W)) for the library GEMM: the cached copy when it is current (same packed weights and
-        scales as when it was made), else a fresh dequantize — into a cache buffer if the device budget admits one,
-        into the shared scratch otherwise."""
-        try:
-            key = (self.qweight.data_ptr(), self.qweight._version, self.scales.data_ptr(), self.scales._version)
-        except RuntimeError:  # inference tensors keep no version counter: an in-place change would go unseen
-            key = None
-        cached = getattr(self, "_w_bf16", None)
-        if cached is not None and self._w_key == key:
-            return cached
-        if cached is not None:  # weights changed in place (e.g. load_state_dict): drop the stale copy
-            _CACHED_BYTES[cached.device] = _CACHED_BYTES.get(cached.device, 0) - cached.numel() * 2
-            self._w_bf16 = None
-        N, K = self.out_features, self.in_features
-        if key is not None and _cache_admits(N * K * 2, device):
-            out = torch.empty(N, K, dtype=torch.bfloat16, device=device)
-            _CACHED_BYTES[device] = _CACHED_BYTES.get(device, 0) + N * K * 2
-            self._w_bf16, self._w_key = out, key
-        else:
-            out = _dequant_scratch(N * K, device)
-        return ops.q4_dequantize(self.qweight, self.scales, N, K, self.group, self.fmt, out=out)
 
     def extra_repr(self) -> str:
         kind = "int4" if self.fmt == ops.FMT_Q4G else "nf4"

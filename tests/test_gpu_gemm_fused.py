@@ -145,6 +145,34 @@ def test_fused_bf16_weights(ops, M, N, K):
     assert float((g - ref).abs().sub(_swiglu_tol(h1.float(), h2.float(), ref)).max()) <= 0.0
 
 
+@pytest.mark.parametrize("M,N,K", [(64, 4096, 4096), (17, 4096, 11008), (128, 1024, 4096)])
+def test_fused_gemm_split_k(ops, M, N, K, monkeypatch):
+    """Short prompts split K over workgroups (fp32 slabs summed in slice order by the tile's last slice): the
+    result is deterministic, within fp32 reassociation of the unsplit kernel, and within bf16 rounding of the
+    fp32 product; also for the SwiGLU form."""
+    g = torch.Generator(device=DEV).manual_seed(M * 7 + K)
+    w = torch.randn(N, K, generator=g, device=DEV) * 0.02
+    qw, sc = ops.quantize(w, 0, 128)
+    x = torch.randn(M, K, generator=g, device=DEV).to(torch.bfloat16)
+    assert ops.load_library().lga_q4f_workspace_bytes(M, N, K, 0) > 0  # this shape splits
+    y1 = ops.q4_gemm_fused(x, qw, sc, N, K, 128, 0)
+    y2 = ops.q4_gemm_fused(x, qw, sc, N, K, 128, 0)
+    assert torch.equal(y1, y2), "split-K must be deterministic"
+    monkeypatch.setenv("LGA_Q4F_SPLITS", "1")
+    y0 = ops.q4_gemm_fused(x, qw, sc, N, K, 128, 0)
+    monkeypatch.delenv("LGA_Q4F_SPLITS")
+    h = x.float() @ ops.q4_dequantize(qw, sc, N, K, 128, 0).float().t()
+    for y in (y0, y1):
+        assert float(((y.float() - h).abs() - h.abs() * 2 ** -7).max()) <= 2e-3
+    w2 = torch.randn(N, K, generator=g, device=DEV) * 0.02
+    q2, s2 = ops.quantize(w2, 0, 128)
+    gg = ops.q4_gemm_swiglu(x, qw, sc, q2, s2, N, K, 128, 0).float()
+    h1 = h.to(torch.bfloat16)
+    h2 = (x.float() @ ops.q4_dequantize(q2, s2, N, K, 128, 0).float().t()).to(torch.bfloat16)
+    ref = ops.swiglu(h1.contiguous(), h2.contiguous()).float()
+    assert float((gg - ref).abs().sub(_swiglu_tol(h1.float(), h2.float(), ref)).max()) <= 0.0
+
+
 def test_fused_gemm_rejects_unsupported_shapes(ops):
     assert not ops.q4f_fits(16, 128, 96, 32, 0)   # K % 64
     assert not ops.q4f_fits(16, 132, 128, 64, 0)  # N % 8

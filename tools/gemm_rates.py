@@ -1,5 +1,5 @@
 """Lab: prefill GEMM rates at Llama-2-7B layer shapes (M = 2048 prompt rows) — the product's int4 GEMM, its
-dequantize pass + bf16 GEMM (gemm.hip's MFMA tiles, and lga_gemm_bf16_blaslt), and torch.matmul on the same bf16
+dequantize pass + bf16 GEMM (gemm.hip's MFMA tiles), and torch.matmul (the vendor library) on the same bf16
 operands for comparison.
 
 usage: python tools/gemm_rates.py [M]
@@ -14,6 +14,9 @@ sys.path[:0] = [str(REPO / "lit-gpt_amd"), str(REPO)]
 from lit_gpt import ops  # noqa: E402
 
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
+if len(sys.argv) > 2:  # an alternative build of the library (lab A/B)
+    ops._lib = ops.load_library(Path(sys.argv[2]))
+ONLY = sys.argv[3].split(",") if len(sys.argv) > 3 else None
 dev = torch.device("cuda")
 SHAPES = {"qkv": (12288, 4096), "proj": (4096, 4096), "fc": (11008, 4096), "down": (4096, 11008)}
 
@@ -40,12 +43,13 @@ for name, (N, K) in SHAPES.items():
     r = {"q4f": timed(lambda: ops.q4_gemm_fused(x, qw, sc, N, K, 128, 0)),
          "q4_gemm": timed(lambda: ops.q4_gemm(x, qw, sc, N, K, 128, 0)),
          "dequant": timed(lambda: ops.q4_dequantize(qw, sc, N, K, 128, 0, out=wb)),
-         "bf16_gemm": timed(lambda: ops.bf16_gemm(x, wb, impl="mfma")),
-         "blaslt": timed(lambda: ops.bf16_gemm(x, wb, impl="blaslt")),
+         "bf16_gemm": timed(lambda: ops.bf16_gemm(x, wb)),
          "q4f_bf16w": timed(lambda: ops.q4_gemm_fused(x, wb, None, N, K, 64, 2)),
          "torch_mm": timed(lambda: torch.matmul(x, wb.t()))}
     if name == "fc":  # fc_1 || fc_2 + SwiGLU in one launch (counts as both GEMMs of the layer)
         r["q4f_swiglu/2"] = timed(lambda: ops.q4_gemm_swiglu(x, qw, sc, qw, sc, N, K, 128, 0)) / 2
+    if ONLY:
+        r = {k: v for k, v in r.items() if k in ONLY}
     for k, v in r.items():
         tot[k] = tot.get(k, 0.0) + v * (2 if name == "fc" else 1)
     print(f"{name:5s} N={N:6d} K={K:6d}  " + "  ".join(

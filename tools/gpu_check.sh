@@ -1,4 +1,7 @@
+# the whole GPU suite + smoke + bench (one call): a test FAILURE does not stop the call, a fault/abort/timeout does
 set -o pipefail
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
-timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench.log 2>&1 && \
-timeout -k 10 900 python -u -m pytest tests/test_gpu_tp.py -x -v --timeout 600 --timeout-method thread -k "xgmi_allreduce or tp8" > gpurun_out/tp.log 2>&1
+mkdir -p gpurun_out
+ok() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
+timeout -k 10 1500 python -u -m pytest tests -m gpu -q --timeout 600 --timeout-method thread -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1; rc=$?; ok $rc || exit $rc
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || exit 1
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/bench.log 2>&1
