@@ -149,7 +149,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
   constexpr int OFF_RAW = T::OFF_RAW, OFF_SC = T::OFF_SC, OFF_WB = T::OFF_WB, OFF_MISC = T::OFF_MISC;
   static_assert(!DUAL || FJ % 2 == 0, "SwiGLU needs fc_1 and fc_2 fragments in pairs");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[T::LDS_BYTES];
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches on it)
   const int wm = wave % T::WM, wn = wave / T::WM;
   const int split = blockIdx.x % a.splits;
   const int tile = blockIdx.x / a.splits;
