@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
     n = min(n, a.N - 1);
     return base + (size_t)n * (FMT == 2 ? (size_t)a.K * 2 : (size_t)a.K / 2);
   };
-  // scale index of weight-tile row r at K-step kt (global). The DMA moves 4 bytes per lane: a bf16 scale is
+  // scale index of weight-tile row r at K-step kt (global). The scale DMA moves 4 bytes per lane: a bf16 scale is
   // fetched with its neighbour from the 4-byte-aligned pair holding it (in bounds: N * groups is even) and the
   // reader picks the half by the index's parity.
   auto sc_index = [&](int r, int kt) -> size_t {
@@ -186,49 +186,58 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
     n = min(n, a.N - 1);
     return (size_t)n * groups + ((kt * BK) >> gshift);
   };
-  auto sc_ptr = [&](int r, int kt) -> const unsigned char* {
-    const unsigned char* base = (const unsigned char*)(DUAL && r >= BN / 2 ? a.sc2 : a.sc);
-    const size_t i = sc_index(r, kt);
-    return base + (FMT == 0 ? (i & ~(size_t)1) * 2 : i * 4);
-  };
 
   // ---- stage issue; `lk` is the slice-local K-step (buffer index), kt0 + lk the global one. Every wave issues
-  // the same number of DMAs per stage, so one count serves all ----
+  // the same number of DMAs per stage, so one count serves all. The per-lane source rows are fixed for the whole
+  // loop: their pointers are computed once, a stage only adds its K offset. ----
+  const unsigned char* xsrc[T::APW];  // X: lane L of piece i -> row r0 + L/8, logical chunk (L%8) ^ (row & 7)
+#pragma unroll
+  for (int i = 0; i < T::APW; ++i) {
+    const int r = (wave * T::APW + i) * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ (r & 7);
+    xsrc[i] = (const unsigned char*)(a.x + (size_t)min(m0 + r, a.M - 1) * a.K + (size_t)kt0 * BK + lc * 8);
+  }
   auto issue_a = [&](int lk) {
     unsigned char* A = lds + (lk % NA) * A_BYTES;
 #pragma unroll
-    for (int i = 0; i < T::APW; ++i) {
-      const int r0 = (wave * T::APW + i) * 8;
-      glds_rows8(a.x, a.K, m0 + r0, a.M - 1, (kt0 + lk) * BK, A + r0 * 128, lane);
-    }
+    for (int i = 0; i < T::APW; ++i) glds<16>(xsrc[i] + (size_t)lk * BK * 2, A + (wave * T::APW + i) * 8 * 128);
   };
+  const unsigned char* bsrc[FMT == 2 ? T::BPW : 1];  // bf16 weights (FMT 2), the same mapping
+  if (FMT == 2) {
+#pragma unroll
+    for (int i = 0; i < T::BPW; ++i) {
+      const int r = (wave * T::BPW + i) * 8 + (lane >> 3);
+      const int lc = (lane & 7) ^ (r & 7);
+      bsrc[i] = wrow_ptr(r) + (size_t)kt0 * BK * 2 + lc * 16;
+    }
+  }
   auto issue_b16 = [&](int lk) {  // bf16 weight tile (FMT 2)
     unsigned char* B = lds + NA * A_BYTES + (lk % NA) * B_BYTES;
 #pragma unroll
-    for (int i = 0; i < T::BPW; ++i) {
-      const int r0 = (wave * T::BPW + i) * 8;
-      const int r = r0 + (lane >> 3);
-      const int lc = (lane & 7) ^ (r & 7);
-      glds<16>(wrow_ptr(r) + (size_t)(kt0 + lk) * BK * 2 + lc * 16, B + r0 * 128);
-    }
+    for (int i = 0; i < T::BPW; ++i) glds<16>(bsrc[i] + (size_t)lk * BK * 2, B + (wave * T::BPW + i) * 8 * 128);
   };
   // packed weight tile (1 KB = 32 rows x 32 B per DMA) and its scales (256 B = 64 rows x 4 B per DMA).
   // BN = 256: every wave one of each (waves 4-7 repeat the scales of 0-3 into their own slots);
   // BN = 128: waves 4-7 the packed rows, waves 0-3 the scales (2, 3 repeat 0, 1): one DMA per wave.
+  const int raw_wave = BN == 256 ? wave : wave - 4;
+  const unsigned char* rsrc =
+      wrow_ptr(max(raw_wave, 0) * 32 + (lane >> 1)) + (size_t)kt0 * (BK / 2) + (lane & 1) * 16;
+  const int sw = wave & (BN / 64 - 1);  // the 64-row scale block this wave fetches
+  const size_t sc_row = sc_index(sw * 64 + lane, 0);  // its scale index at K-step 0
+  const unsigned char* sc_base = (const unsigned char*)(DUAL && sw * 64 + lane >= BN / 2 ? a.sc2 : a.sc);
   auto issue_raw = [&](int lk) {
     const int kt = kt0 + lk;
     unsigned char* R = lds + OFF_RAW + (lk % NRAW) * RAW_BYTES;
     unsigned char* S = lds + OFF_SC + (lk % NRAW) * SC_BYTES + wave * 256;
-    const int sw = wave & (BN / 64 - 1);  // the 64-row scale block this wave fetches
+    const size_t si = sc_row + ((kt * BK) >> gshift);
+    const unsigned char* sp = sc_base + (FMT == 0 ? (si & ~(size_t)1) * 2 : si * 4);
     if (BN == 256) {
-      const int r = wave * 32 + (lane >> 1);
-      glds<16>(wrow_ptr(r) + (size_t)kt * (BK / 2) + (lane & 1) * 16, R + wave * 1024);
-      glds<4>(sc_ptr(sw * 64 + lane, kt), S);
+      glds<16>(rsrc + (size_t)lk * (BK / 2), R + wave * 1024);
+      glds<4>(sp, S);
     } else if (wave >= 4) {
-      const int r = (wave - 4) * 32 + (lane >> 1);
-      glds<16>(wrow_ptr(r) + (size_t)kt * (BK / 2) + (lane & 1) * 16, R + (wave - 4) * 1024);
+      glds<16>(rsrc + (size_t)lk * (BK / 2), R + raw_wave * 1024);
     } else {
-      glds<4>(sc_ptr(sw * 64 + lane, kt), S);
+      glds<4>(sp, S);
     }
   };
 
@@ -239,12 +248,13 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
   // sit between the MFMAs: the reads are issued before the K-step's first MFMA group, the image written after.
   constexpr int RPT = T::RPT, NDW = RPT / 4;
   const int dq_r = tid / T::TPR, dq_q = tid % T::TPR;
+  const size_t dq_row0 = FMT == 2 ? 0 : sc_index(dq_r, 0);  // the row's scale index at K-step 0 (parity source)
   typedef uint32_t raw_t __attribute__((ext_vector_type(NDW)));
   auto dq_load = [&](int lk, raw_t& wv, uint32_t& sb) {
     const unsigned raw_a = lds_addr(lds + OFF_RAW + (lk % NRAW) * RAW_BYTES + dq_r * 32 + dq_q * RPT);
     // the scale of row r sits in the slot of the wave that fetched its 64-row block (wave r / 64)
     const unsigned sc_a = lds_addr(lds + OFF_SC + (lk % NRAW) * SC_BYTES + (dq_r >> 6) * 256 + (dq_r & 63) * 4 +
-                                   (FMT == 0 ? (int)(sc_index(dq_r, kt0 + lk) & 1) * 2 : 0));
+                                   (FMT == 0 ? (int)((dq_row0 + (((kt0 + lk) * BK) >> gshift)) & 1) * 2 : 0));
     if constexpr (NDW == 4) {
       if (FMT == 0)
         asm volatile("ds_read_b128 %0, %2\n\tds_read_u16 %1, %3" : "=&v"(wv), "=&v"(sb) : "v"(raw_a), "v"(sc_a) : "memory");
