@@ -40,6 +40,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 64, NT = 512;
+constexpr int MAX_SPLITS = 8;  // K-slices per tile (split-K for short prompts)
 
 template <int BM_, int BN_>
 struct Tile {
@@ -50,9 +51,13 @@ struct Tile {
   static constexpr int A_BYTES = BM * BK * 2;      // one X tile (BM rows x 128 B)
   static constexpr int B_BYTES = BN * BK * 2;      // one bf16 weight tile
   static constexpr int RAW_BYTES = BN * BK / 2;    // one packed weight tile (BN rows x 32 B)
-  static constexpr int SC_BYTES = 8 * 256;         // one scale stage: a 256-B slot per wave
-  static constexpr int NA = 3, NRAW = 4, NWB = 2;
-  // LDS, 4-bit weights: A[3] | RAW[4] | SC[4] | WB[2] | misc ; bf16 weights: A[3] | B[3] | misc
+  static constexpr int SC_BYTES = (BN == 256 ? 8 : 4) * 256;  // one scale stage: a 256-B slot per scale DMA wave
+  // prefetch depth: X (and bf16 weight) tiles D K-steps ahead, packed weights D + 1 ahead. The 64-row tiles of
+  // short prompts do little MFMA work per K-step, so they hide the DMA latency with depth instead (D = 4; the
+  // 64 x 256 SwiGLU tile has no LDS for it)
+  static constexpr int D = BM == 64 && BN == 128 ? 4 : 2;
+  static constexpr int NA = D + 1, NRAW = D + 2, NWB = 2;
+  // LDS, 4-bit weights: A[NA] | RAW[NRAW] | SC[NRAW] | WB[2] | misc ; bf16 weights: A[NA] | B[NA] | misc
   static constexpr int OFF_RAW = NA * A_BYTES;
   static constexpr int OFF_SC = OFF_RAW + NRAW * RAW_BYTES;
   static constexpr int OFF_WB = OFF_SC + NRAW * SC_BYTES;
@@ -113,16 +118,12 @@ __device__ __forceinline__ void glds(const void* src, unsigned char* lds) {
 // s_waitcnt vmcnt(N) / vmcnt(N) lgkmcnt(0) for a compile-time N (the count is an encoding field)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
-  static_assert(N >= 0 && N <= 8, "vmcnt");
-  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  else if constexpr (N == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-  else if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-  else if constexpr (N == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-  else if constexpr (N == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else if constexpr (N == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  static_assert(N >= 0 && N <= 15, "vmcnt");
+#define LGA_VM(n) \
+  if constexpr (N == n) asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory");
+  LGA_VM(0) LGA_VM(1) LGA_VM(2) LGA_VM(3) LGA_VM(4) LGA_VM(5) LGA_VM(6) LGA_VM(7) LGA_VM(8) LGA_VM(9) LGA_VM(10)
+  LGA_VM(11) LGA_VM(12) LGA_VM(13) LGA_VM(14) LGA_VM(15)
+#undef LGA_VM
 }
 template <int N>
 __device__ __forceinline__ void wait_vm_lgkm() {
@@ -336,54 +337,59 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
       for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[j][i], 0, 0, 0);
   };
 
+  constexpr int D = T::D;
   if (nk > 0) {
     if (FMT == 2) {
-      // X and W both DMA'd two K-steps ahead into 3 buffers: G = APW + BPW DMAs per wave per stage
+      // X and W both DMA'd D K-steps ahead into D + 1 buffers: G = APW + BPW DMAs per wave per stage; at the end
+      // of step lk the stages lk+2 .. lk+D may stay in flight
       constexpr int G = T::APW + T::BPW;
-      issue_a(0);
-      issue_b16(0);
-      if (nk > 1) {
-        issue_a(1);
-        issue_b16(1);
-        wait_vm<G>();
-      } else {
-        wait_vm<0>();
-      }
+#pragma unroll
+      for (int st = 0; st < D; ++st)
+        if (st < nk) {
+          issue_a(st);
+          issue_b16(st);
+        }
+      if (nk >= D) wait_vm<(D - 1) * G>();
+      else wait_vm<0>();
       __builtin_amdgcn_s_barrier();
       for (int lk = 0; lk < nk; ++lk) {
-        const bool full = lk + 2 < nk;
+        const bool full = lk + D < nk;
         if (full) {
-          issue_a(lk + 2);
-          issue_b16(lk + 2);
+          issue_a(lk + D);
+          issue_b16(lk + D);
         }
         const unsigned char* A = lds + (lk % NA) * A_BYTES;
         const unsigned char* B = lds + NA * A_BYTES + (lk % NA) * B_BYTES;
         mfma_sub(A, B, 0);
         mfma_sub(A, B, 1);
-        if (full) wait_vm_lgkm<G>();
+        if (full) wait_vm_lgkm<(D - 1) * G>();
         else wait_vm_lgkm<0>();
         __builtin_amdgcn_s_barrier();
       }
     } else {
-      // G = APW + RAWPW DMAs per wave per stage. Prologue: {A0, raw0, raw1} {A1, raw2}; raw0 -> WB0
+      // G = APW + RAWPW DMAs per wave per group; group g = {A(g), raw(g+1)} (raw(0) rides with group 0), issued
+      // D groups ahead. Prologue: groups 0 .. D-1; raw(0) -> WB0 once group 0 has landed
       constexpr int G = T::APW + T::RAWPW;
       issue_a(0);
       issue_raw(0);
       if (nk > 1) issue_raw(1);
-      if (nk > 1) issue_a(1);
-      if (nk > 2) issue_raw(2);
-      if (nk > 2) wait_vm<G>();
+#pragma unroll
+      for (int g = 1; g < D; ++g) {
+        if (g < nk) issue_a(g);
+        if (g + 1 < nk) issue_raw(g + 1);
+      }
+      if (D < nk) wait_vm<(D - 1) * G>();  // groups 1 .. D-1 all full
       else wait_vm<0>();
       __builtin_amdgcn_s_barrier();
       dequant(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      // iteration lk: issue {A(lk+2), raw(lk+3)}; MFMA on A(lk), WB(lk) with raw(lk+1) dequantized between the
-      // two MFMA groups; wait for {A(lk+1), raw(lk+2)} (issued one iteration earlier); barrier
+      // iteration lk: issue group lk+D {A(lk+D), raw(lk+D+1)}; MFMA on A(lk), WB(lk) with raw(lk+1) dequantized
+      // between the two MFMA groups; wait for group lk+1 {A(lk+1), raw(lk+2)}; barrier
       for (int lk = 0; lk < nk; ++lk) {
-        const bool full = lk + 3 < nk;
-        if (lk + 2 < nk) issue_a(lk + 2);
-        if (full) issue_raw(lk + 3);
+        const bool full = lk + D + 1 < nk;
+        if (lk + D < nk) issue_a(lk + D);
+        if (full) issue_raw(lk + D + 1);
         // past the last stage this dequantizes a stale raw buffer into the bf16 buffer nobody reads again: no
         // branch, so the math can interleave with the MFMAs
         const unsigned char* A = lds + (lk % NA) * A_BYTES;
@@ -396,7 +402,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
         dq_math(wv, sb, o);
         mfma_sub(A, B, 1);
         dq_store(lk + 1, o);
-        if (full) wait_vm_lgkm<G>();
+        if (full) wait_vm_lgkm<(D - 1) * G>();  // groups lk+2 .. lk+D, all full
         else wait_vm_lgkm<0>();
         __builtin_amdgcn_s_barrier();
       }
@@ -436,20 +442,26 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
     }
     __syncthreads();
     if (*last == 0u) return;
+    // every slab value of one output fragment is loaded before any is summed (MAX_SPLITS loads in flight, the
+    // index clamped and the surplus weighted by zero: no branch around a load), summed in slice order
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int jj = DUAL ? j % (FJ / 2) : j;
-      const int n = n0 + (DUAL ? wn * (WC / 2) : wn * WC) + jj * 16 + fk * 4;
-      if (n >= a.N) continue;
+      const int n = min(n0 + (DUAL ? wn * (WC / 2) : wn * WC) + jj * 16 + fk * 4, a.N - 4);
+      const size_t mat = DUAL ? j / (FJ / 2) : 0;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int m = m0 + wm * 64 + i * 16 + fr;
-        if (m >= a.M) continue;
-        f32x4_t t = f32x4_t{0.f, 0.f, 0.f, 0.f};
-        for (int s = 0; s < a.splits; ++s) {
-          const float* slab = a.slabs + ((size_t)s * (DUAL ? 2 : 1) + (DUAL ? j / (FJ / 2) : 0)) * a.M * a.N;
-          t += *(const f32x4_t*)(slab + (size_t)m * a.N + n);
+        const int m = min(m0 + wm * 64 + i * 16 + fr, a.M - 1);
+        f32x4_t v[MAX_SPLITS];
+#pragma unroll
+        for (int s2 = 0; s2 < MAX_SPLITS; ++s2) {
+          const int sc = min(s2, a.splits - 1);
+          const float* slab = a.slabs + ((size_t)sc * (DUAL ? 2 : 1) + mat) * a.M * a.N;
+          v[s2] = *(const f32x4_t*)(slab + (size_t)m * a.N + n);
         }
+        f32x4_t t = v[0];
+#pragma unroll
+        for (int s2 = 1; s2 < MAX_SPLITS; ++s2) t += s2 < a.splits ? v[s2] : f32x4_t{0.f, 0.f, 0.f, 0.f};
         acc[j][i] = t;
       }
     }
@@ -535,9 +547,9 @@ Plan q4f_plan(int M, int N, int K, bool dual) {
   p.tiles = p.mt * ((N + p.tn - 1) / p.tn);
   const int nk = K / lga::pf::BK;
   int s = 1;
-  // each slice keeps >= 4 K-steps; aim at ~256 workgroups
-  while (p.tiles * s * 2 <= 256 && nk / (s * 2) >= 4) s *= 2;
-  if (const char* e = getenv("LGA_Q4F_SPLITS")) s = std::max(1, std::min(atoi(e), nk));
+  // each slice keeps >= 4 K-steps; aim at one workgroup per CU
+  while (p.tiles * s * 2 <= 256 && nk / (s * 2) >= 4 && s * 2 <= lga::pf::MAX_SPLITS) s *= 2;
+  if (const char* e = getenv("LGA_Q4F_SPLITS")) s = std::max(1, std::min({atoi(e), nk, lga::pf::MAX_SPLITS}));
   p.splits = s;
   return p;
 }
