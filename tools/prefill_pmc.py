@@ -31,7 +31,7 @@ def run() -> None:
     T = 2048
     dev = torch.device("cuda", 0)
     cfg = Config.from_name("Llama-2-7b-hf")
-    model = build_model(cfg, quantize="int4-g128", device=dev, max_seq_length=T + 16, prefill_rows=T)
+    model = build_model(cfg, quantize="int4-g128", device=dev, max_seq_length=T + 16)
     prompt = torch.randint(0, cfg.vocab_size, (1, T), dtype=torch.int32, device=dev)
     with torch.inference_mode():
         for _ in range(2):
@@ -63,8 +63,24 @@ def summarize(d: Path) -> None:
         print(f"{'all MFMA kernels (GUI_ACTIVE-weighted)':72s} {'':5s} {tg:13.0f} {tb / (tg * simds):10.3f}")
 
 
+def dump(d: Path) -> None:
+    """Every counter of a pass, per kernel name, averaged per dispatch (the second, stall-breakdown pass)."""
+    rows = [r for f in d.rglob("*counter_collection.csv") for r in csv.DictReader(open(f))]
+    by = defaultdict(lambda: defaultdict(float))
+    calls = defaultdict(lambda: defaultdict(int))
+    for r in rows:
+        by[r["Kernel_Name"]][r["Counter_Name"]] += float(r["Counter_Value"])
+        calls[r["Kernel_Name"]][r["Counter_Name"]] += 1
+    for name, c in sorted(by.items(), key=lambda kv: -max(kv[1].values())):
+        print(name[:100])
+        for k, v in sorted(c.items()):
+            print(f"    {k:28s} {v / max(calls[name][k], 1):16.0f} per dispatch")
+
+
 if __name__ == "__main__":
     if len(sys.argv) > 2 and sys.argv[1] == "--summarize":
         summarize(Path(sys.argv[2]))
+    elif len(sys.argv) > 2 and sys.argv[1] == "--dump":
+        dump(Path(sys.argv[2]))
     else:
         run()
