@@ -15,6 +15,8 @@
 // With splits > 1 every workgroup publishes (m, l, o) write-through (sc1) and bumps a per-(t, group) counter;
 // the workgroup that arrives last merges the splits and writes the bf16 output (flash-decoding combine inside
 // the same launch; MI355X_MICROARCH.md "Valid forms" row 1), then re-arms the counter for the next launch.
+#include <cstdlib>
+
 #include "decode_ops.h"
 
 namespace lga {
@@ -306,8 +308,9 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 // O^T += V^T . P^T, whose A operand comes straight from the row-major V image by ds_read_b64_tr_b16 (transposed
 // LDS read) — no P or V^T round trip through LDS. O^T's lane also owns one query, so the rescale by
 // exp(m_old - m_new) is a per-lane scalar, skipped when no row max of the wave moved. Causal masking only on the
-// tiles that cross a row's position; query blocks are dispatched heaviest first. Llama-2-7B, T = 2048: 102 us per
-// layer = 336 TFLOP/s (tools/prefill_attn_bench.py), was 295 us with 16-row query blocks on 16x16x32 MFMAs.
+// tiles that cross a row's position; a 1-D grid dispatches the query blocks of every head longest-first, so the
+// light blocks fill the CUs that finished early. Llama-2-7B, T = 2048: 88-90 us per layer = 380-392 TFLOP/s
+// (tools/prefill_attn_bench.py; 102 us with a (blocks, heads) grid, 295 us with 16-row query blocks on 16x16x32).
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
 typedef short i16x8_t __attribute__((ext_vector_type(8)));
@@ -339,8 +342,11 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(const uint16_t* __
   __shared__ long s_pos[2][4];                                          // per wave: max / min row position
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hh = lane >> 5, lq = lane & 31;
-  const int head = blockIdx.y, g = head / (n_head / G);
-  const int blk = gridDim.x - 1 - blockIdx.x;  // heaviest (latest) query blocks first
+  // 1-D grid, heaviest (latest) query blocks of every head first: the dispatcher then fills the CUs
+  // longest-first, the light blocks landing on the CUs whose first block was shortest
+  const int nblk = (T + 127) / 128;
+  const int head = blockIdx.x % n_head, g = head / (n_head / G);
+  const int blk = nblk - 1 - (int)(blockIdx.x / n_head);
   const int q0 = blk * 128 + wave * 32;
   const int t = q0 + lq;
   const long mypos = t < T ? input_pos[t] : -1;
@@ -559,15 +565,20 @@ extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_c
   LGA_CHECK_ARG(n_splits >= 1 && n_splits <= 256, "lga_attention: n_splits must be in [1, 256]");
   LGA_CHECK_ARG(n_splits == 1 || (workspace && counters), "lga_attention: split attention needs workspace + counters");
   if (T >= 16 && n_splits == 1 && (head_size == 128 || head_size == 64)) {  // prefill: flash attention on MFMA
-    const dim3 grid((T + 127) / 128, n_head);
+    const dim3 grid(((T + 127) / 128) * n_head);
+    // LGA_ATTN_PF_SMEM: extra dynamic LDS per workgroup (lab: 90000 leaves one workgroup per CU)
+    static const int extra = [] {
+      const char* e = getenv("LGA_ATTN_PF_SMEM");
+      return e ? atoi(e) : 0;
+    }();
     if (head_size == 128)
-      lga::attn_prefill_kernel<128><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
-                                                              (const uint16_t*)v_cache, input_pos, (uint16_t*)y, T,
-                                                              n_head, n_query_groups, max_seq, scale);
+      lga::attn_prefill_kernel<128><<<grid, 256, extra, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+                                                                  (const uint16_t*)v_cache, input_pos, (uint16_t*)y,
+                                                                  T, n_head, n_query_groups, max_seq, scale);
     else
-      lga::attn_prefill_kernel<64><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
-                                                             (const uint16_t*)v_cache, input_pos, (uint16_t*)y, T,
-                                                             n_head, n_query_groups, max_seq, scale);
+      lga::attn_prefill_kernel<64><<<grid, 256, extra, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+                                                                 (const uint16_t*)v_cache, input_pos, (uint16_t*)y,
+                                                                 T, n_head, n_query_groups, max_seq, scale);
     LGA_LAUNCH_RETURN();
   }
   int rc;
