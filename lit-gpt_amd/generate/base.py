@@ -100,7 +100,6 @@ def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temp
                         break
                 i += n
         tokens.append(out[:produced])
-        dg.check()
         _check_collectives()
         return torch.cat(tokens)
     input_pos = torch.tensor([T], device=device)

@@ -73,16 +73,9 @@ SIGNATURES = {
     "lga_comm_close": [_P],
     "lga_comm_free": [_P],
     "lga_allreduce_bf16": [_P, _P, _P, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P, _P],
-    "lga_engine_check": [_P],
-    "lga_engine_scratch_bytes": [_P],
-    "lga_engine_x0": [_P, _P],
-    "lga_engine_reset": [_P, _P, _P],
-    "lga_engine_error": [_P, _P, _P],
-    "lga_decode_engine": [_P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P],
 }
 _RESTYPES = {"lga_q4f_workspace_bytes": ctypes.c_size_t, "lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
-             "lga_comm_mailbox_bytes": ctypes.c_size_t, "lga_engine_scratch_bytes": ctypes.c_size_t,
-             "lga_engine_x0": ctypes.c_void_p}
+             "lga_comm_mailbox_bytes": ctypes.c_size_t}
 
 _lib: Optional[ctypes.CDLL] = None
 

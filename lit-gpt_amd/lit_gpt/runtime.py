@@ -12,27 +12,19 @@ embedding row for the next step (so the step has no embedding launch) — so a d
 
 from __future__ import annotations
 
-import os
 from typing import Optional
 
 import torch
 
 from lit_gpt import ops
 
-# the persistent one-launch decode step (lit_gpt/engine.py) where the model is in its scope; LGA_ENGINE=0 keeps
-# the per-op graph everywhere
-ENGINE_DEFAULT = os.environ.get("LGA_ENGINE", "0") != "0"
-
-
 class DecodeGraph:
-    def __init__(self, model, first_token: torch.Tensor, first_pos: int, chunk: int = 1,
-                 engine: Optional[bool] = None) -> None:
+    def __init__(self, model, first_token: torch.Tensor, first_pos: int, chunk: int = 1) -> None:
         """Runs one real decode step eagerly (token ``first_token`` at position ``first_pos``) to warm up, then
         captures the step. Afterwards ``self.token`` holds the newest token and ``self.pos`` its position.
         ``chunk`` > 1 also captures ``chunk`` consecutive steps as one graph (``steps()``): the argmax of step i
         writes its token into ``self.history[i]`` as well, and one launch replaces ``chunk`` (≈9 us of
-        graph-launch gap per step on MI355X, profiles/r02b_*). ``engine`` (default: LGA_ENGINE, on) runs each step
-        as ONE persistent launch (lit_gpt/engine.py) when the model is in its scope, else the per-op chain."""
+        graph-launch gap per step on MI355X, profiles/r02b_*)."""
         dev = first_token.device
         self.model = model
         self.token = first_token.reshape(1, 1).to(torch.int32).clone()
@@ -47,13 +39,6 @@ class DecodeGraph:
         self.x_emb = torch.empty(wte.shape[1], dtype=torch.bfloat16, device=dev) if self.fuse_embedding else None
         self.graph: Optional[torch.cuda.CUDAGraph] = None
         self.chunk_graph: Optional[torch.cuda.CUDAGraph] = None
-        self.engine = None
-        if ENGINE_DEFAULT if engine is None else engine:
-            from lit_gpt.engine import DecodeEngine
-
-            if DecodeEngine.supported(model)[0]:
-                self.engine = DecodeEngine(model)
-                self.engine.set_embedding(ops.embedding(self.token.view(-1), wte).view(-1))
         self._step_eager()
         torch.cuda.synchronize(dev)
         g = torch.cuda.CUDAGraph()
@@ -68,9 +53,6 @@ class DecodeGraph:
             self.chunk_graph = gc
 
     def _step_body(self, idx_out: Optional[torch.Tensor] = None, embedded: bool = True) -> None:
-        if self.engine is not None:  # the whole step in one launch: token, pos and the next embedding on device
-            self.engine.step(self.pos, token=self.token.view(-1), out_idx=idx_out)
-            return
         if not self.fuse_embedding:
             logits = self.model(self.token, self.pos, last_token_only=True)
             ops.argmax(logits.reshape(-1), out_idx=idx_out, token_out=self.token.view(-1), pos_inout=self.pos)
@@ -86,11 +68,6 @@ class DecodeGraph:
         """One decode step; returns the (device) token buffer holding the new token."""
         self.graph.replay()
         return self.token
-
-    def check(self) -> None:
-        """Raise if an engine launch gave up waiting (lit_gpt/engine.py EngineTimeout); no-op on the per-op path."""
-        if self.engine is not None:
-            self.engine.check()
 
     def steps(self) -> torch.Tensor:
         """``chunk`` decode steps in one graph launch; returns the (device, int64) buffer of their tokens."""

@@ -35,7 +35,7 @@
 #include <string.h>
 
 #include "decode_ops.h"
-#include "litgpt_amd.h"
+#include "engine.h"
 
 namespace lga {
 namespace eng {

@@ -1,4 +1,6 @@
-"""Persistent decode engine: one launch per greedy decode step (``lga_decode_engine``, csrc/engine.hip).
+"""LAB: persistent decode engine, one launch per greedy decode step (``lga_decode_engine``, tools/lab/engine/
+engine.hip, built into tools/_lab/liblga_engine.so by ``make -C lit-gpt_amd/csrc lab-engine``). Measured slower
+than the product's per-op decode graph, so it is not part of liblitgpt_amd.so.
 
 The reference runs a decode step as ``next_token`` -> ``GPT.forward`` -> every ``Block.forward`` -> ``ln_f`` ->
 ``lm_head`` -> ``sample`` (reference generate/base.py:44-47,87-92; lit_gpt/model.py:499-519,572-593), ~50 kernels
@@ -16,11 +18,40 @@ parallelism. Everything else keeps the per-op path (``DecodeEngine.supported`` r
 from __future__ import annotations
 
 import ctypes
+import os
+from pathlib import Path
 from typing import Optional, Tuple
 
 import torch
 
 from lit_gpt import ops
+
+LAB_LIB = Path(os.environ.get("LGA_ENGINE_LIB", Path(__file__).resolve().parents[2] / "_lab" / "liblga_engine.so"))
+_elib: Optional[ctypes.CDLL] = None
+
+
+def engine_library() -> ctypes.CDLL:
+    """The lab library (product objects + the engine), loaded once with the engine's signatures."""
+    global _elib
+    if _elib is None:
+        if not LAB_LIB.is_file():
+            raise ops.NativeLibraryError(f"lab engine library not found at {LAB_LIB}: make -C lit-gpt_amd/csrc lab-engine")
+        lib = ctypes.CDLL(str(LAB_LIB))
+        P, I = ctypes.c_void_p, ctypes.c_int
+        sig = {"lga_engine_check": ([P], I), "lga_engine_scratch_bytes": ([P], ctypes.c_size_t),
+               "lga_engine_x0": ([P, P], ctypes.c_void_p), "lga_engine_reset": ([P, P, P], I),
+               "lga_engine_error": ([P, P, P], I),
+               "lga_decode_engine": ([P] * 13 + [I, P], I), "lga_last_error_string": ([], ctypes.c_char_p)}
+        for name, (args, res) in sig.items():
+            fn = getattr(lib, name)
+            fn.argtypes, fn.restype = args, res
+        _elib = lib
+    return _elib
+
+
+def _check(rc: int) -> None:
+    if rc != 0:
+        raise RuntimeError(f"engine error {rc}: {engine_library().lga_last_error_string().decode()}")
 
 
 class EngineLayer(ctypes.Structure):
@@ -93,7 +124,7 @@ class DecodeEngine:
         self.geom = EngineGeom(c.n_layer, c.n_embd, c.n_head, c.n_query_groups, c.head_size, c.intermediate_size,
                                lm.out_features, kv.k.size(-2), lm.group, lm.fmt, self.cos.size(0),
                                int(n_cu or ops.num_cus()), float(blocks[0].norm_1.eps), float(c.head_size ** -0.5))
-        lib = ops.load_library()
+        lib = engine_library()
         if lib.lga_engine_check(ctypes.byref(self.geom)) != 0:
             raise NotImplementedError(f"DecodeEngine: {lib.lga_last_error_string().decode()}")
         table = (EngineLayer * c.n_layer)()
@@ -133,7 +164,7 @@ class DecodeEngine:
             g = EngineGeom(c.n_layer, c.n_embd, c.n_head, c.n_query_groups, c.head_size, c.intermediate_size,
                            lm.out_features, kv.k.size(-2), lm.group, lm.fmt, model.cos.size(0), ops.num_cus(),
                            1e-5, 1.0)
-            lib = ops.load_library()
+            lib = engine_library()
             if lib.lga_engine_check(ctypes.byref(g)) != 0:
                 why = lib.lga_last_error_string().decode()
         return why is None, why or ""
@@ -149,7 +180,7 @@ class DecodeEngine:
         if pos.dtype != torch.int64 or not pos.is_cuda:
             raise TypeError("pos must be an int64 GPU tensor")
         lm = self._lm
-        ops._check(ops.load_library().lga_decode_engine(
+        _check(engine_library().lga_decode_engine(
             ctypes.byref(self.geom), self.layers.data_ptr(), lm.qweight.data_ptr(), lm.scales.data_ptr(),
             self._ln_f.data_ptr(), self._wte.data_ptr(), self.cos.data_ptr(), self.sin.data_ptr(), pos.data_ptr(),
             None if token is None else token.data_ptr(), None if out_idx is None else out_idx.data_ptr(),
@@ -158,13 +189,13 @@ class DecodeEngine:
     def errors(self) -> int:
         """Non-zero after a launch that gave up waiting (syncs)."""
         e = ctypes.c_uint(0)
-        ops._check(ops.load_library().lga_engine_error(ctypes.byref(self.geom), ctypes.c_void_p(self.scratch.data_ptr()),
+        _check(engine_library().lga_engine_error(ctypes.byref(self.geom), ctypes.c_void_p(self.scratch.data_ptr()),
                                                        ctypes.byref(e)))
         return int(e.value)
 
     def reset(self) -> None:
         """Zero the counters / epoch / error words (after an error, or after op_limit test launches)."""
-        ops._check(ops.load_library().lga_engine_reset(ctypes.byref(self.geom),
+        _check(engine_library().lga_engine_reset(ctypes.byref(self.geom),
                                                        ctypes.c_void_p(self.scratch.data_ptr()), ops._stream()))
 
     def check(self) -> None:

@@ -2,12 +2,13 @@
 after a 2048-token prefill, same process and weights (interleaved rounds, MI355X_MICROARCH.md rule 24)."""
 import sys, time
 from pathlib import Path
-REPO = Path(__file__).resolve().parents[1]
-sys.path[:0] = [str(REPO / "lit-gpt_amd"), str(REPO)]
+REPO = Path(__file__).resolve().parents[3]
+sys.path[:0] = [str(Path(__file__).resolve().parent), str(REPO / "lit-gpt_amd"), str(REPO)]
 import torch
 from generate.base import build_model
 from lit_gpt import Config, ops
 from lit_gpt.runtime import DecodeGraph
+from engine import DecodeEngine
 
 dev = torch.device("cuda", 0)
 T, STEPS = 2048, 64
@@ -18,20 +19,25 @@ with torch.inference_mode():
     lg = model(prompt.view(1, -1), torch.arange(T, device=dev), last_token_only=True)
     first = ops.argmax(lg.reshape(-1)).to(torch.int32)
     pos = T
-    graphs = {}
-    for name, eng in (("per-op", False), ("engine", True)):
-        graphs[name] = DecodeGraph(model, first, pos, chunk=8, engine=eng)
-        pos += 1
+    dg = DecodeGraph(model, first, pos, chunk=8)
+    pos += 1
+    eng = DecodeEngine(model)
+    eng.set_embedding(model.transformer.wte.weight[int(first)])
+    epos = torch.tensor([pos], device=dev)
+    etok = torch.zeros(1, dtype=torch.int32, device=dev)
+    eng.step(epos, token=etok)
+    ge = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(ge):
+        for _ in range(8):
+            eng.step(epos, token=etok)
     for rnd in range(3):
-        for name, dg in graphs.items():
-            dg.pos.fill_(pos)
+        for name in ("per-op", "engine"):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(STEPS // 8):
-                dg.steps()
+                dg.steps() if name == "per-op" else ge.replay()
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / STEPS
-            if dg.engine is not None:
-                dg.check()
-            print(f"round {rnd} {name:7s} {dt * 1e6:8.1f} us/step  {1 / dt:7.1f} tok/s  (pos {pos})", flush=True)
-            pos += STEPS
+            if name == "engine":
+                eng.check()
+            print(f"round {rnd} {name:7s} {dt * 1e6:8.1f} us/step  {1 / dt:7.1f} tok/s", flush=True)

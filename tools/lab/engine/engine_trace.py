@@ -1,23 +1,23 @@
 """Per-op timeline of the persistent decode engine (lab build with -DLGA_ENGINE_TRACE: make -C lit-gpt_amd/csrc
-lab-trace). Runs a few engine steps of Llama-2-7B int4-g128 after a 2048-token prefill and prints, per op of one
+lab-engine LABFLAGS=-DLGA_ENGINE_TRACE LAB=../../tools/_lab/liblga_engine_trace.so). Runs a few engine steps of Llama-2-7B int4-g128 after a 2048-token prefill and prints, per op of one
 step, the spread over CUs of: counter wait, gather, unit compute, publish, and the loader's issue window."""
 import ctypes, os, sys
 from pathlib import Path
-REPO = Path(__file__).resolve().parents[1]
-os.environ["LGA_LIB"] = sys.argv[3] if len(sys.argv) > 3 else str(REPO / "tools" / "_lab" / "liblga_engine_trace.so")
-sys.path[:0] = [str(REPO / "lit-gpt_amd"), str(REPO)]
+REPO = Path(__file__).resolve().parents[3]
+os.environ["LGA_ENGINE_LIB"] = sys.argv[3] if len(sys.argv) > 3 else str(REPO / "tools" / "_lab" / "liblga_engine_trace.so")
+sys.path[:0] = [str(Path(__file__).resolve().parent), str(REPO / "lit-gpt_amd"), str(REPO)]
 import numpy as np
 import torch
 from generate.base import build_model
 from lit_gpt import Config, ops
-from lit_gpt.engine import DecodeEngine
+from engine import DecodeEngine, engine_library
 
 dev = torch.device("cuda", 0)
 L = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 T = 2048
 cfg = Config.from_name("Llama-2-7b-hf", n_layer=L)
 model = build_model(cfg, quantize="int4-g128", device=dev, max_seq_length=T + 64)
-lib = ops.load_library()
+lib = engine_library()
 lib.lga_engine_trace_read.argtypes = [ctypes.c_void_p, ctypes.c_long]
 TR_OPS, TR_EV, NCU = 192, 8, 256
 buf = np.zeros(NCU * TR_OPS * TR_EV, dtype=np.uint64)

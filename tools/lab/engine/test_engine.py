@@ -1,4 +1,5 @@
-"""The persistent decode engine (lga_decode_engine, csrc/engine.hip) against the per-op kernels and the oracle.
+"""LAB (not collected by the product suite): the persistent decode engine (lga_decode_engine, tools/lab/engine/
+engine.hip) against the per-op kernels and the oracle. Run: python -m pytest tools/lab/engine/test_engine.py -m gpu
 
 The engine runs a whole greedy decode step (every block + ln_f + lm_head + argmax; reference generate/base.py:44-47,
 lit_gpt/model.py:499-519) as ONE launch. Its GEMVs reproduce the per-op kernels' arithmetic (same chunk mapping,
@@ -14,12 +15,17 @@ Geometry: Llama-2-7B width (C 4096, 32 heads, I 11008, V 32000), two blocks, int
 from __future__ import annotations
 
 import math
+import sys
+from pathlib import Path
 
 import numpy as np
 import pytest
 import torch
 
-from oracle import synth
+_HERE = Path(__file__).resolve().parent
+sys.path[:0] = [str(_HERE), str(_HERE.parents[2] / "tests"), str(_HERE.parents[2] / "lit-gpt_amd"),
+                str(_HERE.parents[2])]
+from oracle import synth  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda", 0)
@@ -48,7 +54,7 @@ def _ulps_close(a: torch.Tensor, b: torch.Tensor, ulps: int = 2) -> bool:
 @torch.inference_mode()
 def test_engine_ops_match_per_op_kernels(T):
     from lit_gpt import ops
-    from lit_gpt.engine import DecodeEngine
+    from engine import DecodeEngine
 
     model, cfg, first = _model(T)
     eng = DecodeEngine(model)
@@ -137,7 +143,7 @@ def test_engine_greedy_decode_matches_per_op_graph_and_oracle():
     per-op DecodeGraph — identical tokens up to the first step whose per-op top-2 margin is inside the logit
     tolerance, and every engine step's logits within the tests/parity.py bounds of the oracle."""
     from lit_gpt import ops
-    from lit_gpt.engine import DecodeEngine
+    from engine import DecodeEngine
     from lit_gpt.runtime import DecodeGraph
     from parity import check_step
     from oracle import model as om
@@ -147,7 +153,7 @@ def test_engine_greedy_decode_matches_per_op_graph_and_oracle():
     model, cfg, first = _model(T, extra=N + 4)
     kv0 = [(b.attn.kv_cache.k.clone(), b.attn.kv_cache.v.clone()) for b in model.transformer.h]
     # per-op path: captured decode graph, logits per step
-    dg = DecodeGraph(model, torch.tensor([first], device=DEV), T, engine=False)
+    dg = DecodeGraph(model, torch.tensor([first], device=DEV), T)
     ref_toks = [int(dg.token)]
     for _ in range(N - 1):
         ref_toks.append(int(dg.step()))
@@ -199,7 +205,7 @@ def test_engine_greedy_decode_matches_per_op_graph_and_oracle():
 def test_engine_declines_unsupported_models():
     from generate.base import build_model
     from lit_gpt import Config
-    from lit_gpt.engine import DecodeEngine
+    from engine import DecodeEngine
 
     cfg = Config.from_name("Llama-2-7b-hf", n_layer=1, n_embd=256, n_head=2, intermediate_size=640)
     model = build_model(cfg, quantize="int4-g128", device=DEV, max_seq_length=64)
