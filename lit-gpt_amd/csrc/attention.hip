@@ -308,9 +308,17 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 // O^T += V^T . P^T, whose A operand comes straight from the row-major V image by ds_read_b64_tr_b16 (transposed
 // LDS read) — no P or V^T round trip through LDS. O^T's lane also owns one query, so the rescale by
 // exp(m_old - m_new) is a per-lane scalar, skipped when no row max of the wave moved. Causal masking only on the
-// tiles that cross a row's position; a 1-D grid dispatches the query blocks of every head longest-first, so the
-// light blocks fill the CUs that finished early. Llama-2-7B, T = 2048: 88-90 us per layer = 380-392 TFLOP/s
-// (tools/prefill_attn_bench.py; 102 us with a (blocks, heads) grid, 295 us with 16-row query blocks on 16x16x32).
+// tiles that cross a row's position (a 32-bit compare + select per element, on those tiles only); the scores stay
+// raw — the max runs on them and one fma(s, scale log2 e, -m) per element feeds v_exp_f32 (max(s) c == max(s c) for
+// c > 0). K / V tiles are staged by buffer loads (a per-thread 32-bit offset plus a scalar per tile; rows past the
+// cache read as zeros by the range check) and every LDS address is a per-lane base plus a compile-time offset (the
+// tile loop is unrolled by the two buffers). Grid: 1-D, `order` 1 pairs the two workgroups a CU holds — the first
+// half walks query blocks nblk-1 .. nblk/2, the second half blocks 0 .. nblk/2-1, so workgroups i and i + half sum
+// to a constant number of key tiles and share a head (its K / V in one XCD's L2).
+// Llama-2-7B, T = 2048: 64-65 us per layer = 529-540 TFLOP/s causal, 652-667 TFLOP/s with every row seeing all
+// keys (tools/prefill_attn_bench.py; round 2's kernel: 88-90 us). PMC (profiles/r03c_prefill_fa_pmc.txt): MFMA busy
+// 0.24, SQ_WAIT_ANY 30 % / SQ_WAIT_INST_ANY 35 % of wave cycles, L2 hit 85 % — latency inside each wave (K read ->
+// S MFMA -> max -> exp -> P -> PV chains), not bandwidth; one workgroup per CU is only 19 % slower.
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
 typedef short i16x8_t __attribute__((ext_vector_type(8)));
@@ -327,75 +335,94 @@ __device__ __forceinline__ int kv_off(int row, int ch) {
 
 template <int HS>
 __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(const uint16_t* __restrict__ q,
-                                                               const uint16_t* __restrict__ kc,
-                                                               const uint16_t* __restrict__ vc,
-                                                               const int64_t* __restrict__ input_pos,
-                                                               uint16_t* __restrict__ y, int T, int n_head, int G,
-                                                               int max_seq, float scale) {
-  constexpr int KT = 64;         // keys per tile
-  constexpr int CH = HS / 8;     // 16-B chunks per key row
-  constexpr int DK = HS / 16;    // 32x32x16 k-steps over the head dim (S^T)
-  constexpr int DT = HS / 32;    // 32-row tiles of O^T
-  constexpr int TB = KT * HS * 2;  // bytes of one K or V tile image
+                                                                const uint16_t* __restrict__ kc,
+                                                                const uint16_t* __restrict__ vc,
+                                                                const int64_t* __restrict__ input_pos,
+                                                                uint16_t* __restrict__ y, int T, int n_head, int G,
+                                                                int max_seq, float scale, int order) {
+  constexpr int KT = 64;              // keys per tile
+  constexpr int CH = HS / 8;          // 16-B chunks per key row
+  constexpr int DK = HS / 16;         // 32x32x16 k-steps over the head dim (S^T)
+  constexpr int DT = HS / 32;         // 32-row tiles of O^T
+  constexpr int TB = KT * HS * 2;     // bytes of one K or V tile image
   constexpr int LPT = KT * CH / 256;  // 16-B chunks per thread per tile (K and V each)
+  constexpr int RPI = 256 / CH;       // key rows between a thread's consecutive chunks
   __shared__ __attribute__((aligned(16))) unsigned char lds[2][2][TB];  // [buffer][K | V]
-  __shared__ long s_pos[2][4];                                          // per wave: max / min row position
+  __shared__ int s_pos[2][4];                                           // per wave: max / min row position
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, hh = lane >> 5, lq = lane & 31;
-  // 1-D grid, heaviest (latest) query blocks of every head first: the dispatcher then fills the CUs
-  // longest-first, the light blocks landing on the CUs whose first block was shortest
   const int nblk = (T + 127) / 128;
-  const int head = blockIdx.x % n_head, g = head / (n_head / G);
-  const int blk = nblk - 1 - (int)(blockIdx.x / n_head);
+  // order 0: longest first; order 1: the first half of the grid walks blocks nblk-1 .. nblk/2, the second half
+  // blocks 0 .. nblk/2-1, so workgroups i and i + half hold key-tile counts summing to a constant and the same head
+  // (its K / V stays in one XCD's L2 when half is a multiple of 8)
+  const int nhi = (nblk - nblk / 2) * n_head;
+  const int i = blockIdx.x;
+  const bool lo_half = order == 1 && i >= nhi;
+  const int jj = lo_half ? i - nhi : i;
+  const int head = jj % n_head, g = head / (n_head / G);
+  const int blk = lo_half ? jj / n_head : nblk - 1 - jj / n_head;
   const int q0 = blk * 128 + wave * 32;
   const int t = q0 + lq;
-  const long mypos = t < T ? input_pos[t] : -1;
-
-  // positions: this wave's max (key range) and min (masking needed from there); the workgroup's max
+  const int mypos = t < T ? (int)input_pos[t] : -1;
   {
-    long mx = mypos, mn = t < T ? mypos : LONG_MAX;
+    int mx = mypos, mn = t < T ? mypos : INT_MAX;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
-      mx = max(mx, (long)__shfl_xor(mx, o));
-      mn = min(mn, (long)__shfl_xor(mn, o));
+      mx = max(mx, __shfl_xor(mx, o));
+      mn = min(mn, __shfl_xor(mn, o));
     }
     if (lane == 0) {
       s_pos[0][wave] = mx;
       s_pos[1][wave] = mn;
     }
   }
-  // Q^T fragments (B operand): lane l holds Q[t][ks*16 + 8*hh .. +8]
-  bf16x8_t qb[DK];
+  bf16x8_t qb[DK];  // Q^T fragments (B operand): lane l holds Q[t][ks*16 + 8*hh .. +8]
   {
     const uint16_t* qr = q + ((size_t)min(t, T - 1) * n_head + head) * HS + 8 * hh;
 #pragma unroll
     for (int ks = 0; ks < DK; ++ks) qb[ks] = *(const bf16x8_t*)(qr + ks * 16);
   }
   __syncthreads();
-  const long wmax = s_pos[0][wave], wmin = s_pos[1][wave];
-  long bmax = max(max(s_pos[0][0], s_pos[0][1]), max(s_pos[0][2], s_pos[0][3]));
-  bmax = min(bmax, (long)max_seq - 1);
-  const int kend = (int)bmax + 1;
-  const int ntiles = (kend + KT - 1) / KT;
+  const int wmax = s_pos[0][wave], wmin = s_pos[1][wave];
+  const int bmax = min(max(max(s_pos[0][0], s_pos[0][1]), max(s_pos[0][2], s_pos[0][3])), max_seq - 1);
+  const int ntiles = (bmax + 1 + KT - 1) / KT;
 
-  const uint16_t* kbase = kc + (size_t)g * max_seq * HS;
-  const uint16_t* vbase = vc + (size_t)g * max_seq * HS;
-  // staging: thread tid moves chunks c = tid + 256 i (row c / CH, chunk c % CH) of the K and V tiles
-  uint4 kr[LPT], vr[LPT];
+  // K / V staging: thread tid moves chunk tid % CH of rows tid / CH + RPI i of every tile
+  const __amdgpu_buffer_rsrc_t krs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(kc + (size_t)g * max_seq * HS), (short)0, max_seq * HS * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(vc + (size_t)g * max_seq * HS), (short)0, max_seq * HS * 2, 0x00020000);
+  const int gvoff = ((tid / CH) * HS + (tid % CH) * 8) * 2;
+  u32x4_t kr[LPT], vr[LPT];  // tile t + 1 in flight under tile t
   int soff[LPT];
 #pragma unroll
-  for (int i = 0; i < LPT; ++i) soff[i] = kv_off<HS>((tid + 256 * i) / CH, (tid + 256 * i) % CH);
-#define LGA_PF2_GLOAD(K0)                                                                                       \
-  _Pragma("unroll") for (int i = 0; i < LPT; ++i) {                                                             \
-    const int c_ = tid + 256 * i;                                                                               \
-    const size_t key_ = (size_t)min((K0) + c_ / CH, max_seq - 1); /* past the cache: its last row (masked) */  \
-    kr[i] = *(const uint4*)(kbase + key_ * HS + (c_ % CH) * 8);                                                 \
-    vr[i] = *(const uint4*)(vbase + key_ * HS + (c_ % CH) * 8);                                                 \
-  }
-#define LGA_PF2_LSTORE(BUF)                                              \
-  _Pragma("unroll") for (int i = 0; i < LPT; ++i) {                      \
-    *(uint4*)(lds[BUF][0] + soff[i]) = kr[i];                            \
-    *(uint4*)(lds[BUF][1] + soff[i]) = vr[i];                            \
+  for (int i = 0; i < LPT; ++i) soff[i] = kv_off<HS>(tid / CH + RPI * i, tid % CH);
+  auto gload = [&](int k0) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      const int so = (k0 + RPI * i) * HS * 2;
+      kr[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, gvoff, so, 0);
+      vr[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, gvoff, so, 0);
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < LPT; ++i) {
+      *(u32x4_t*)(lds[buf][0] + soff[i]) = kr[i];
+      *(u32x4_t*)(lds[buf][1] + soff[i]) = vr[i];
+    }
+  };
+  // LDS read bases: K row lq (+ 32 st), chunk 2 ks + hh; V^T transposed reads (16-lane group grp, quad qq, pair pp)
+  int koff[DK];
+#pragma unroll
+  for (int ks = 0; ks < DK; ++ks) koff[ks] = kv_off<HS>(lq, 2 * ks + hh);
+  const int gi = lane & 15, qq = gi >> 2, pp = gi & 3, grp = lane >> 4;
+  int voff0[DT], voff1[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int ch = ((dt * 32 + 16 * (grp & 1)) >> 3) + (pp >> 1);
+    voff0[dt] = kv_off<HS>(8 * (grp >> 1) + qq, ch) + 8 * (pp & 1);
+    voff1[dt] = kv_off<HS>(8 * (grp >> 1) + 4 + qq, ch) + 8 * (pp & 1);
   }
 
   f32x16_t o[DT];
@@ -403,99 +430,101 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(const uint16_t* __
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[dt][r] = 0.0f;
-  float m = -INFINITY, l = 0.0f;
-  const float sl2 = scale * 1.4426950408889634f;  // scores in the log2 domain: one v_exp_f32 per element
+  float m = -INFINITY, l = 0.0f;  // m in the scaled log2 domain; l = this lane's 16-key half of the row sum
+  const float sl2 = scale * 1.4426950408889634f;
 
-  if (ntiles > 0) {
-    LGA_PF2_GLOAD(0)
-    LGA_PF2_LSTORE(0)
-  }
-  __syncthreads();
-  for (int it = 0; it < ntiles; ++it) {
-    const int k0 = it * KT, buf = it & 1;
-    LGA_PF2_GLOAD(k0 + KT)  // next tile, in flight under this tile's MFMAs (past the end: clamped, unused)
-    if (k0 <= wmax) {                      // wave-uniform: some row of this wave sees keys of this tile
-      const unsigned char* K = lds[buf][0];
-      const unsigned char* V = lds[buf][1];
-      // S^T for keys k0 + 32 st + crow(r), crow(r) = (r & 3) + 8 (r >> 2) + 4 hh; query t
-      f32x16_t sacc[2];
+  auto tile = [&](const unsigned char* K, const unsigned char* V, int k0) {
+    // S^T of the two 32-key halves as two interleaved accumulation chains
+    f32x16_t sacc[2];
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[st][r] = 0.0f;
+#pragma unroll
+    for (int ks = 0; ks < DK; ++ks)
 #pragma unroll
       for (int st = 0; st < 2; ++st) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) sacc[st][r] = 0.0f;
-#pragma unroll
-        for (int ks = 0; ks < DK; ++ks) {
-          const bf16x8_t ka = *(const bf16x8_t*)(K + kv_off<HS>(st * 32 + lq, 2 * ks + hh));
-          sacc[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qb[ks], sacc[st], 0, 0, 0);
-        }
+        const bf16x8_t ka = *(const bf16x8_t*)(K + st * 32 * HS * 2 + koff[ks]);
+        sacc[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ka, qb[ks], sacc[st], 0, 0, 0);
       }
-      const bool need_mask = (long)(k0 + KT - 1) > wmin;  // wave-uniform
-      float x[2][16];
-      float tmax = -INFINITY;
+    if (__builtin_amdgcn_readfirstlane(k0 + KT - 1 > wmin)) {  // a row of this wave ends inside the tile
 #pragma unroll
       for (int st = 0; st < 2; ++st)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int key = k0 + st * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
-          const float v = sacc[st][r] * sl2;
-          x[st][r] = (!need_mask || key <= mypos) ? v : -INFINITY;
-          tmax = fmaxf(tmax, x[st][r]);
-        }
-      tmax = fmaxf(tmax, __shfl_xor(tmax, 32));
-      const float mnew = fmaxf(m, tmax);
-      const float mref = mnew == -INFINITY ? 0.0f : mnew;  // rows with no visible key yet: p = 0, o stays 0
-      if (!__all(mnew == m)) {  // some row max moved: rescale (exactly; no threshold)
-        const float c = __builtin_amdgcn_exp2f(m - mref);
-        l *= c;
+        for (int r = 0; r < 16; ++r)
+          if (k0 + st * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh > mypos) sacc[st][r] = -INFINITY;
+    }
+    float tmax = -INFINITY;
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt)
+    for (int st = 0; st < 2; ++st)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) o[dt][r] *= c;
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[st][r]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+      tmax = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));  // both halves of the row
+    }
+    const float mnew = fmaxf(m, tmax * sl2);
+    const float mref = mnew == -INFINITY ? 0.0f : mnew;  // rows with no visible key yet: p = 0, o stays 0
+    if (!__all(mnew == m)) {                              // some row max moved: rescale (exactly; no threshold)
+      const float c = __builtin_amdgcn_exp2f(m - mref);
+      l *= c;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= c;
+    }
+    m = mnew;
+    // P^T . V per 16-key k-step kk: its 8 exponentials (half-tile kk / 2, registers 8 (kk & 1) .. +7) become the
+    // B operand just before its DT MFMAs, so the next k-step's exponentials can issue under them
+    float rs = 0.0f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int st = kk >> 1, r0 = 8 * (kk & 1);
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        x[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[st][r0 + e], sl2, -mref));
+        rs += x[e];
       }
-      m = mnew;
-      float rs = 0.0f;
-#pragma unroll
-      for (int st = 0; st < 2; ++st)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          x[st][r] = __builtin_amdgcn_exp2f(x[st][r] - mref);
-          rs += x[st][r];
-        }
-      l += rs + __shfl_xor(rs, 32);
-      // P^T as B operands: k-step kk (16 keys) = half-tile kk / 2, registers 8 (kk & 1) .. +7
-      bf16x8_t pb[4];
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        const int st = kk >> 1, r0 = 8 * (kk & 1);
-        const uint32_t w0 = pack2(x[st][r0], x[st][r0 + 1]), w1 = pack2(x[st][r0 + 2], x[st][r0 + 3]);
-        const uint32_t w2 = pack2(x[st][r0 + 4], x[st][r0 + 5]), w3 = pack2(x[st][r0 + 6], x[st][r0 + 7]);
-        const auto a = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
-        const auto b = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
-        const u32x4_t f = {a[0], b[0], a[1], b[1]};  // keys 8 hh + 0..7 of the k-step, in order
-        pb[kk] = __builtin_bit_cast(bf16x8_t, f);
-      }
-      // O^T[d][t] += V^T[d][key] . P^T[key][t]; A = V^T by transposed reads of the row-major V image
-      const int gi = lane & 15, qq = gi >> 2, pp = gi & 3, grp = lane >> 4;
+      const uint32_t w0 = pack2(x[0], x[1]), w1 = pack2(x[2], x[3]);
+      const uint32_t w2 = pack2(x[4], x[5]), w3 = pack2(x[6], x[7]);
+      const auto a = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
+      const auto b = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
+      const u32x4_t f = {a[0], b[0], a[1], b[1]};
+      const bf16x8_t pb = __builtin_bit_cast(bf16x8_t, f);
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        const int c0 = dt * 32 + 16 * (grp & 1);  // first column (d) of this 16-lane group
-#pragma unroll
-        for (int kk = 0; kk < 4; ++kk) {
-          const int r0 = kk * 16 + 8 * (grp >> 1);
-          const int a0 = kv_off<HS>(r0 + qq, (c0 >> 3) + (pp >> 1)) + 8 * (pp & 1);
-          const int a1 = kv_off<HS>(r0 + 4 + qq, (c0 >> 3) + (pp >> 1)) + 8 * (pp & 1);
-          const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(V + a0));
-          const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) i16x4_t*)(V + a1));
-          const i16x8_t f = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, f), pb[kk], o[dt], 0, 0, 0);
-        }
+        typedef __attribute__((address_space(3))) i16x4_t lds_i16x4;
+        const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(V + kk * 16 * HS * 2 + voff0[dt]));
+        const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(V + kk * 16 * HS * 2 + voff1[dt]));
+        const i16x8_t vf = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vf), pb, o[dt], 0, 0, 0);
       }
     }
-    LGA_PF2_LSTORE(buf ^ 1)  // the other buffer: every wave finished reading it before the last barrier
+    l += rs;
+  };
+
+  // unrolled by the two buffers so every LDS address is base + constant; tile t + 1's loads are in flight under
+  // tile t's MFMAs (past the cache: zeros, unused) and written to the other buffer after them (a second register
+  // set, two tiles ahead, measured no faster: the loop is latency-bound inside the wave, not on the loads)
+  if (ntiles > 0) {
+    gload(0);
+    lstore(0);
+  }
+  __syncthreads();
+  for (int it = 0; it < ntiles; it += 2) {
+    const int k0 = it * KT;
+    gload(k0 + KT);
+    if (k0 <= wmax) tile(lds[0][0], lds[0][1], k0);
+    lstore(1);
+    __syncthreads();
+    if (it + 1 >= ntiles) break;
+    gload(k0 + 2 * KT);
+    if (k0 + KT <= wmax) tile(lds[1][0], lds[1][1], k0 + KT);
+    lstore(0);
     __syncthreads();
   }
-#undef LGA_PF2_GLOAD
-#undef LGA_PF2_LSTORE
+  l += __shfl_xor(l, 32);
   // y[t][head * HS + d] = O^T[d][t] / l, d = dt * 32 + crow(r): pairs (r, r + 1) are adjacent columns
   if (t < T) {
     const float inv = 1.0f / l;
@@ -566,19 +595,14 @@ extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_c
   LGA_CHECK_ARG(n_splits == 1 || (workspace && counters), "lga_attention: split attention needs workspace + counters");
   if (T >= 16 && n_splits == 1 && (head_size == 128 || head_size == 64)) {  // prefill: flash attention on MFMA
     const dim3 grid(((T + 127) / 128) * n_head);
-    // LGA_ATTN_PF_SMEM: extra dynamic LDS per workgroup (lab: 90000 leaves one workgroup per CU)
-    static const int extra = [] {
-      const char* e = getenv("LGA_ATTN_PF_SMEM");
-      return e ? atoi(e) : 0;
-    }();
     if (head_size == 128)
-      lga::attn_prefill_kernel<128><<<grid, 256, extra, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
-                                                                  (const uint16_t*)v_cache, input_pos, (uint16_t*)y,
-                                                                  T, n_head, n_query_groups, max_seq, scale);
+      lga::attn_prefill_kernel<128><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+                                                              (const uint16_t*)v_cache, input_pos, (uint16_t*)y, T,
+                                                              n_head, n_query_groups, max_seq, scale, 1);
     else
-      lga::attn_prefill_kernel<64><<<grid, 256, extra, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
-                                                                 (const uint16_t*)v_cache, input_pos, (uint16_t*)y,
-                                                                 T, n_head, n_query_groups, max_seq, scale);
+      lga::attn_prefill_kernel<64><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+                                                             (const uint16_t*)v_cache, input_pos, (uint16_t*)y, T,
+                                                             n_head, n_query_groups, max_seq, scale, 1);
     LGA_LAUNCH_RETURN();
   }
   int rc;

@@ -23,7 +23,8 @@ def main(T=2048, H=32, G=32, hs=128, S=2304, layers=8):
     caches = [(torch.randn(G, S, hs, device=dev).bfloat16(), torch.randn(G, S, hs, device=dev).bfloat16())
               for _ in range(layers)]
     q = torch.randn(T, H, hs, device=dev).bfloat16()
-    pos = torch.arange(T, device=dev)
+    full = os.environ.get("ATT_FULL") == "1"  # every query row sees all T keys (no causal imbalance)
+    pos = torch.full((T,), T - 1, device=dev, dtype=torch.long) if full else torch.arange(T, device=dev)
     y = torch.empty(T, H * hs, device=dev, dtype=torch.bfloat16)
     scale = 1.0 / math.sqrt(hs)
 
@@ -45,8 +46,8 @@ def main(T=2048, H=32, G=32, hs=128, S=2304, layers=8):
     e1.record()
     e1.synchronize()
     us = e0.elapsed_time(e1) / (5 * layers) * 1e3
-    fl = 2.0 * 2.0 * H * hs * T * (T + 1) / 2
-    print(f"prefill attention T={T} H={H} G={G} hs={hs}: {us:8.1f} us/layer  {fl / us / 1e6:7.1f} TFLOP/s", flush=True)
+    fl = 2.0 * 2.0 * H * hs * T * (T if full else (T + 1) / 2)
+    print(f"prefill attention {'full' if full else 'causal'} T={T} H={H} G={G} hs={hs}: {us:8.1f} us/layer  {fl / us / 1e6:7.1f} TFLOP/s", flush=True)
 
 
 if __name__ == "__main__":
