@@ -33,6 +33,10 @@ typedef struct ihipStream_t* lga_stream_t; /* == hipStream_t */
 const char* lga_last_error_string(void);
 int lga_version(void);
 int lga_device_info(int device, int* n_cu, char* arch_name, int arch_len);
+/* builds the device objects of the prefill path's kernels (fused GEMM, flash attention, norms, RoPE, embedding,
+ * lm_head GEMV, argmax) now instead of at their first launch, where the runtime spends about 0.5 ms per kernel
+ * inside the first prompt (called by build_model, the model-load step; nothing is launched) */
+int lga_preload_kernels(void);
 
 /* -- quantize at load (Lightning BitsandbytesPrecision.convert_module + bnb quantize on .to(device);
  *    generate/base.py:168, generate/tp.py:171-190) ------------------------------------------------------

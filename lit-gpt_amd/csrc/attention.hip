@@ -586,6 +586,10 @@ static int launch_hs(const void* q, void* kc, void* vc, const int64_t* pos, void
 
 }  // namespace lga
 
+int lga::preload_attention() {
+  return lga::preload(lga::attn_prefill_kernel<128>) + lga::preload(lga::attn_prefill_kernel<64>);
+}
+
 extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_cache, const int64_t* input_pos,
                              void* y, float* workspace, unsigned* counters, int T, int n_head, int n_query_groups,
                              int head_size, int max_seq, int n_splits, float scale, hipStream_t stream) {

@@ -15,6 +15,17 @@ extern "C" const char* lga_last_error_string(void) { return g_err; }
 
 extern "C" int lga_version(void) { return 1; }
 
+// builds the device objects of the prefill path's kernels now rather than at their first launch (common.h)
+extern "C" int lga_preload_kernels(void) {
+  const int bad = lga::preload_gemm_q4f() + lga::preload_attention() + lga::preload_norm_rope() +
+                  lga::preload_sample() + lga::preload_gemv();
+  if (bad) {
+    lga_set_error("lga_preload_kernels: hipFuncGetAttributes failed");
+    return 1;
+  }
+  return 0;
+}
+
 // fills *n_cu and *arch_major/minor for device `dev`; 0 on success
 extern "C" int lga_device_info(int dev, int* n_cu, char* arch_name, int arch_len) {
   hipDeviceProp_t p;

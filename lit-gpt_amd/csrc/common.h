@@ -57,6 +57,20 @@ __device__ __forceinline__ float add_rn(float a, float b) {
 
 __device__ __forceinline__ float silu_f(float x) { return x / (1.0f + expf(-x)); }
 
+// The runtime builds a kernel's device-side object at the kernel's first launch (about 0.5 ms each on ROCm 7.2,
+// profiles/r03c_cold_prefill.txt); hipFuncGetAttributes builds it ahead of time. Each file lists the kernels of the
+// prefill path it owns; lga_preload_kernels (capi.hip) runs them all at model load.
+template <class F>
+inline int preload(F* f) {
+  hipFuncAttributes a;
+  return hipFuncGetAttributes(&a, (const void*)f) == hipSuccess ? 0 : 1;
+}
+int preload_gemm_q4f();
+int preload_attention();
+int preload_norm_rope();
+int preload_sample();
+int preload_gemv();
+
 }  // namespace lga
 
 // error plumbing shared by every C entry point

@@ -594,6 +594,22 @@ int run(Args a, int fmt, bool dual, void* ws, size_t ws_bytes, hipStream_t strea
 }
 }  // namespace
 
+int lga::preload_gemm_q4f() {
+  using namespace lga::pf;
+  int bad = 0;
+#define LGA_PRE(F, D)                                                                                         \
+  bad += lga::preload(gemm_q4f_kernel<F, D, 256, 128>) + lga::preload(gemm_q4f_kernel<F, D, 64, 256>) +  \
+         lga::preload(gemm_q4f_kernel<F, false, 64, 128>)
+  LGA_PRE(0, false);
+  LGA_PRE(0, true);
+  LGA_PRE(1, false);
+  LGA_PRE(1, true);
+  LGA_PRE(2, false);
+  LGA_PRE(2, true);
+#undef LGA_PRE
+  return bad;
+}
+
 extern "C" int lga_q4f_fits(int M, int N, int K, int group, int fmt) { return q4f_fits(M, N, K, group, fmt) ? 1 : 0; }
 
 extern "C" size_t lga_q4f_workspace_bytes(int M, int N, int K, int swiglu) {

@@ -161,6 +161,13 @@ static int dispatch(const GemvArgs& a, int variant, hipStream_t stream) {
 
 }  // namespace lga
 
+int lga::preload_gemv() {  // the prefill's lm_head row (last_token_only): the streaming form with the norm fused
+  return lga::preload(lga::gemv_q4s_kernel<2, 1, 0, false, true, false>) +
+         lga::preload(lga::gemv_q4s_kernel<2, 2, 0, false, true, false>) +
+         lga::preload(lga::gemv_q4s_kernel<2, 1, 1, false, true, false>) +
+         lga::preload(lga::gemv_q4s_kernel<2, 2, 1, false, true, false>);
+}
+
 extern "C" int lga_q4_gemv(const void* x, const uint8_t* qweight, const void* scales, const void* bias,
                            const void* residual, const void* norm_weight, float norm_eps, void* y, int N, int K,
                            int group, int fmt, int variant, hipStream_t stream) {

@@ -271,6 +271,13 @@ static unsigned elementwise_grid(size_t n) {
 
 }  // namespace lga
 
+int lga::preload_norm_rope() {
+  return lga::preload(lga::rmsnorm_vec_kernel<1>) + lga::preload(lga::rmsnorm_vec_kernel<2>) +
+         lga::preload(lga::rmsnorm_vec_kernel<3>) + lga::preload(lga::rmsnorm_vec_kernel<4>) +
+         lga::preload(lga::rope_kv_vec_kernel) + lga::preload(lga::embedding_kernel<int64_t>) +
+         lga::preload(lga::embedding_kernel<int32_t>);
+}
+
 extern "C" int lga_rmsnorm(const void* x, const void* weight, void* y, int rows, int n, float eps,
                            hipStream_t stream) {
   LGA_CHECK_ARG(x && weight && y && rows > 0 && n > 0, "lga_rmsnorm: bad arguments");

@@ -95,6 +95,10 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict
 
 }  // namespace lga
 
+int lga::preload_sample() {
+  return lga::preload(lga::argmax_kernel<true>) + lga::preload(lga::argmax_kernel<false>);
+}
+
 extern "C" int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
                           hipStream_t stream) {
   LGA_CHECK_ARG(logits && n > 0, "lga_argmax: bad arguments");

@@ -208,6 +208,7 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
     finally:
         torch.set_default_dtype(prev)
     model.set_kv_cache(batch_size=1, device=device)
+    ops.preload_kernels()  # the runtime would otherwise build each prefill kernel inside the first prompt
     return model.eval()
 
 

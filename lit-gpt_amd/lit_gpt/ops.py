@@ -36,6 +36,7 @@ SIGNATURES = {
     "lga_version": [],
     "lga_last_error_string": [],
     "lga_device_info": [_I, _P, _P, _I],
+    "lga_preload_kernels": [],
     "lga_quantize": [_P, _I, _P, _P, _I, _I, _I, _I, _P],
     "lga_nf4_double_quant": [_P, _L, _P, _P, _P],
     "lga_q4_gemv": [_P, _P, _P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _I, _P],
@@ -360,6 +361,12 @@ def attention_decode_fused(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin,
         cos.shape[0], _dev(y, "y", torch.bfloat16), ws, cnt, n_head, n_query_groups, head_size, rope_n_elem, max_seq,
         n_splits, float(scale), _stream()))
     return y
+
+
+def preload_kernels() -> None:
+    """Build the prefill path's kernel objects now (model load) rather than at their first launch
+    (lga_preload_kernels; nothing runs on the GPU)."""
+    _check(load_library().lga_preload_kernels())
 
 
 _N_CU = None
