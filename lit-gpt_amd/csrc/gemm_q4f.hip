@@ -325,16 +325,22 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
   auto brow = [&](int j) {
     return DUAL ? (j / (FJ / 2)) * (BN / 2) + wn * (WC / 2) + (j % (FJ / 2)) * 16 : wn * WC + j * 16;
   };
-  auto mfma_sub = [&](const unsigned char* A, const unsigned char* B, int sub) {
+  // a K-step's fragments, per 32-deep sub: weight rows (A operand) and X rows (B operand) of this wave
+  struct Frags {
     bf16x8_t af[4], bfr[FJ];
+  };
+  auto frag_read = [&](const unsigned char* A, const unsigned char* B, int sub, Frags& f) {
 #pragma unroll
-    for (int j = 0; j < FJ; ++j) bfr[j] = *(const bf16x8_t*)(B + swz(brow(j) + fr, sub * 4 + fk));
+    for (int j = 0; j < FJ; ++j) f.bfr[j] = *(const bf16x8_t*)(B + swz(brow(j) + fr, sub * 4 + fk));
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8_t*)(A + swz(wm * 64 + i * 16 + fr, sub * 4 + fk));
+    for (int i = 0; i < 4; ++i) f.af[i] = *(const bf16x8_t*)(A + swz(wm * 64 + i * 16 + fr, sub * 4 + fk));
+  };
+  auto frag_mfma = [&](const Frags& f) {
 #pragma unroll
     for (int j = 0; j < FJ; ++j)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[j][i], 0, 0, 0);
+      for (int i = 0; i < 4; ++i)
+        acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.bfr[j], f.af[i], acc[j][i], 0, 0, 0);
   };
 
   constexpr int D = T::D;
@@ -352,16 +358,27 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
       if (nk >= D) wait_vm<(D - 1) * G>();
       else wait_vm<0>();
       __builtin_amdgcn_s_barrier();
-      for (int lk = 0; lk < nk; ++lk) {
+      for (int lk = 0; lk < nk; ++lk) {  // the schedule of the 4-bit loop below, without the dequantization
         const bool full = lk + D < nk;
+        const unsigned char* A = lds + (lk % NA) * A_BYTES;
+        const unsigned char* B = lds + NA * A_BYTES + (lk % NA) * B_BYTES;
+        Frags f0, f1;
+        frag_read(A, B, 0, f0);
+        __builtin_amdgcn_sched_barrier(0);
         if (full) {
           issue_a(lk + D);
           issue_b16(lk + D);
         }
-        const unsigned char* A = lds + (lk % NA) * A_BYTES;
-        const unsigned char* B = lds + NA * A_BYTES + (lk % NA) * B_BYTES;
-        mfma_sub(A, B, 0);
-        mfma_sub(A, B, 1);
+        __builtin_amdgcn_sched_barrier(0);
+        frag_read(A, B, 1, f1);
+        frag_mfma(f0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        frag_mfma(f1);
         if (full) wait_vm_lgkm<(D - 1) * G>();
         else wait_vm_lgkm<0>();
         __builtin_amdgcn_s_barrier();
@@ -384,23 +401,39 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
       dequant(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-      // iteration lk: issue group lk+D {A(lk+D), raw(lk+D+1)}; MFMA on A(lk), WB(lk) with raw(lk+1) dequantized
-      // between the two MFMA groups; wait for group lk+1 {A(lk+1), raw(lk+2)}; barrier
+      // iteration lk: the dequant reads of raw(lk+1) and sub 0's 8 fragment reads; group lk+D {A(lk+D),
+      // raw(lk+D+1)} issued under their latency (it fills buffers read one step earlier); sub 0's 16 MFMAs with
+      // sub 1's 8 reads two per 4 MFMAs; raw(lk+1) dequantized between them and sub 1's MFMAs; WB(lk+1) stored;
+      // wait for group lk+1 and the LDS traffic; barrier. Past the last stage the dequantization reads a stale raw
+      // buffer into the bf16 buffer nobody reads again (no branch). sched_barrier / sched_group_barrier pin the
+      // order: hipcc would otherwise sink the reads next to their MFMAs (one LDS round trip exposed per 4 MFMAs),
+      // and with at most 10 LDS reads in flight its counted lgkmcnt stays exact (the inline-asm dequant reads are
+      // older than every fragment read they could be confused with).
       for (int lk = 0; lk < nk; ++lk) {
         const bool full = lk + D + 1 < nk;
-        if (lk + D < nk) issue_a(lk + D);
-        if (full) issue_raw(lk + D + 1);
-        // past the last stage this dequantizes a stale raw buffer into the bf16 buffer nobody reads again: no
-        // branch, so the math can interleave with the MFMAs
         const unsigned char* A = lds + (lk % NA) * A_BYTES;
         const unsigned char* B = lds + OFF_WB + (lk & 1) * B_BYTES;
         raw_t wv;
         uint32_t sb, o[4 * NDW];
+        Frags f0, f1;
         dq_load(lk + 1, wv, sb);
-        mfma_sub(A, B, 0);
+        __builtin_amdgcn_sched_barrier(0);
+        frag_read(A, B, 0, f0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (lk + D < nk) issue_a(lk + D);
+        if (full) issue_raw(lk + D + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        frag_read(A, B, 1, f1);
+        frag_mfma(f0);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMAs
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // 2 LDS reads
+        }
+        __builtin_amdgcn_sched_barrier(0);
         dq_wait(wv, sb);
         dq_math(wv, sb, o);
-        mfma_sub(A, B, 1);
+        frag_mfma(f1);
         dq_store(lk + 1, o);
         if (full) wait_vm_lgkm<(D - 1) * G>();  // groups lk+2 .. lk+D, all full
         else wait_vm_lgkm<0>();
