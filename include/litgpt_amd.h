@@ -28,6 +28,8 @@ typedef struct ihipStream_t* lga_stream_t; /* == hipStream_t */
 /* weight formats */
 #define LGA_FMT_Q4G 0 /* int4, symmetric, per-group bf16 scale = bf16(absmax/7), nibble = q + 8 */
 #define LGA_FMT_NF4 1 /* bitsandbytes NF4 codebook, per-block fp32 absmax */
+#define LGA_FMT_BF16 2 /* unquantized bf16 weight [N][K] (lga_q4_gemm_fused / lga_q4_gemm_swiglu only) */
+#define LGA_FMT_FP4 3 /* bitsandbytes FP4 code (get_4bit_type('fp4'), "bnb.fp4"), per-block fp32 absmax */
 
 /* -- plumbing ---------------------------------------------------------------------------------------- */
 const char* lga_last_error_string(void);
@@ -41,10 +43,11 @@ int lga_preload_kernels(void);
 /* -- quantize at load (Lightning BitsandbytesPrecision.convert_module + bnb quantize on .to(device);
  *    generate/base.py:168, generate/tp.py:171-190) ------------------------------------------------------
  * w: (N, K) fp32 (w_is_bf16 = 0) or bf16 (1). qweight: (N, K/2) bytes, byte j = k 2j (low) | 2j+1 (high).
- * scales: (N, K/group) bf16 for Q4G, fp32 for NF4. Layout spec: oracle/quant.py. */
+ * scales: (N, K/group) bf16 for Q4G, fp32 for NF4 / FP4. Layout spec: oracle/quant.py. Every 4-bit entry point
+ * below takes fmt 0 / 1 / 3 (FP4 runs the NF4 kernels with its own 16-entry codebook). */
 int lga_quantize(const void* w, int w_is_bf16, uint8_t* qweight, void* scales, int N, int K, int group, int fmt,
                  lga_stream_t stream);
-/* bitsandbytes double quantization of nf4 statistics ("bnb.nf4-dq"; quantize_4bit(compress_statistics=True),
+/* bitsandbytes double quantization of nf4 / fp4 statistics ("bnb.nf4-dq", "bnb.fp4-dq"; quantize_4bit(compress_statistics=True),
  * generate/base.py:105): absmax (n fp32, bnb's flattened 64-blocks, i.e. the NF4 scales of lga_quantize) is
  * replaced in place by code[q] * absmax2 + offset — q = nearest entry of `code` (the 256-entry signed dynamic
  * map, device fp32) to (absmax - offset) / absmax2 per block of 256, offset = mean(absmax) (written to
@@ -67,7 +70,7 @@ int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const void* scale
 int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* scales, const void* bias, const void* residual,
                 void* y, int M, int N, int K, int group, int fmt, lga_stream_t stream);
 /* The same product with the dequantization fused into a 256 x 128 MFMA tile (csrc/gemm_q4f.hip): the weight
- * is never written out in bf16. fmt 0 int4-g / 1 nf4 / 2 bf16 weights [N][K]; needs N % 8 == 0, K % 64 == 0 and
+ * is never written out in bf16. fmt 0 int4-g / 1 nf4 / 2 bf16 weights [N][K] / 3 fp4; needs N % 8 == 0, K % 64 == 0 and
  * (4-bit) a power-of-two group >= 64 dividing K (lga_q4f_fits). Numerically the bnb path: bf16(value * scale)
  * weights, fp32 accumulation, one bf16 rounding (+bias), then + residual. */
 int lga_q4f_fits(int M, int N, int K, int group, int fmt);
@@ -185,6 +188,16 @@ int lga_comm_close(void* ptr);
 int lga_comm_free(void* ptr);
 int lga_allreduce_bf16(const void* x, const void* residual, void* y, int n, void* const* mailboxes, int rank,
                        int world, int cap, unsigned* seq_counter, unsigned* err, lga_stream_t stream);
+/* The row-parallel decode Linear and its all-reduce in ONE launch (generate/tp.py:53,57,70 hook the reduction on
+ * attn.proj / mlp.proj; lit_gpt/model.py:591-592 adds the residual): y (N) = lga_allreduce_bf16 of
+ * lga_q4_gemv(x, W, bias) over the ranks (+ residual), bit for bit — each workgroup pushes its partial rows into
+ * every rank's mailbox, the last-arriving workgroup of the rank raises the flags, waits for the peers and sums in
+ * rank order. Same mailboxes / sequence counter / error word as lga_allreduce_bf16 (calls of the two may be mixed);
+ * arrive_counter: 1 uint32 zeroed once (re-armed by the kernel). N % 8 == 0, N <= cap. Graph-capturable. */
+int lga_q4_gemv_allreduce(const void* x, const uint8_t* qweight, const void* scales, const void* bias,
+                          const void* residual, void* y, int N, int K, int group, int fmt, void* const* mailboxes,
+                          int rank, int world, int cap, unsigned* seq_counter, unsigned* arrive_counter,
+                          unsigned* err, lga_stream_t stream);
 
 /* -- greedy sampling (generate/base.py:30-47 at temperature 0): lowest index among the maxima; optionally
  *    writes the token (int32) and advances *pos_inout by one (generate/base.py:92) -------------------------- */

@@ -16,22 +16,11 @@
 // so the launch is graph-capturable (the replayed arguments never change).
 #include <string.h>
 
-#include "common.h"
+#include "comm.h"
 
 namespace lga {
 
-constexpr int kMaxRanks = 8;
-constexpr int kFlagStride = 64;                        // uint32 per flag (256 B)
-constexpr size_t kFlagBytes = kMaxRanks * kFlagStride * 4;
 constexpr int kCommThreads = 512;
-
-struct Peers {
-  unsigned char* mb[kMaxRanks];
-};
-
-__device__ __forceinline__ uint16_t* slot_ptr(unsigned char* mb, int slot, int src, int cap) {
-  return (uint16_t*)(mb + kFlagBytes) + ((size_t)slot * kMaxRanks + src) * cap;
-}
 
 __global__ void __launch_bounds__(kCommThreads) allreduce_kernel(const uint16_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ residual,
@@ -49,64 +38,21 @@ __global__ void __launch_bounds__(kCommThreads) allreduce_kernel(const uint16_t*
     uint4* dst = (uint4*)slot_ptr(peers.mb[r], slot, rank, cap);
     for (int i = t; i < n8; i += kCommThreads) dst[i] = ((const uint4*)x)[i];
   }
-  // 2. release: every storing thread's writes are complete and visible system-wide before any flag
-  //    (each storing wave drains its stores, the workgroup barrier orders them before the flag writers, and each
-  //    flag writer publishes with a system-scope RELEASE store behind an explicit drain: MI355X_MICROARCH.md
-  //    "Compiler hazard" — the asm wait keeps the release's write-back wait from being dropped)
+  // 2. release: every storing thread's writes are complete and visible system-wide before any flag (each storing
+  //    wave drains its stores, the workgroup barrier orders them before the flag writers: raise_flags in comm.h;
+  //    MI355X_MICROARCH.md "Compiler hazard" — the asm wait keeps the release's write-back wait from being dropped)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t < world && t != rank) {
-    unsigned* f = (unsigned*)peers.mb[t] + rank * kFlagStride;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  // 3. wait for every peer's flag in this rank's own mailbox (bounded: 5 s of the 100 MHz real-time clock — far
-  //    beyond any host-side skew between live ranks — then the error word is set and the kernel finishes with
-  //    whatever arrived, so a lost peer never hangs the GPU)
-  if (t < 64) {
-    const bool mine = t < world && t != rank;
-    const unsigned* f = (const unsigned*)peers.mb[rank] + (mine ? t : 0) * kFlagStride;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (true) {
-      const unsigned v = mine ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : seq;
-      if (__all((int)(v - seq) >= 0)) break;
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {
-        if (t == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-  }
+  raise_flags(peers, rank, world, seq, t);
+  // 3. wait for every peer's flag in this rank's own mailbox (bounded at 5 s, then the error word is set and the
+  //    kernel finishes with whatever arrived, so a lost peer never hangs the GPU)
+  wait_flags(peers, rank, world, seq, err, t);
   __syncthreads();
   // 4. ordered fp32 sum over ranks 0..W-1, bf16 once, then the residual add in the reference's rounding
-  for (int i = t; i < n8; i += kCommThreads) {
-    float acc[8];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
-    for (int r = 0; r < world; ++r) {
-      const uint4 v = r == rank ? ((const uint4*)x)[i] : ((const uint4*)slot_ptr(peers.mb[rank], slot, r, cap))[i];
-      const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc[2 * e] += bflo(d[e]);
-        acc[2 * e + 1] += bfhi(d[e]);
-      }
-    }
-    uint32_t o[4];
-    if (residual) {
-      const uint4 rv = ((const uint4*)residual)[i];
-      const uint32_t rd[4] = {rv.x, rv.y, rv.z, rv.w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        o[e] = pack2(round_bf(acc[2 * e]) + bflo(rd[e]), round_bf(acc[2 * e + 1]) + bfhi(rd[e]));
-    } else {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = pack2(acc[2 * e], acc[2 * e + 1]);
-    }
-    ((uint4*)y)[i] = make_uint4(o[0], o[1], o[2], o[3]);
-  }
+  const uint4* src[kMaxRanks];
+  for (int r = 0; r < world; ++r)
+    src[r] = r == rank ? (const uint4*)x : (const uint4*)slot_ptr(peers.mb[rank], slot, r, cap);
+  for (int i = t; i < n8; i += kCommThreads) ((uint4*)y)[i] = ordered_sum8(src, world, residual, i);
   __syncthreads();
   if (t == 0) *seq_ctr = seq;
 }

@@ -8,6 +8,24 @@ namespace lga {
 
 constexpr int kWave = 64;  // CDNA wavefront
 
+// 4-bit codebook formats (kernel template FMT 1, weight = code[nibble] * fp32 block absmax, one fp32 multiply):
+//   row 0 — bitsandbytes NF4 (LGA_FMT_NF4 = 1), get_4bit_type('nf4');
+//   row 1 — bitsandbytes FP4 (LGA_FMT_FP4 = 3), get_4bit_type('fp4') = {0, .0625, 8, 12, 4, 6, 2, 3, -0, -.0625,
+//           -8, -12, -4, -6, -2, -3} / 12: the sign-bit / 2-bit exponent / 1-bit mantissa code whose values
+//           dDequantizeFP4Tree returns (bnb 0.41.0 csrc/kernels.cu, upstream; reference generate/base.py:105).
+// Kernels take the row as a runtime index (`cb`), so FP4 shares every NF4 instantiation.
+constexpr int kFmtFP4 = 3;
+__host__ __device__ constexpr int codebook_of(int fmt) { return fmt == kFmtFP4 ? 1 : 0; }
+__host__ __device__ constexpr int kernel_fmt(int fmt) { return fmt == kFmtFP4 ? 1 : fmt; }
+static __constant__ float kCode4[2][16] = {
+    {-1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
+     -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
+     0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
+     0.7229568362236023f, 1.0f},
+    {0.0f, 0.005208333333333333f, 0.6666666666666666f, 1.0f, 0.3333333333333333f, 0.5f, 0.16666666666666666f,
+     0.25f, -0.0f, -0.005208333333333333f, -0.6666666666666666f, -1.0f, -0.3333333333333333f, -0.5f,
+     -0.16666666666666666f, -0.25f}};
+
 // ---- bf16 <-> f32 (bf16 stored as raw uint16_t; RNE on the way down, NaN kept a NaN) ----
 __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 __device__ __forceinline__ float bflo(uint32_t w) { return __uint_as_float(w << 16); }

@@ -72,11 +72,7 @@ __device__ __forceinline__ int bfly_index(int lane) {
                 : (R == 4 ? ((lane >> 5) & 1) * 2 + ((lane >> 4) & 1) : ((lane >> 5) & 1));
 }
 
-static __constant__ float kNF4v[16] = {
-    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
-    -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
-    0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
-    0.7229568362236023f, 1.0f};
+#define kNF4v (kCode4[0])  // (lab engine)
 
 // Scales stay raw bits until used: converting at load time makes the compiler wait for the scale load at once,
 // and vmcnt is in order, so that wait would also drain every weight load issued before it.

@@ -32,12 +32,6 @@ constexpr int TILE_BYTES = BM * BK * 2;  // one operand tile in LDS (128 rows x 
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
 
-__constant__ float kNF4g[16] = {
-    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
-    -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
-    0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
-    0.7229568362236023f, 1.0f};
-
 struct GemmArgs {
   const uint16_t* x;  // [M][K]
   const uint8_t* qw;  // [N][K/2]
@@ -46,6 +40,7 @@ struct GemmArgs {
   const uint16_t* residual;  // [M][N]
   uint16_t* y;               // [M][N]
   int M, N, K, G;
+  int cb = 0;  // codebook row of kCode4 (FMT 1): 0 nf4, 1 fp4
 };
 
 // X tile rows [r0, r0 + 8) of one 128-B-row tile, one wave instruction: lane L fills LDS bytes base + 16 L (row
@@ -76,7 +71,7 @@ __global__ void __launch_bounds__(256) gemm_q4_kernel(GemmArgs a) {
   const int m0 = by * BM, n0 = bx * BN;
   const int nk = (a.K + BK - 1) / BK, groups = FMT == 2 ? 1 : a.K / a.G;
   const size_t wrow_bytes = (size_t)a.K / 2;
-  if (tid < 16) wtab[tid] = FMT == 1 ? kNF4g[tid] : (float)(tid - 8);
+  if (tid < 16) wtab[tid] = FMT == 1 ? kCode4[a.cb][tid] : (float)(tid - 8);
 
   // global -> register staging: X 4 x 16 B per thread (row tid/8 + 32 i, chunk tid%8); W one row-half of 32 k
   uint4 xa[4];
@@ -228,9 +223,9 @@ extern "C" int lga_q4_gemm(const void* x, const uint8_t* qweight, const void* sc
   LGA_CHECK_ARG(x && qweight && scales && y, "lga_q4_gemm: null pointer");
   LGA_CHECK_ARG(M > 0 && N > 0 && K > 0 && K % 32 == 0, "lga_q4_gemm: K must be a positive multiple of 32");
   LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemm: group must be a multiple of 32 dividing K");
-  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemm: fmt must be 0 or 1");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_q4_gemm: fmt must be 0, 1 or 3");
   lga::GemmArgs a{(const uint16_t*)x, qweight, scales, (const uint16_t*)bias, (const uint16_t*)residual,
-                  (uint16_t*)y, M, N, K, group};
+                  (uint16_t*)y, M, N, K, group, lga::codebook_of(fmt)};
   const dim3 grid((N + lga::BN - 1) / lga::BN, (M + lga::BM - 1) / lga::BM);
   const bool glds = LGA_GEMM_GLDS && K % lga::BK == 0;
   if (fmt == 0) {

@@ -73,12 +73,6 @@ struct Tile {
   static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
-__constant__ float kNF4f[16] = {
-    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
-    -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
-    0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
-    0.7229568362236023f, 1.0f};
-
 struct Args {
   const uint16_t* x;   // [M][K]
   const void* w;       // packed [N][K/2] (4-bit) or bf16 [N][K]
@@ -93,6 +87,7 @@ struct Args {
   int splits;                // K-slices per tile (1: no split)
   unsigned* counters;        // split-K: one per tile, zero between launches (the last arriver re-zeroes it)
   float* slabs;              // split-K: [splits][M][N] fp32 partial products
+  int cb = 0;                // codebook row of kCode4 (FMT 1): 0 nf4, 1 fp4
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
@@ -165,7 +160,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
   const int groups = a.K / (FMT == 2 ? 1 : a.G);
   const int gshift = FMT == 2 ? 0 : 31 - __builtin_clz((unsigned)a.G);
   float* tab = (float*)(lds + OFF_MISC);
-  if (FMT == 1 && tid < 16) tab[tid] = kNF4f[tid];
+  if (FMT == 1 && tid < 16) tab[tid] = kCode4[a.cb][tid];
 
   // the weight tile's row r -> (matrix, row)
   auto wrow_ptr = [&](int r) -> const unsigned char* {
@@ -616,7 +611,8 @@ int run(Args a, int fmt, bool dual, void* ws, size_t ws_bytes, hipStream_t strea
     a.counters = (unsigned*)ws;
     a.slabs = (float*)((unsigned char*)ws + 4096);
   }
-  switch (fmt * 2 + (dual ? 1 : 0)) {
+  a.cb = lga::codebook_of(fmt);
+  switch (lga::kernel_fmt(fmt) * 2 + (dual ? 1 : 0)) {
     case 0: return launch_q4f<0, false>(a, p, stream);
     case 1: return launch_q4f<0, true>(a, p, stream);
     case 2: return launch_q4f<1, false>(a, p, stream);
@@ -655,7 +651,7 @@ extern "C" int lga_q4_gemm_fused(const void* x, const void* weight, const void* 
                                  const void* residual, void* y, int M, int N, int K, int group, int fmt,
                                  void* workspace, size_t workspace_bytes, hipStream_t stream) {
   LGA_CHECK_ARG(x && weight && y && (fmt == 2 || scales), "lga_q4_gemm_fused: null pointer");
-  LGA_CHECK_ARG(fmt >= 0 && fmt <= 2, "lga_q4_gemm_fused: fmt must be 0 (int4-g), 1 (nf4) or 2 (bf16)");
+  LGA_CHECK_ARG(fmt >= 0 && fmt <= 3, "lga_q4_gemm_fused: fmt must be 0 (int4-g), 1 (nf4), 2 (bf16) or 3 (fp4)");
   LGA_CHECK_ARG(q4f_fits(M, N, K, group, fmt),
                 "lga_q4_gemm_fused: needs N % 8 == 0, K % 64 == 0 and a power-of-two group >= 64 dividing K");
   LGA_CHECK_ARG(((uintptr_t)x | (uintptr_t)weight | (uintptr_t)y | (uintptr_t)residual) % 16 == 0,
@@ -669,7 +665,7 @@ extern "C" int lga_q4_gemm_swiglu(const void* x, const void* qw1, const void* sc
                                   void* y, int M, int N, int K, int group, int fmt, void* workspace,
                                   size_t workspace_bytes, hipStream_t stream) {
   LGA_CHECK_ARG(x && qw1 && qw2 && y && (fmt == 2 || (sc1 && sc2)), "lga_q4_gemm_swiglu: null pointer");
-  LGA_CHECK_ARG(fmt >= 0 && fmt <= 2, "lga_q4_gemm_swiglu: fmt must be 0 (int4-g), 1 (nf4) or 2 (bf16)");
+  LGA_CHECK_ARG(fmt >= 0 && fmt <= 3, "lga_q4_gemm_swiglu: fmt must be 0 (int4-g), 1 (nf4), 2 (bf16) or 3 (fp4)");
   LGA_CHECK_ARG(q4f_fits(M, N, K, group, fmt),
                 "lga_q4_gemm_swiglu: needs N % 8 == 0, K % 64 == 0 and a power-of-two group >= 64 dividing K");
   LGA_CHECK_ARG(((uintptr_t)x | (uintptr_t)qw1 | (uintptr_t)qw2 | (uintptr_t)y) % 16 == 0,

@@ -174,9 +174,10 @@ extern "C" int lga_q4_gemv(const void* x, const uint8_t* qweight, const void* sc
   LGA_CHECK_ARG(x && qweight && scales && y, "lga_q4_gemv: null pointer");
   LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0, "lga_q4_gemv: K must be a positive multiple of 32");
   LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv: group must be a multiple of 32 dividing K");
-  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv: fmt must be 0 (int4-g) or 1 (nf4)");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_q4_gemv: fmt must be 0 (int4-g), 1 (nf4) or 3 (fp4)");
   lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, (const uint16_t*)bias,
                   (const uint16_t*)residual, (const uint16_t*)norm_weight, (uint16_t*)y, N, K, group, norm_eps};
+  a.cb = lga::codebook_of(fmt);
   const int rc = fmt == 0 ? lga::dispatch<0, false>(a, variant, stream) : lga::dispatch<1, false>(a, variant, stream);
   if (rc) return rc;
   LGA_LAUNCH_RETURN();
@@ -189,9 +190,10 @@ extern "C" int lga_q4_gemv_swiglu(const void* x, const uint8_t* qweight1, const 
   LGA_CHECK_ARG(x && qweight1 && scales1 && qweight2 && scales2 && y, "lga_q4_gemv_swiglu: null pointer");
   LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0, "lga_q4_gemv_swiglu: K must be a positive multiple of 32");
   LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv_swiglu: bad group");
-  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv_swiglu: fmt must be 0 or 1");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_q4_gemv_swiglu: fmt must be 0, 1 or 3");
   lga::GemvArgs a{(const uint16_t*)x, qweight1, scales1, qweight2, scales2, nullptr, nullptr,
                   (const uint16_t*)norm_weight, (uint16_t*)y, N, K, group, norm_eps};
+  a.cb = lga::codebook_of(fmt);
   const int rc = fmt == 0 ? lga::dispatch<0, true>(a, variant, stream) : lga::dispatch<1, true>(a, variant, stream);
   if (rc) return rc;
   LGA_LAUNCH_RETURN();
@@ -203,11 +205,12 @@ extern "C" int lga_q4_gemv_experts(const void* x, const uint8_t* qweight, const 
   LGA_CHECK_ARG(x && qweight && scales && expert_ids && y, "lga_q4_gemv_experts: null pointer");
   LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0, "lga_q4_gemv_experts: K must be a positive multiple of 32");
   LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv_experts: bad group");
-  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv_experts: fmt must be 0 or 1");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_q4_gemv_experts: fmt must be 0, 1 or 3");
   LGA_CHECK_ARG(n_slots > 0 && n_slots <= 65535 && n_expert > 0 && w_stride >= (long long)N * K / 2 && s_stride > 0 &&
                     x_stride >= 0, "lga_q4_gemv_experts: bad routing geometry");
   lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, nullptr, nullptr, nullptr, (uint16_t*)y,
                   N, K, group, 0.0f, expert_ids, w_stride, s_stride, x_stride, n_expert, n_slots};
+  a.cb = lga::codebook_of(fmt);
   const int rc = fmt == 0 ? lga::dispatch<0, false>(a, variant, stream) : lga::dispatch<1, false>(a, variant, stream);
   if (rc) return rc;
   LGA_LAUNCH_RETURN();
@@ -222,13 +225,14 @@ extern "C" int lga_q4_gemv_swiglu_experts(const void* x, const uint8_t* qweight1
                 "lga_q4_gemv_swiglu_experts: null pointer");
   LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0, "lga_q4_gemv_swiglu_experts: K must be a positive multiple of 32");
   LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv_swiglu_experts: bad group");
-  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_gemv_swiglu_experts: fmt must be 0 or 1");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_q4_gemv_swiglu_experts: fmt must be 0, 1 or 3");
   LGA_CHECK_ARG(n_slots > 0 && n_slots <= 65535 && n_expert > 0 && w_stride >= (long long)N * K / 2 && s_stride > 0,
                 "lga_q4_gemv_swiglu_experts: bad routing geometry");
   LGA_CHECK_ARG(!norm_weight || K / 32 <= 128, "lga_q4_gemv_swiglu_experts: fused RMSNorm needs K <= 4096");
   lga::GemvArgs a{(const uint16_t*)x, qweight1, scales1, qweight2, scales2, nullptr, nullptr,
                   (const uint16_t*)norm_weight, (uint16_t*)y, N, K, group, norm_eps, expert_ids, w_stride, s_stride, 0,
                   n_expert, n_slots};
+  a.cb = lga::codebook_of(fmt);
   const int rc = fmt == 0 ? lga::dispatch<0, true>(a, variant, stream) : lga::dispatch<1, true>(a, variant, stream);
   if (rc) return rc;
   LGA_LAUNCH_RETURN();

@@ -44,11 +44,19 @@ struct GemvArgs {
   const int32_t* eidx;
   long long ew, es;
   int xs, n_expert, slots;
+  int cb = 0;  // codebook row of kCode4 (FMT 1): 0 nf4, 1 fp4
 };
 
+// LDS of gemv_q4_body: x pairs (2K B), chunk sums (K/32 floats), norm partials (16), codebook (16), then (LDS_OUT)
+// the workgroup's output rows at a 16-B-aligned offset
+__host__ __device__ inline size_t gemv_out_offset(int K) { return ((size_t)K * 2 + (K / 32) * 4 + 128 + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t gemv_lds_bytes(int K) { return gemv_out_offset(K) + 256; }
+__device__ __forceinline__ uint16_t* gemv_out_lds(unsigned char* smem, int K) { return (uint16_t*)(smem + gemv_out_offset(K)); }
+
 // One wave of a decode GEMV (see gemv.hip for the design). NW waves per workgroup (each its own row slot); the
-// workgroup stages x once for all of them.
-template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, int NW = 4>
+// workgroup stages x once for all of them. LDS_OUT (gemv_ar.hip): the workgroup's NW * RPR bf16 rows go to LDS
+// (gemv_out_lds) instead of a.y, for an epilogue that moves them on as 16-B pieces.
+template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, int NW = 4, bool LDS_OUT = false>
 __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char* smem) {
   if (a.eidx) {  // wave-uniform: one scalar load of the routed expert id, then plain pointer offsets
     const long long e = min(max(a.eidx[blockIdx.y], 0), a.n_expert - 1);
@@ -72,7 +80,7 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int NC = a.K / 32, n8 = a.K / 8, groups = a.K / a.G;
   const int row0 = (blk * NW + wave) * RPR;
-  if (FMT == 1 && t < 16) nf4[t] = kNF4v[t];
+  if (FMT == 1 && t < 16) nf4[t] = kCode4[a.cb][t];
   LGA_GTRACE_NOWAIT(0);
 
   // 1. activation (and norm weight) share of this thread: uint4 t, t+NT, ... (clamped, branch-free)
@@ -246,7 +254,11 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
     } else if (a.bias) {
       o += bf2f(a.bias[min(row, a.N - 1)]);
     }
-    if ((lane & (GROUP - 1)) == 0 && row < a.N) a.y[row] = f2bf(o);
+    if (LDS_OUT) {
+      if ((lane & (GROUP - 1)) == 0) gemv_out_lds(smem, a.K)[wave * RPR + vi] = f2bf(o);
+    } else if ((lane & (GROUP - 1)) == 0 && row < a.N) {
+      a.y[row] = f2bf(o);
+    }
     LGA_GTRACE(5);
   }
 }

@@ -31,7 +31,7 @@ __device__ __forceinline__ void gemv_q4_stream(GemvArgs a, unsigned char* smem) 
   const int NC = a.K / 32, n8 = a.K / 8, groups = a.K / a.G;
   const int gw = blockIdx.x * NW + wave, W = gridDim.x * NW;
   const int T = (a.N + RT - 1) / RT;
-  if (FMT == 1 && t < 16) nf4[t] = kNF4v[t];
+  if (FMT == 1 && t < 16) nf4[t] = kCode4[a.cb][t];
 
   // 1. activation (and norm weight) share of this thread, first in the vmcnt order
   uint4 xr[XI], nr[XI];

@@ -5,6 +5,9 @@
 // `cquantize_blockwise_*_nf4`, upstream). Formats are specified byte-for-byte in oracle/quant.py:
 //   LGA_FMT_Q4G (0): symmetric int4, group G along K, scale = bf16(absmax / 7), nibble = q + 8
 //   LGA_FMT_NF4 (1): bnb NF4 codebook, block G along K, fp32 absmax
+//   LGA_FMT_FP4 (3): bnb FP4 codebook (common.h kCode4[1]), block G along K, fp32 absmax; the code of w / absmax
+//                    is bnb's dQuantizeFP4 (csrc/kernels.cu, upstream): sign bit for x < 0, then the magnitude
+//                    against the seven literal pivots below (strict >, so a tie takes the smaller magnitude)
 // Packed byte j of a row holds k = 2j (low nibble) and k = 2j + 1 (high nibble).
 //
 // lga_nf4_double_quant: bitsandbytes' double quantization of the nf4 statistics ("bnb.nf4-dq",
@@ -16,11 +19,19 @@
 
 namespace lga {
 
-__constant__ float kNF4[16] = {
-    -1.0f, -0.6961928009986877f, -0.5250730514526367f, -0.39491748809814453f, -0.28444138169288635f,
-    -0.18477343022823334f, -0.09105003625154495f, 0.0f, 0.07958029955625534f, 0.16093020141124725f,
-    0.24611230194568634f, 0.33791524171829224f, 0.44070982933044434f, 0.5626170039176941f,
-    0.7229568362236023f, 1.0f};
+
+// dQuantizeFP4: pivots between the sorted magnitudes {0, 1/192, 1/6, 1/4, 1/3, 1/2, 2/3, 1} (codes 0, 1, 6, 7, 4,
+// 5, 2, 3), the float literals bitsandbytes compares against
+__device__ __forceinline__ unsigned fp4_code(float x) {
+  const unsigned sign = x < 0.0f ? 8u : 0u;
+  const float a = fabsf(x);
+  const float piv[7] = {0.00260417f, 0.0859375f, 0.20833333f, 0.29166667f, 0.4166667f, 0.583333f, 0.8333333f};
+  unsigned r = 0;
+#pragma unroll
+  for (int j = 0; j < 7; ++j) r += a > piv[j] ? 1u : 0u;
+  const unsigned code_of_rank = 0x32547610u;  // rank r -> code nibble r of this word: 0 1 6 7 4 5 2 3
+  return ((code_of_rank >> (4 * r)) & 0xFu) + sign;
+}
 
 template <bool IN_BF16>
 __device__ __forceinline__ float load_w(const void* w, size_t i) {
@@ -59,11 +70,13 @@ __global__ void __launch_bounds__(256) quantize_kernel(const void* __restrict__ 
         float q = rintf(v);
         q = fminf(fmaxf(q, -8.0f), 7.0f);
         c[h] = (unsigned)((int)q + 8);
+      } else if (FMT == 3) {
+        c[h] = fp4_code(v);
       } else {
         unsigned code = 0;
 #pragma unroll
         for (int j = 0; j < 15; ++j) {
-          const float mid = __fmul_rn(__fadd_rn(kNF4[j + 1], kNF4[j]), 0.5f);
+          const float mid = __fmul_rn(__fadd_rn(kCode4[0][j + 1], kCode4[0][j]), 0.5f);
           code += (mid < v) ? 1u : 0u;
         }
         c[h] = code;
@@ -148,7 +161,7 @@ __global__ void __launch_bounds__(256) double_quant_kernel(float* __restrict__ a
 // reads 256 and writes 1024 contiguous bytes.
 template <int FMT>
 __global__ void __launch_bounds__(256) dequant_kernel(const uint32_t* __restrict__ qw, const void* __restrict__ sc,
-                                                       uint4* __restrict__ w, long words, int K, int group) {
+                                                       uint4* __restrict__ w, long words, int K, int group, int cb) {
   const long c = (long)blockIdx.x * 256 + threadIdx.x;
   if (c >= words) return;
   const long n = c / (K / 8), k0 = (c % (K / 8)) * 8;
@@ -159,7 +172,8 @@ __global__ void __launch_bounds__(256) dequant_kernel(const uint32_t* __restrict
 #pragma unroll
   for (int e = 0; e < 8; e += 2) {
     const uint32_t lo = (q >> (4 * e)) & 0xF, hi = (q >> (4 * e + 4)) & 0xF;
-    const float vl = FMT == 0 ? (float)((int)lo - 8) : kNF4[lo], vh = FMT == 0 ? (float)((int)hi - 8) : kNF4[hi];
+    const float vl = FMT == 0 ? (float)((int)lo - 8) : kCode4[cb][lo];
+    const float vh = FMT == 0 ? (float)((int)hi - 8) : kCode4[cb][hi];
     o[e / 2] = pack2(mul_rn(vl, s), mul_rn(vh, s));
   }
   w[c] = make_uint4(o[0], o[1], o[2], o[3]);
@@ -172,12 +186,13 @@ extern "C" int lga_q4_dequantize(const uint8_t* qweight, const void* scales, voi
   LGA_CHECK_ARG(qweight && scales && w, "lga_q4_dequantize: null pointer");
   LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0 && group >= 32 && group % 32 == 0 && K % group == 0,
                 "lga_q4_dequantize: K must be a positive multiple of 32 and of the group (a multiple of 32)");
-  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_q4_dequantize: fmt must be 0 (int4-g) or 1 (nf4)");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_q4_dequantize: fmt must be 0 (int4-g), 1 (nf4) or 3 (fp4)");
   LGA_CHECK_ARG(((uintptr_t)qweight | (uintptr_t)w) % 16 == 0, "lga_q4_dequantize: 16-B aligned buffers required");
   const long words = (long)N * (K / 8);
   const dim3 grid((unsigned)((words + 255) / 256));
-  if (fmt == 0) lga::dequant_kernel<0><<<grid, 256, 0, stream>>>((const uint32_t*)qweight, scales, (uint4*)w, words, K, group);
-  else lga::dequant_kernel<1><<<grid, 256, 0, stream>>>((const uint32_t*)qweight, scales, (uint4*)w, words, K, group);
+  if (fmt == 0) lga::dequant_kernel<0><<<grid, 256, 0, stream>>>((const uint32_t*)qweight, scales, (uint4*)w, words, K, group, 0);
+  else lga::dequant_kernel<1><<<grid, 256, 0, stream>>>((const uint32_t*)qweight, scales, (uint4*)w, words, K, group,
+                                                        lga::codebook_of(fmt));
   LGA_LAUNCH_RETURN();
 }
 
@@ -194,15 +209,17 @@ extern "C" int lga_quantize(const void* w, int w_is_bf16, uint8_t* qweight, void
   LGA_CHECK_ARG(w && qweight && scales, "lga_quantize: null pointer");
   LGA_CHECK_ARG(N > 0 && K > 0 && group > 0 && group % 2 == 0 && K % group == 0,
                 "lga_quantize: K must be a positive multiple of an even group size");
-  LGA_CHECK_ARG(fmt == 0 || fmt == 1, "lga_quantize: fmt must be 0 (int4-g) or 1 (nf4)");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_quantize: fmt must be 0 (int4-g), 1 (nf4) or 3 (fp4)");
   const long total = (long)N * (K / group);
   const dim3 grid((unsigned)((total + 255) / 256)), block(256);
   if (w_is_bf16) {
     if (fmt == 0) lga::quantize_kernel<true, 0><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
-    else lga::quantize_kernel<true, 1><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
+    else if (fmt == 1) lga::quantize_kernel<true, 1><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
+    else lga::quantize_kernel<true, 3><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
   } else {
     if (fmt == 0) lga::quantize_kernel<false, 0><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
-    else lga::quantize_kernel<false, 1><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
+    else if (fmt == 1) lga::quantize_kernel<false, 1><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
+    else lga::quantize_kernel<false, 3><<<grid, block, 0, stream>>>(w, qweight, scales, N, K, group);
   }
   LGA_LAUNCH_RETURN();
 }

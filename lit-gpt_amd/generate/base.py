@@ -6,7 +6,7 @@ steps at ``input_pos = T, T+1, ...``, stop on ``eos_id``, ``NotImplementedError`
 short) and ``main`` (:96-187) with the same flags and the same stderr timing line. Differences:
   * greedy decoding (``temperature == 0``) runs each step as one HIP graph replay (lit_gpt/runtime.py) with the
     argmax on the device — the role ``--compile`` (CUDA graphs) plays in the reference;
-  * ``--quantize`` takes this build's formats (int4-g128, nf4 / bnb.nf4 / bnb.nf4-dq); without it the Linears
+  * ``--quantize`` takes this build's formats (int4-g128, nf4 / bnb.nf4 / bnb.nf4-dq, bnb.fp4 / bnb.fp4-dq); without it the Linears
     stay bf16 ``nn.Linear`` (BASELINE config 2) and run on the bf16 GEMV / GEMM kernels;
   * ``--synthetic NAME`` builds a random-init model of a registered config (no checkpoint, no tokenizer): the
     prompt is ``--prompt_len`` synthetic token ids.

@@ -70,6 +70,7 @@ class XgmiAllReduce:
                 ptrs.append(p.value)
         self.seq = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.arrive = torch.zeros(64, dtype=torch.int32, device=self.device)  # lga_q4_gemv_allreduce's counter
         self._agree(failure, "mailbox mapping")
         self._mailboxes = (ctypes.c_void_p * self.world)(*ptrs)
         self._self_test()
@@ -120,6 +121,30 @@ class XgmiAllReduce:
             ops._dev(x, "x", torch.bfloat16), res, ops._dev(y, "y", torch.bfloat16), x.numel(), self._mailboxes,
             self.rank, self.world, self.cap, self.seq.data_ptr(), self.err.data_ptr(), ops._stream()))
         return y
+
+    def gemv_all_reduce(self, lin, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                        out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """bf16(sum over ranks of ``lin(x)``) (+ residual) for a one-token row-parallel ``QuantLinear``, in ONE launch
+        (``lga_q4_gemv_allreduce``): the GEMV's workgroups push their partial rows into the mailboxes and the last
+        one sums the ranks. Bit-identical to ``all_reduce(lin(x), residual)``."""
+        N, K = lin.out_features, lin.in_features
+        if x.numel() != K or not self.supports_rows(N):
+            raise ValueError(f"XgmiAllReduce.gemv_all_reduce: needs one row of {K} and N % 8 == 0, N <= {self.cap}")
+        y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
+        res = None
+        if residual is not None:
+            if residual.numel() != N:
+                raise ValueError("XgmiAllReduce.gemv_all_reduce: residual shape differs from the output")
+            res = ops._dev(residual.contiguous(), "residual", torch.bfloat16)
+        ops._check(ops.load_library().lga_q4_gemv_allreduce(
+            ops._dev(x.contiguous(), "x", torch.bfloat16), ops._dev(lin.qweight, "qweight", torch.uint8),
+            ops._dev(lin.scales, "scales"), ops._opt(lin.bias, "bias", torch.bfloat16), res,
+            ops._dev(y, "y", torch.bfloat16), N, K, lin.group, lin.fmt, self._mailboxes, self.rank, self.world,
+            self.cap, self.seq.data_ptr(), self.arrive.data_ptr(), self.err.data_ptr(), ops._stream()))
+        return y
+
+    def supports_rows(self, n: int) -> bool:
+        return 0 < n <= self.cap and n % 8 == 0
 
     def errors(self) -> int:
         """Non-zero when a call timed out waiting for a peer since the last check (syncs; clears the word)."""
@@ -193,6 +218,30 @@ def tp_hook(module: torch.nn.Module):
     if len(hooks) == 1 and isinstance(hooks[0], functools.partial) and hooks[0].func is all_reduce_output:
         return hooks[0]
     return None
+
+
+def linear_reduce(hook, lin: torch.nn.Module, x: torch.Tensor, residual: Optional[torch.Tensor],
+                  compute) -> torch.Tensor:
+    """The row-parallel Linear under TP, its all-reduce hook and the Block residual add: ONE fused launch
+    (``XgmiAllReduce.gemv_all_reduce``) for a one-token 4-bit Linear when a communicator is installed, else
+    ``compute()`` (the plain Linear) followed by the hook's reduction (+ residual)."""
+    from lit_gpt.quantize import QuantLinear
+
+    comm = _default
+    world = hook.args[0]
+    if (comm is not None and comm.world == world and isinstance(lin, QuantLinear) and x.numel() == lin.in_features
+            and x.dtype == torch.bfloat16 and x.is_cuda and comm.supports_rows(lin.out_features)
+            and (residual is None or residual.numel() == lin.out_features) and fused_gemv_allreduce):
+        y = comm.gemv_all_reduce(lin, x.reshape(-1), residual)
+        return y.view(*x.shape[:-1], lin.out_features)
+    h = compute()
+    if residual is None:
+        return hook(lin, (), h)
+    return reduce_add(hook, lin, h, residual)
+
+
+# the fused row-parallel GEMV + all-reduce (lga_q4_gemv_allreduce); False keeps the two-launch form (tests A/B them)
+fused_gemv_allreduce = True
 
 
 def reduce_add(hook, module: torch.nn.Module, h: torch.Tensor, residual: torch.Tensor) -> torch.Tensor:

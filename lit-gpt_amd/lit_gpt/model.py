@@ -81,8 +81,17 @@ def _fused_prefill(M: int, N: int, K: int, group: int, fmt: int) -> bool:
     return M > 1 and ops.q4f_fits(M, N, K, group, fmt)
 
 
-def _lin(linear: nn.Module, x: torch.Tensor, **kw) -> torch.Tensor:
+def _lin(linear: nn.Module, x: torch.Tensor, *, reduce=None, **kw) -> torch.Tensor:
+    """Run a Linear on the MI355X kernels. ``reduce``: the TP all-reduce hook of a row-parallel projection
+    (generate/tp.py) — the partial output is summed over the ranks (+ ``residual``), fused into the GEMV launch for
+    one-token inputs (lit_gpt/comm.py linear_reduce)."""
     from lit_gpt.quantize import QuantLinear
+
+    if reduce is not None:
+        from lit_gpt import comm
+
+        res = kw.pop("residual", None)
+        return comm.linear_reduce(reduce, linear, x, res, lambda: _lin(linear, x, **kw))
 
     if isinstance(linear, QuantLinear):
         return linear(x, **kw)
@@ -225,12 +234,14 @@ class Block(nn.Module):
 
         ha = comm.tp_hook(self.attn)
         if ha is not None:
-            x = comm.reduce_add(ha, self.attn, self.attn.forward(x, cos, sin, mask, input_pos, norm=self.norm_1), x)
+            x = self.attn.forward(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x, reduce=ha)
         elif not self.attn._forward_hooks:
             x = self.attn(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x)
         else:
             x = ops.add(self.attn(self.norm_1(x), cos, sin, mask, input_pos).contiguous(), x.contiguous())
         hm = comm.tp_hook(self.mlp)
+        if hm is not None and isinstance(self.mlp, LLaMAMLP):
+            return self.mlp.forward(x, norm=self.norm_2, residual=x, reduce=hm)
         if hm is not None:
             return comm.reduce_add(hm, self.mlp, self.mlp.forward(x, norm=self.norm_2), x)
         if not self.mlp._forward_hooks:  # (a sparse-MoE block applies its experts' TP hooks itself)
@@ -268,9 +279,10 @@ class CausalSelfAttention(nn.Module):
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
                 input_pos: Optional[torch.Tensor] = None, *, norm: Optional["RMSNorm"] = None,
-                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """``norm`` / ``residual`` are fusion hooks used by Block.forward: the RMSNorm runs in the qkv GEMV
-        prologue and the residual add in the proj epilogue. Without them this is the reference forward."""
+                residual: Optional[torch.Tensor] = None, reduce=None) -> torch.Tensor:
+        """``norm`` / ``residual`` / ``reduce`` are fusion hooks used by Block.forward: the RMSNorm runs in the qkv
+        GEMV prologue, the residual add (and under TP the all-reduce hook ``reduce``) in the proj epilogue. Without
+        them this is the reference forward."""
         B, T, C = x.size()
         c = self.config
         H, G, hs = c.n_head, c.n_query_groups, c.head_size
@@ -311,7 +323,7 @@ class CausalSelfAttention(nn.Module):
         else:
             q = ops.rope_kv_append(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem)
             y = ops.attention(q, kc, vc, pos, H, G, hs, 1.0 / math.sqrt(hs), n_splits, workspace=ws)
-        out = _lin(self.proj, y.view(1, T, H * hs), residual=residual)
+        out = _lin(self.proj, y.view(1, T, H * hs), residual=residual, reduce=reduce)
         return out.view(B, T, -1)
 
     def scaled_dot_product_attention(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
@@ -367,8 +379,9 @@ class LLaMAMLP(nn.Module):
         self.proj = nn.Linear(config.intermediate_size, config.n_embd, bias=config.bias)
 
     def forward(self, x: torch.Tensor, *, norm: Optional["RMSNorm"] = None,
-                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
-        """proj(silu(fc_1 x) * fc_2 x) (model.py:712-716); ``norm``/``residual`` are Block fusion hooks."""
+                residual: Optional[torch.Tensor] = None, reduce=None) -> torch.Tensor:
+        """proj(silu(fc_1 x) * fc_2 x) (model.py:712-716); ``norm``/``residual``/``reduce`` are Block fusion hooks
+        (``reduce``: the TP all-reduce of the row-parallel proj, see CausalSelfAttention.forward)."""
         from lit_gpt.quantize import QuantLinear
 
         lead, C = x.shape[:-1], x.shape[-1]
@@ -402,7 +415,7 @@ class LLaMAMLP(nn.Module):
                     g = ops.q4_gemm_swiglu(n, _dense_weight(f1), None, _dense_weight(f2), None, I, C, 64, 2)
             if g is None:
                 g = ops.swiglu(_lin(f1, n).contiguous(), _lin(f2, n).contiguous())
-        out = _lin(self.proj, g, residual=residual)
+        out = _lin(self.proj, g, residual=residual, reduce=reduce)
         return out.view(*lead, -1)
 
 

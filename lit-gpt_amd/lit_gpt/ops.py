@@ -24,6 +24,8 @@ LIB_PATH = Path(os.environ.get("LGA_LIB", Path(__file__).resolve().parent / "_li
 
 FMT_Q4G = 0  # int4, symmetric, per-group bf16 scale
 FMT_NF4 = 1  # bitsandbytes NF4 codebook, per-block fp32 absmax
+FMT_BF16 = 2  # (prefill GEMM only) unquantized bf16 weight
+FMT_FP4 = 3  # bitsandbytes FP4 code, per-block fp32 absmax
 
 _P = ctypes.c_void_p
 _I = ctypes.c_int
@@ -74,6 +76,8 @@ SIGNATURES = {
     "lga_comm_close": [_P],
     "lga_comm_free": [_P],
     "lga_allreduce_bf16": [_P, _P, _P, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P, _P],
+    "lga_q4_gemv_allreduce": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P, _P,
+                              _P],
 }
 _RESTYPES = {"lga_q4f_workspace_bytes": ctypes.c_size_t, "lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
              "lga_comm_mailbox_bytes": ctypes.c_size_t}

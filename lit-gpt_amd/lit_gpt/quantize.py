@@ -15,6 +15,8 @@ Modes:
                                               mean, 8-bit dynamic-map codes per 256 blocks, fp32 absmax2): the
                                               kernels scale by the dequantized statistic code[q]*absmax2+offset,
                                               held expanded as fp32 per 64-block (lga_nf4_double_quant)
+  "bnb.fp4" / "bnb.fp4-dq"                    bitsandbytes FP4 code ({0, .0625, 8, 12, 4, 6, 2, 3} / 12, sign
+                                              bit), fp32 absmax per 64 (+ the same double quantization)
 Group sizes must divide in_features; for a TP row-shard whose width is not a multiple of the requested group
 (e.g. Llama-2-7B mlp.proj at TP=8: 1376) the largest of {128, 64, 32} that divides it is used.
 """
@@ -29,7 +31,7 @@ import torch.nn as nn
 
 from lit_gpt import ops
 
-_DOUBLE_QUANT = {"bnb.nf4-dq"}
+_DOUBLE_QUANT = {"bnb.nf4-dq", "bnb.fp4-dq"}
 _CODE_CACHE = {}
 
 
@@ -55,6 +57,8 @@ _MODES = {
     "nf4": (ops.FMT_NF4, 64),
     "bnb.nf4": (ops.FMT_NF4, 64),
     "bnb.nf4-dq": (ops.FMT_NF4, 64),
+    "bnb.fp4": (ops.FMT_FP4, 64),
+    "bnb.fp4-dq": (ops.FMT_FP4, 64),
 }
 
 
@@ -62,7 +66,7 @@ def parse_mode(mode: str):
     if mode not in _MODES:
         raise NotImplementedError(
             f"quantize mode {mode!r} is not supported on this build (supported: {sorted(_MODES)}); "
-            "bnb.fp4 / bnb.int8 have no MI355X kernel")
+            "bnb.int8 (LLM.int8 outlier decomposition) has no MI355X kernel")
     return _MODES[mode]
 
 
@@ -140,7 +144,7 @@ class QuantLinear(nn.Module):
         return y.view(*lead, self.out_features)
 
     def extra_repr(self) -> str:
-        kind = "int4" if self.fmt == ops.FMT_Q4G else "nf4"
+        kind = {ops.FMT_Q4G: "int4", ops.FMT_NF4: "nf4", ops.FMT_FP4: "fp4"}[self.fmt]
         return f"in_features={self.in_features}, out_features={self.out_features}, {kind}, group={self.group}"
 
 

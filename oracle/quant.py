@@ -13,6 +13,9 @@ int4-g128 ("q4g"): per group of G consecutive k (default 128):
     q = clamp(rint(w * inv), -8, 7) (round-half-even); nibble = q + 8
     packed byte j of a row holds k = 2j in its low nibble and k = 2j + 1 in its high nibble
     dequant: w' = float(nibble - 8) * float(scale)
+fp4-b64 ("fp4"): bitsandbytes' FP4 code (get_4bit_type('fp4') = {0, .0625, 8, 12, 4, 6, 2, 3, -0, ...} / 12),
+    blocks of 64, absmax fp32; code = dQuantizeFP4(w * (1/absmax)) — sign bit for x < 0, magnitude by strict >
+    against bnb's seven literal pivots; dequant: w' = FP4[code] * absmax (dDequantizeFP4Tree's values).
 nf4-b64 ("nf4"): bitsandbytes' NF4 codebook (bnb ``get_4bit_type('nf4')``),
     blocks of 64 along K, absmax fp32; code = argmin_i |w/absmax - NF4[i]| (ties -> lower index)
     using the codebook midpoints; same nibble packing; dequant: w' = NF4[code] * absmax.
@@ -30,6 +33,15 @@ NF4 = np.array([
     0.24611230194568634, 0.33791524171829224, 0.44070982933044434, 0.5626170039176941,
     0.7229568362236023, 1.0], dtype=np.float32)
 NF4_MID = ((NF4[1:] + NF4[:-1]) * np.float32(0.5)).astype(np.float32)
+
+# bitsandbytes 0.41.0 functional.get_4bit_type('fp4') (upstream, not vendored): the list divided by its absmax 12 in
+# float32; the same values dDequantizeFP4Tree (csrc/kernels.cu) returns per code
+FP4 = (np.array([0, 0.0625, 8.0, 12.0, 4.0, 6.0, 2.0, 3.0, -0.0, -0.0625, -8.0, -12.0, -4.0, -6.0, -2.0, -3.0],
+                dtype=np.float32) / np.float32(12.0)).astype(np.float32)
+# dQuantizeFP4's pivots (float literals in kernels.cu) between the sorted magnitudes and the code of each rank
+FP4_PIVOTS = np.array([0.00260417, 0.0859375, 0.20833333, 0.29166667, 0.4166667, 0.583333, 0.8333333],
+                      dtype=np.float32)
+FP4_CODE_OF_RANK = np.array([0, 1, 6, 7, 4, 5, 2, 3], dtype=np.uint8)
 
 
 def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
@@ -100,12 +112,45 @@ def quantize_nf4(w: np.ndarray, block: int = 64) -> Tuple[np.ndarray, np.ndarray
     return _pack_nibbles(codes.reshape(N, K)), absmax
 
 
+def quantize_fp4(w: np.ndarray, block: int = 64) -> Tuple[np.ndarray, np.ndarray]:
+    """(N, K) float32 -> (packed uint8 (N, K/2), absmax float32 (N, K/block)) — bnb quantize_4bit(quant_type='fp4')."""
+    w = np.ascontiguousarray(w, dtype=np.float32)
+    N, K = w.shape
+    if K % block:
+        raise ValueError(f"K={K} must be a multiple of the block size {block}")
+    g = w.reshape(N, K // block, block)
+    absmax = np.abs(g).max(axis=-1).astype(np.float32)
+    with np.errstate(divide="ignore"):
+        inv = np.where(absmax > 0, np.float32(1.0) / absmax, np.float32(0.0)).astype(np.float32)
+    xn = (g * inv[..., None]).astype(np.float32)
+    rank = (np.abs(xn)[..., None] > FP4_PIVOTS).sum(axis=-1)
+    codes = FP4_CODE_OF_RANK[rank] + np.where(xn < 0, 8, 0).astype(np.uint8)
+    return _pack_nibbles(codes.reshape(N, K)), absmax
+
+
+def dequantize_fp4(packed: np.ndarray, absmax: np.ndarray, block: int = 64) -> np.ndarray:
+    N = packed.shape[0]
+    codes = _unpack_nibbles(packed)
+    K = codes.shape[1]
+    vals = FP4[codes].reshape(N, K // block, block)
+    return (vals * absmax[..., None]).reshape(N, K).astype(np.float32)
+
+
 def dequantize_nf4(packed: np.ndarray, absmax: np.ndarray, block: int = 64) -> np.ndarray:
     N = packed.shape[0]
     codes = _unpack_nibbles(packed)
     K = codes.shape[1]
     vals = NF4[codes].reshape(N, K // block, block)
     return (vals * absmax[..., None]).reshape(N, K).astype(np.float32)
+
+
+def quantize_fmt(w: np.ndarray, fmt: int, group: int):
+    """By the C-ABI format code: 0 int4-g, 1 nf4, 3 fp4 (include/litgpt_amd.h LGA_FMT_*)."""
+    return {0: quantize_q4g, 1: quantize_nf4, 3: quantize_fp4}[fmt](w, group)
+
+
+def dequantize_fmt(packed: np.ndarray, scales: np.ndarray, fmt: int, group: int) -> np.ndarray:
+    return {0: dequantize_q4g, 1: dequantize_nf4, 3: dequantize_fp4}[fmt](packed, scales, group)
 
 
 # ---- bitsandbytes double quantization of the nf4 absmax ("bnb.nf4-dq", compress_statistics=True) --------------

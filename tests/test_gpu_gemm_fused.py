@@ -43,8 +43,8 @@ def _w(N, K, tag, std=0.02):
 
 def _quant(ops, w, fmt, group):
     qw, sc = ops.quantize(torch.from_numpy(w).to(DEV), fmt, group)
-    p, s = quant.quantize_q4g(w, group) if fmt == 0 else quant.quantize_nf4(w, group)
-    wd = quant.dequantize_q4g(p, s, group) if fmt == 0 else quant.dequantize_nf4(p, s, group)
+    p, s = quant.quantize_fmt(w, fmt, group)
+    wd = quant.dequantize_fmt(p, s, fmt, group)
     return qw, sc, bf16_np(wd)
 
 
@@ -59,7 +59,7 @@ def _swiglu_tol(a, b, g):
     return 2 ** -7 * (1.1 * abs(a) * abs(b) + abs(sa) * abs(b)) + 2 ** -8 * abs(g) + 2e-3
 
 
-@pytest.mark.parametrize("fmt,group", [(0, 128), (0, 64), (1, 64)])
+@pytest.mark.parametrize("fmt,group", [(0, 128), (0, 64), (1, 64), (3, 64)])
 @pytest.mark.parametrize("M,N,K", [(1, 128, 64), (17, 136, 256), (300, 392, 1024), (513, 256, 704)])
 @pytest.mark.parametrize("epi", ["none", "residual", "bias+residual"])
 def test_fused_gemm_matches_oracle(ops, fmt, group, M, N, K, epi):

@@ -46,12 +46,17 @@ def _weights(N, K, name, std=0.02):
 
 
 # ------------------------------------------------------------------------------------------------ quantizer
-@pytest.mark.parametrize("fmt,group", [(0, 128), (0, 64), (0, 32), (1, 64)])
+@pytest.mark.parametrize("fmt,group", [(0, 128), (0, 64), (0, 32), (1, 64), (3, 64)])
 @pytest.mark.parametrize("in_bf16", [False, True])
 def test_quantizer_bit_exact(ops, fmt, group, in_bf16):
     w = _weights(96, 512, f"qz{fmt}{group}")
     w[3, :group] = 0.0  # an all-zero group (scale 0)
     w[5, 7] = 0.5  # an outlier
+    if fmt == 3:  # every fp4 pivot exactly, just below and just above (relative to the block absmax 0.5)
+        piv = quant.FP4_PIVOTS.astype(np.float32) * np.float32(0.5)
+        edge = np.concatenate([piv, np.nextafter(piv, np.float32(0)), np.nextafter(piv, np.float32(1))])
+        w[5, 8:8 + edge.size] = edge
+        w[5, 32:32 + edge.size] = -edge
     if in_bf16:
         w = bf16_np(w)
     wt = torch.from_numpy(w).to(DEV)
@@ -62,7 +67,7 @@ def test_quantizer_bit_exact(ops, fmt, group, in_bf16):
         p_ref, s_ref = quant.quantize_q4g(w, group)
         np.testing.assert_array_equal(sc.view(torch.int16).cpu().numpy().view(np.uint16), s_ref)
     else:
-        p_ref, s_ref = quant.quantize_nf4(w, group)
+        p_ref, s_ref = quant.quantize_fmt(w, fmt, group)
         np.testing.assert_array_equal(sc.cpu().numpy(), s_ref)
     np.testing.assert_array_equal(qw.cpu().numpy(), p_ref)
 
@@ -93,12 +98,11 @@ def _ref_linear(x, wdeq, bias=None):
 def _deq(ops, w, fmt, group):
     key = ("d", id(w), fmt, group)
     if key not in _CACHE:
-        p, s = (quant.quantize_q4g(w, group) if fmt == 0 else quant.quantize_nf4(w, group))
-        _CACHE[key] = quant.dequantize_q4g(p, s, group) if fmt == 0 else quant.dequantize_nf4(p, s, group)
+        _CACHE[key] = quant.dequantize_fmt(*quant.quantize_fmt(w, fmt, group), fmt, group)
     return _CACHE[key]
 
 
-@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (0, 32)])
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (0, 32), (3, 64)])
 @pytest.mark.parametrize("N,K", [(12288, 4096), (4096, 11008), (1000, 256), (77, 1376), (640, 4096)])
 @pytest.mark.parametrize("variant", [-1, 0, 3, 4, 38])  # 4 / 38: the streaming form (2 / 3 workgroups per CU)
 def test_gemv_matches_reference(ops, fmt, group, N, K, variant):
@@ -115,7 +119,7 @@ def test_gemv_matches_reference(ops, fmt, group, N, K, variant):
     assert np.all(np.abs(y - ref) <= tol), float(np.max(np.abs(y - ref) - tol))
 
 
-@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (3, 64)])
 def test_gemv_fused_norm_residual_bias(ops, fmt, group):
     N, K = 1536, 1024
     w = _weights(N, K, "gvf")
@@ -132,7 +136,7 @@ def test_gemv_fused_norm_residual_bias(ops, fmt, group):
     assert np.max(np.abs(y - ref) - np.abs(ref) * 2 ** -7 - np.abs(h) * 2 ** -7) <= 2e-3
 
 
-@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (3, 64)])
 @pytest.mark.parametrize("variant", [-1, 0, 1, 36])  # -1 picks the streaming form at this shape, 0 / 1 one-shot
 def test_gemv_swiglu(ops, fmt, group, variant):
     N, K = 11008, 4096
@@ -151,7 +155,7 @@ def test_gemv_swiglu(ops, fmt, group, variant):
 
 
 # ------------------------------------------------------------------------------------------------ GEMM (prefill)
-@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (3, 64)])
 @pytest.mark.parametrize("M,N,K", [(200, 768, 256), (2048, 1024, 4096), (5, 640, 1376), (130, 4096, 11008)])
 def test_gemm_matches_reference(ops, fmt, group, M, N, K):
     if K % group:
@@ -169,7 +173,7 @@ def test_gemm_matches_reference(ops, fmt, group, M, N, K):
     assert np.max(err) <= 2e-3, float(np.max(err))
 
 
-@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (0, 32)])
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (0, 32), (3, 64)])
 @pytest.mark.parametrize("M,N,K", [(512, 768, 256), (600, 1024, 4096), (2048, 640, 1376), (517, 4096, 11008)])
 def test_dequantize_then_bf16_gemm_is_q4_gemm(ops, fmt, group, M, N, K):
     """lga_q4_dequantize == the oracle's bf16(dequantize) bit for bit; gemm.hip's bf16 GEMM over it == lga_q4_gemm
@@ -575,7 +579,7 @@ def test_moe_combine_matches_reference_loop(ops):
     assert torch.equal(got_nores, y)
 
 
-@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (3, 64)])
 def test_routed_expert_gemvs_equal_per_expert_gemvs(ops, fmt, group):
     """Slot s of the routed GEMVs == the plain GEMV on expert ids[s]'s own weights (same kernel, bit-exact)."""
     E, N, K = 4, 1408, 512

@@ -61,10 +61,11 @@ def oracle_for(cfg, sd, mode, dtype=torch.bfloat16):
                 return vb
             if mode == "int4-g128":
                 return quant.dequantize_q4g(*quant.quantize_q4g(vb, 128), 128)
-            packed, absmax = quant.quantize_nf4(vb, 64)
-            if mode == "bnb.nf4-dq":  # bitsandbytes double quantization of the statistics
+            fmt = 3 if mode.startswith("bnb.fp4") else 1
+            packed, absmax = quant.quantize_fmt(vb, fmt, 64)
+            if mode.endswith("-dq"):  # bitsandbytes double quantization of the statistics
                 absmax = quant.double_quant_absmax(absmax)[3]
-            return quant.dequantize_nf4(packed, absmax, 64)
+            return quant.dequantize_fmt(packed, absmax, fmt, 64)
         return v
 
     return om.OracleGPT(cfg, sd, dtype=dtype, weight_override=deq)
@@ -121,7 +122,7 @@ def _routing_ambiguous(margins, tol=2 ** -6):
 
 
 @pytest.mark.parametrize("key", list(CFGS))
-@pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bnb.nf4-dq", "bf16"])
+@pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bnb.nf4-dq", "bnb.fp4", "bnb.fp4-dq", "bf16"])
 @torch.inference_mode()
 def test_teacher_forced_logits_match_oracle(key, mode):
     if mode == "bf16" and key == "moe":

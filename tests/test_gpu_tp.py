@@ -69,6 +69,24 @@ def test_xgmi_allreduce_late_peer_raises_on_every_rank(tmp_path):
     assert out.read_text() == "ok", out.read_text()
 
 
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("nproc", [2, 4, 8])
+def test_fused_gemv_allreduce_bit_exact_vs_two_launches(nproc, tmp_path):
+    """lga_q4_gemv_allreduce (row-parallel GEMV with the all-reduce in its epilogue, one launch) == lga_q4_gemv +
+    lga_allreduce_bf16 bit for bit at 2, 4 and 8 ranks: 7B / 70B-like shard shapes, int4 / nf4 / fp4, bias and
+    residual, graph-captured (mixed with plain all-reduce calls in one sequence) and back-to-back eager calls."""
+    out = tmp_path / "status.txt"
+    _launch("gemv_allreduce_worker.py", nproc, [out], timeout=280)
+    assert out.read_text() == "ok", out.read_text()
+
+
+@pytest.mark.timeout(120)
+def test_fused_gemv_allreduce_late_peer_raises_on_every_rank(tmp_path):
+    out = tmp_path / "status.txt"
+    _launch("gemv_allreduce_worker.py", 2, [out, "--late-peer"], timeout=100)
+    assert out.read_text() == "ok", out.read_text()
+
+
 @pytest.mark.timeout(600)
 def test_tp8_llama2_70b_rank_geometry(tmp_path):
     """BASELINE config 4 per rank: Llama-2-70B at TP=8 (C 8192, 8 query heads + 1 KV group per rank, qkv 1280 rows,

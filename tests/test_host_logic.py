@@ -256,3 +256,33 @@ def test_double_quant_code_table_is_bitsandbytes_dynamic_map():
     q, amax2, off, out = quant.double_quant_absmax(a)
     assert q.dtype == np.uint8 and amax2.shape == (4,) and np.abs(out - a).max() <= 0.01 * a.max()
 
+
+
+def test_fp4_oracle_is_bitsandbytes_fp4():
+    """oracle/quant.py's bnb.fp4 restatement: the code table is bitsandbytes get_4bit_type('fp4') (= the values
+    dDequantizeFP4Tree returns), every pivot sits halfway between neighbouring magnitudes, quantize picks the
+    nearest code (ties to the smaller magnitude), dequantize -> quantize is idempotent, and the modes parse as
+    fp4 blocks of 64 on the nf4 kernels' table slot."""
+    import numpy as np
+
+    from lit_gpt import ops
+    from lit_gpt.quantize import parse_mode
+    from oracle import quant
+
+    tree = {0: 0.0, 1: 5.208333333e-03, 2: 0.66666667, 3: 1.0, 4: 0.33333333, 5: 0.5, 6: 0.16666667, 7: 0.25}
+    for c, v in tree.items():
+        assert quant.FP4[c] == np.float32(v) and quant.FP4[c + 8] == -np.float32(v)
+    assert np.signbit(quant.FP4[8])
+    mags = np.sort(quant.FP4[:8])
+    np.testing.assert_allclose(quant.FP4_PIVOTS, (mags[1:] + mags[:-1]) / 2, rtol=2e-6)
+    assert list(quant.FP4[quant.FP4_CODE_OF_RANK]) == list(mags)
+    rng = np.random.default_rng(7)
+    w = rng.standard_normal((8, 256)).astype(np.float32)
+    p, a = quant.quantize_fp4(w, 64)
+    d = quant.dequantize_fp4(p, a, 64)
+    xn = w.reshape(8, 4, 64) / a[..., None]
+    err = np.abs(d.reshape(8, 4, 64) / a[..., None] - xn)
+    nearest = np.abs(np.abs(xn)[..., None] - mags).min(-1)
+    assert np.all(err <= nearest + 1e-6)
+    np.testing.assert_array_equal(quant.dequantize_fp4(*quant.quantize_fp4(d, 64), 64), d)
+    assert parse_mode("bnb.fp4") == (ops.FMT_FP4, 64) and parse_mode("bnb.fp4-dq") == (ops.FMT_FP4, 64)
