@@ -209,6 +209,33 @@ int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, 
 int lga_argmax_embed(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
                      const void* table, int n_embd, int vocab, void* emb_out, lga_stream_t stream);
 
+/* -- fp32 forward (the reference's --precision 32-true, generate/base.py:132; BASELINE config 1 pythia-160m fp32):
+ *    float32 weights and activations, no bf16 rounding; plumbing-sized kernels (csrc/fp32.hip) -------------- */
+/* y (M, N) = x (M, K) . w (N, K)^T (+ bias[N]) (+ residual (M, N)) — F.linear (lit_gpt/model.py:519,619,656,699-702) */
+int lga_f32_linear(const float* x, const float* w, const float* bias, const float* residual, float* y, int M, int N,
+                   int K, lga_stream_t stream);
+/* torch.nn.LayerNorm over rows of n (config.py:137-144): two-pass mean / biased variance, (x - mean) * rstd * w + b */
+int lga_f32_layernorm(const float* x, const float* w, const float* b, float* y, int rows, int n, float eps,
+                      lga_stream_t stream);
+/* F.gelu (exact erf, or tanh when approximate_tanh) — GptNeoxMLP (model.py:699-702) */
+int lga_f32_gelu(const float* a, float* y, long n, int approximate_tanh, lga_stream_t stream);
+/* y = a + b (the Block residual adds, model.py:584-593) */
+int lga_f32_add(const float* a, const float* b, float* y, long n, lga_stream_t stream);
+/* lga_rope_kv_append in fp32: apply_rope on the first rope_n_elem dims (model.py:641-644, 767-773) + KVCache.forward
+ * (:788-795); caches (G, max_seq, hs) fp32 */
+int lga_f32_rope_kv_append(const float* qkv, float* q_out, float* k_cache, float* v_cache, const int64_t* cache_pos,
+                           const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, int T,
+                           int n_head, int n_query_groups, int head_size, int rope_n_elem, int max_seq,
+                           lga_stream_t stream);
+/* SDPA (model.py:651, 658-665) in fp32: q (T, H, hs), caches (G, max_seq, hs), query t attends keys 0..input_pos[t];
+ * y (T, H*hs). head_size <= 256, max_seq <= 32768. */
+int lga_f32_attention(const float* q, const float* k_cache, const float* v_cache, const int64_t* input_pos, float* y,
+                      int T, int n_head, int n_query_groups, int head_size, int max_seq, float scale,
+                      lga_stream_t stream);
+/* lga_argmax over fp32 logits (generate/base.py:30-47 at temperature 0) */
+int lga_argmax_f32(const float* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
+                   lga_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

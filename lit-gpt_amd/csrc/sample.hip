@@ -93,6 +93,36 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict
   }
 }
 
+// fp32 logits (the reference's --precision 32-true, lit_gpt/fp32 path): same selection, one workgroup
+__global__ void __launch_bounds__(1024) argmax_f32_kernel(const float* __restrict__ logits, int n,
+                                                          int64_t* __restrict__ out_idx, int32_t* __restrict__ token_out,
+                                                          int64_t* __restrict__ pos_inout) {
+  float bv = -INFINITY;
+  int bi = 0x7FFFFFFF;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) take(logits[i], i, bv, bi);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float ov = __shfl_xor(bv, off);
+    const int oi = __shfl_xor(bi, off);
+    take(ov, oi, bv, bi);
+  }
+  __shared__ float sv[16];
+  __shared__ int si[16];
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sv[wave] = bv;
+    si[wave] = bi;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) take(sv[w], si[w], bv, bi);
+    if (bi >= n) bi = 0;
+    if (out_idx) *out_idx = bi;
+    if (token_out) *token_out = bi;
+    if (pos_inout) *pos_inout += 1;
+  }
+}
+
 }  // namespace lga
 
 int lga::preload_sample() {
@@ -121,5 +151,12 @@ extern "C" int lga_argmax_embed(const void* logits, int n, int64_t* out_idx, int
   else
     lga::argmax_kernel<false, true><<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, out_idx, token_out, pos_inout,
                                                             (const uint16_t*)table, n_embd, vocab, (uint16_t*)emb_out);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_argmax_f32(const float* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
+                              hipStream_t stream) {
+  LGA_CHECK_ARG(logits && n > 0, "lga_argmax_f32: bad arguments");
+  lga::argmax_f32_kernel<<<1, 1024, 0, stream>>>(logits, n, out_idx, token_out, pos_inout);
   LGA_LAUNCH_RETURN();
 }

@@ -46,7 +46,7 @@ def sample(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] 
             logits = torch.full_like(logits, float("-inf")).scatter_(-1, i, v)
         probs = torch.nn.functional.softmax(logits.float() / temperature, dim=-1)
         return multinomial_num_samples_1(probs)
-    return ops.argmax(logits.to(torch.bfloat16).contiguous())
+    return ops.argmax((logits if logits.dtype == torch.float32 else logits.to(torch.bfloat16)).contiguous())
 
 
 def next_token(model: GPT, input_pos: torch.Tensor, x: torch.Tensor, **kwargs: Any) -> torch.Tensor:
@@ -124,7 +124,8 @@ def _check_collectives() -> None:
 
 def build_model(config: Config, *, quantize: Optional[str], device: torch.device, seed: int = 1234,
                 checkpoint_path: Optional[Path] = None, max_seq_length: Optional[int] = None,
-                fabric=None, rope_positions: str = "reference", prefill_rows: Optional[int] = None) -> GPT:
+                fabric=None, rope_positions: str = "reference", prefill_rows: Optional[int] = None,
+                dtype: torch.dtype = torch.bfloat16) -> GPT:
     """Instantiate on the meta device, then materialise (load, or random-init as GPT._init_weights) the float
     weights on the GPU in the model's parameter order; with ``fabric`` (world_size / global_rank, generate/tp.py)
     every block is sharded (``tensor_parallel_block``) and quantized as soon as its weights exist, so a rank holds
@@ -136,7 +137,12 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
     ``with fabric.init_tensor(): model.max_seq_length = ...`` does under bf16-true / bnb precision
     (generate/base.py:153-157): positions above 256 round to bf16. ``"exact"`` keeps fp32 positions.
     ``prefill_rows`` (the prompt length about to be served) is accepted for API stability; the prefill GEMMs are
-    hand-written (csrc/gemm_q4f.hip) and need no per-shape tuning or warm-up."""
+    hand-written (csrc/gemm_q4f.hip) and need no per-shape tuning or warm-up. ``dtype`` float32 is the reference's
+    ``--precision 32-true`` (GPT-NeoX family, csrc/fp32.hip; no quantization, no TP)."""
+    if dtype not in (torch.bfloat16, torch.float32):
+        raise NotImplementedError(f"precision with dtype {dtype}: the MI355X path computes in bf16 or fp32")
+    if dtype == torch.float32 and (quantize is not None or (fabric is not None and fabric.world_size > 1)):
+        raise NotImplementedError("32-true runs unquantized on one device (BASELINE config 1)")
     if rope_positions not in ("reference", "exact"):
         raise ValueError(f"rope_positions must be 'reference' or 'exact', got {rope_positions!r}")
     from lit_gpt.quantize import QuantizedPrecision
@@ -184,14 +190,14 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
         open_block = blk
         mod = model.get_submodule(mod_name)
         if state is not None:
-            t = state[name].to(device=device, dtype=torch.bfloat16)
+            t = state[name].to(device=device, dtype=dtype)
         elif attr == "weight" and (isinstance(mod, (torch.nn.Linear, torch.nn.Embedding))):
             t = torch.empty(p.shape, dtype=torch.float32, device=device).normal_(0.0, 0.02, generator=gen)
-            t = t.to(torch.bfloat16)
+            t = t.to(dtype)
         elif attr == "bias":
-            t = torch.zeros(p.shape, dtype=torch.bfloat16, device=device)
+            t = torch.zeros(p.shape, dtype=dtype, device=device)
         else:  # norm weights
-            t = torch.ones(p.shape, dtype=torch.bfloat16, device=device)
+            t = torch.ones(p.shape, dtype=dtype, device=device)
         setattr(mod, attr, torch.nn.Parameter(t, requires_grad=False))
     if open_block is not None:
         finish(model.transformer.h[open_block])
@@ -201,13 +207,15 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
         tp.shard_config(fabric, model)
     torch.cuda.empty_cache()
     prev = torch.get_default_dtype()
-    torch.set_default_dtype(torch.bfloat16 if rope_positions == "reference" else torch.float32)
+    # (32-true: the reference's default dtype stays float32, so its positions are exact)
+    torch.set_default_dtype(torch.bfloat16 if rope_positions == "reference" and dtype == torch.bfloat16
+                            else torch.float32)
     try:
         model.max_seq_length = max_seq_length or config.block_size
         model.cos, model.sin = model.rope_cache(device=device)
     finally:
         torch.set_default_dtype(prev)
-    model.set_kv_cache(batch_size=1, device=device)
+    model.set_kv_cache(batch_size=1, device=device, dtype=dtype)
     ops.preload_kernels()  # the runtime would otherwise build each prefill kernel inside the first prompt
     return model.eval()
 
@@ -219,8 +227,9 @@ def main(prompt: str = "What food do llamas eat?", *, num_samples: int = 1, max_
          quantize: Optional[str] = None, precision: Optional[str] = None, compile: bool = False,
          synthetic: Optional[str] = None, prompt_len: int = 16) -> None:
     precision = precision or "bf16-true"
-    if precision != "bf16-true":
-        raise NotImplementedError("the MI355X path computes in bf16 (precision bf16-true)")
+    if precision not in ("bf16-true", "32-true"):
+        raise NotImplementedError("the MI355X path computes in bf16 (bf16-true) or fp32 (32-true)")
+    dtype = torch.float32 if precision == "32-true" else torch.bfloat16
     device = torch.device("cuda", torch.cuda.current_device())
     tokenizer = None
     if synthetic is not None:
@@ -242,7 +251,7 @@ def main(prompt: str = "What food do llamas eat?", *, num_samples: int = 1, max_
     print(f"Loading model {str(checkpoint_path or synthetic)!r} with {config.__dict__}", file=sys.stderr)
     t0 = time.perf_counter()
     model = build_model(config, quantize=quantize, device=device, checkpoint_path=checkpoint_path,
-                        max_seq_length=max_returned_tokens, prefill_rows=prompt_length)
+                        max_seq_length=max_returned_tokens, prefill_rows=prompt_length, dtype=dtype)
     print(f"Time to load the model weights: {time.perf_counter() - t0:.02f} seconds.", file=sys.stderr)
     torch.manual_seed(1234)
     eos_id = tokenizer.eos_id if tokenizer is not None else None

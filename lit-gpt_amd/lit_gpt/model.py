@@ -77,6 +77,24 @@ def _dense(linear: nn.Linear, x: torch.Tensor, *, residual: Optional[torch.Tenso
     return y.view(*lead, N)
 
 
+def _dense_f32(linear: nn.Linear, x: torch.Tensor, *, residual: Optional[torch.Tensor] = None,
+               norm_weight: Optional[torch.Tensor] = None, norm_eps: float = 1e-5) -> torch.Tensor:
+    """F.linear in float32 (the reference's --precision 32-true, BASELINE config 1): lga_f32_linear."""
+    if norm_weight is not None:
+        raise NotImplementedError("fp32 path: RMSNorm-family blocks are not built in fp32 (GPT-NeoX LayerNorm is)")
+    w = linear.weight
+    if not w.is_contiguous():
+        linear.weight.data = w.data.contiguous()
+        w = linear.weight
+    N, K = w.shape
+    if x.dtype != torch.float32:
+        raise TypeError(f"fp32 Linear expects fp32 activations (32-true), got {x.dtype}")
+    lead = x.shape[:-1]
+    x2 = x.reshape(-1, K).contiguous()
+    res = None if residual is None else residual.reshape(x2.shape[0], N).contiguous()
+    return ops.f32_linear(x2, w, bias=linear.bias, residual=res).view(*lead, N)
+
+
 def _fused_prefill(M: int, N: int, K: int, group: int, fmt: int) -> bool:
     return M > 1 and ops.q4f_fits(M, N, K, group, fmt)
 
@@ -95,6 +113,8 @@ def _lin(linear: nn.Module, x: torch.Tensor, *, reduce=None, **kw) -> torch.Tens
 
     if isinstance(linear, QuantLinear):
         return linear(x, **kw)
+    if isinstance(linear, nn.Linear) and linear.weight.is_cuda and linear.weight.dtype == torch.float32:
+        return _dense_f32(linear, x, **kw)
     if isinstance(linear, nn.Linear) and linear.weight.is_cuda:
         return _dense(linear, x, **kw)
     raise NotImplementedError(
@@ -299,8 +319,8 @@ class CausalSelfAttention(nn.Module):
             if not isinstance(self.kv_cache, KVCache):
                 raise TypeError("You need to call `gpt.set_kv_cache()`")
             kv = self.kv_cache
-            if kv.k.dtype != torch.bfloat16:  # reference KVCache.forward casts to the activation dtype (:790-791)
-                kv.k, kv.v = kv.k.to(torch.bfloat16), kv.v.to(torch.bfloat16)
+            if kv.k.dtype != qkv.dtype:  # reference KVCache.forward casts to the activation dtype (:790-791)
+                kv.k, kv.v = kv.k.to(qkv.dtype), kv.v.to(qkv.dtype)
             kc, vc = kv.k, kv.v
             pos = input_pos
             # callers may pass the full cos/sin tables (our GPT.forward) or rows pre-selected by input_pos (the
@@ -311,12 +331,12 @@ class CausalSelfAttention(nn.Module):
         S = kc.size(-2)
         ws = None
         n_splits = 1
-        if T == 1:
+        if T == 1 and qkv.dtype == torch.bfloat16:
             n_splits = ops.decode_splits(G, H // G, hs, S)
             ws = getattr(self, "_attn_ws", None)
             if ws is None or ws.key != (1, H, G, hs, n_splits) or ws.counters.device != dev:
                 ws = self._attn_ws = ops.AttentionWorkspace(1, H, G, hs, n_splits, dev)
-        if T == 1 and self.fuse_decode and ops.decode_fusable(hs, c.rope_n_elem):
+        if T == 1 and self.fuse_decode and ops.decode_fusable(hs, c.rope_n_elem) and qkv.dtype == torch.bfloat16:
             # decode token: RoPE + KV-append + attention in a single launch
             y = ops.attention_decode_fused(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem,
                                            1.0 / math.sqrt(hs), n_splits, workspace=ws)
@@ -513,9 +533,9 @@ class LayerNorm(nn.LayerNorm):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not x.is_cuda:
             _gpu_only("LayerNorm")
-        w = self.weight.to(torch.bfloat16) if self.weight.dtype != torch.bfloat16 else self.weight
-        b = None if self.bias is None else (self.bias.to(torch.bfloat16) if self.bias.dtype != torch.bfloat16
-                                            else self.bias)
+        dt = torch.float32 if x.dtype == torch.float32 else torch.bfloat16  # 32-true or bf16-true
+        w = self.weight.to(dt) if self.weight.dtype != dt else self.weight
+        b = None if self.bias is None else (self.bias.to(dt) if self.bias.dtype != dt else self.bias)
         return ops.layernorm(x.contiguous(), w, b, self.eps)
 
 

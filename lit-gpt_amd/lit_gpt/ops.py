@@ -76,6 +76,13 @@ SIGNATURES = {
     "lga_comm_close": [_P],
     "lga_comm_free": [_P],
     "lga_allreduce_bf16": [_P, _P, _P, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P, _P],
+    "lga_f32_linear": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lga_f32_layernorm": [_P, _P, _P, _P, _I, _I, _F, _P],
+    "lga_f32_gelu": [_P, _P, _L, _I, _P],
+    "lga_f32_add": [_P, _P, _P, _L, _P],
+    "lga_f32_rope_kv_append": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
+    "lga_f32_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
+    "lga_argmax_f32": [_P, _I, _P, _P, _P, _P],
     "lga_q4_gemv_allreduce": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P, _P,
                               _P],
 }
@@ -299,7 +306,14 @@ def rope_kv_append(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin, n_head,
     (G, max_seq, hs) caches at rows cache_pos."""
     T = qkv.shape[0]
     max_seq = k_cache.shape[-2]
-    q = q_out if q_out is not None else torch.empty(T, n_head, head_size, dtype=torch.bfloat16, device=qkv.device)
+    q = q_out if q_out is not None else torch.empty(T, n_head, head_size, dtype=qkv.dtype, device=qkv.device)
+    if qkv.dtype == torch.float32:  # --precision 32-true (csrc/fp32.hip)
+        _check(load_library().lga_f32_rope_kv_append(
+            _dev(qkv, "qkv", torch.float32), _dev(q, "q", torch.float32), _dev(k_cache, "k_cache", torch.float32),
+            _dev(v_cache, "v_cache", torch.float32), _dev(cache_pos, "cache_pos", torch.int64),
+            _dev(rope_pos, "rope_pos", torch.int64), _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32),
+            cos.shape[0], T, n_head, n_query_groups, head_size, rope_n_elem, max_seq, _stream()))
+        return q
     _check(load_library().lga_rope_kv_append(
         _dev(qkv, "qkv", torch.bfloat16), _dev(q, "q", torch.bfloat16), _dev(k_cache, "k_cache", torch.bfloat16),
         _dev(v_cache, "v_cache", torch.bfloat16), _dev(cache_pos, "cache_pos", torch.int64),
@@ -328,7 +342,13 @@ def attention(q, k_cache, v_cache, input_pos, n_head, n_query_groups, head_size,
     """y (T, H*hs): causal attention of q (T, H, hs) over the (G, max_seq, hs) caches, keys <= input_pos[t]."""
     T = q.shape[0]
     max_seq = k_cache.shape[-2]
-    y = out if out is not None else torch.empty(T, n_head * head_size, dtype=torch.bfloat16, device=q.device)
+    y = out if out is not None else torch.empty(T, n_head * head_size, dtype=q.dtype, device=q.device)
+    if q.dtype == torch.float32:  # --precision 32-true: one workgroup per (row, head), no splits (csrc/fp32.hip)
+        _check(load_library().lga_f32_attention(
+            _dev(q, "q", torch.float32), _dev(k_cache, "k_cache", torch.float32),
+            _dev(v_cache, "v_cache", torch.float32), _dev(input_pos, "input_pos", torch.int64),
+            _dev(y, "y", torch.float32), T, n_head, n_query_groups, head_size, max_seq, float(scale), _stream()))
+        return y
     if n_splits > 1:
         if workspace is None or workspace.key != (T, n_head, n_query_groups, head_size, n_splits):
             workspace = AttentionWorkspace(T, n_head, n_query_groups, head_size, n_splits, q.device)
@@ -402,19 +422,27 @@ def decode_splits(n_query_groups: int, q_per_kv: int, head_size: int, max_seq: i
 
 
 def embedding(idx, table, out=None):
+    """out[t] = table[idx[t]]; bf16 or fp32 rows (fp32 rows move as pairs of 16-bit words: a byte copy)."""
     T = idx.numel()
     V, C = table.shape
-    y = out if out is not None else torch.empty(T, C, dtype=torch.bfloat16, device=table.device)
+    y = out if out is not None else torch.empty(T, C, dtype=table.dtype, device=table.device)
     if idx.dtype not in (torch.int32, torch.int64):
         raise TypeError(f"embedding: idx must be int32/int64, got {idx.dtype}")
+    if table.dtype not in (torch.bfloat16, torch.float32):
+        raise TypeError(f"embedding: table must be bf16 or fp32, got {table.dtype}")
+    words = C * (2 if table.dtype == torch.float32 else 1)
     _check(load_library().lga_embedding(_dev(idx, "idx"), int(idx.dtype == torch.int64),
-                                        _dev(table, "table", torch.bfloat16), _dev(y, "y", torch.bfloat16), T, C, V,
+                                        _dev(table, "table", table.dtype), _dev(y, "y", table.dtype), T, words, V,
                                         _stream()))
     return y
 
 
 def add(a, b, out=None):
     y = out if out is not None else torch.empty_like(a)
+    if a.dtype == torch.float32:
+        _check(load_library().lga_f32_add(_dev(a, "a", torch.float32), _dev(b, "b", torch.float32),
+                                          _dev(y, "y", torch.float32), a.numel(), _stream()))
+        return y
     _check(load_library().lga_add(_dev(a, "a", torch.bfloat16), _dev(b, "b", torch.bfloat16),
                                   _dev(y, "y", torch.bfloat16), a.numel(), _stream()))
     return y
@@ -424,6 +452,11 @@ def layernorm(x, weight, bias, eps, out=None):
     """torch.nn.LayerNorm over the last dim of a contiguous bf16 GPU tensor (GPT-NeoX)."""
     n = x.shape[-1]
     y = out if out is not None else torch.empty_like(x)
+    if x.dtype == torch.float32:
+        _check(load_library().lga_f32_layernorm(_dev(x, "x", torch.float32), _dev(weight, "weight", torch.float32),
+                                                _opt(bias, "bias", torch.float32), _dev(y, "y", torch.float32),
+                                                x.numel() // n, n, float(eps), _stream()))
+        return y
     _check(load_library().lga_layernorm(_dev(x, "x", torch.bfloat16), _dev(weight, "weight", torch.bfloat16),
                                         _opt(bias, "bias", torch.bfloat16), _dev(y, "y", torch.bfloat16),
                                         x.numel() // n, n, float(eps), _stream()))
@@ -435,6 +468,10 @@ def gelu(a, approximate: str = "none", out=None):
     if approximate not in ("none", "tanh"):
         raise ValueError(f"gelu approximate must be 'none' or 'tanh', got {approximate!r}")
     y = out if out is not None else torch.empty_like(a)
+    if a.dtype == torch.float32:
+        _check(load_library().lga_f32_gelu(_dev(a, "a", torch.float32), _dev(y, "y", torch.float32), a.numel(),
+                                           int(approximate == "tanh"), _stream()))
+        return y
     _check(load_library().lga_gelu(_dev(a, "a", torch.bfloat16), _dev(y, "y", torch.bfloat16), a.numel(),
                                    int(approximate == "tanh"), _stream()))
     return y
@@ -451,10 +488,26 @@ def argmax(logits, out_idx=None, token_out=None, pos_inout=None):
     """Greedy token (lowest index on ties); optionally writes the token buffer and advances input_pos."""
     n = logits.numel()
     idx = out_idx if out_idx is not None else torch.empty(1, dtype=torch.int64, device=logits.device)
+    if logits.dtype == torch.float32:
+        _check(load_library().lga_argmax_f32(_dev(logits, "logits", torch.float32), n,
+                                             _dev(idx, "out_idx", torch.int64), _opt(token_out, "token_out", torch.int32),
+                                             _opt(pos_inout, "pos_inout", torch.int64), _stream()))
+        return idx
     _check(load_library().lga_argmax(_dev(logits, "logits", torch.bfloat16), n, _dev(idx, "out_idx", torch.int64),
                                      _opt(token_out, "token_out", torch.int32),
                                      _opt(pos_inout, "pos_inout", torch.int64), _stream()))
     return idx
+
+
+def f32_linear(x, weight, bias=None, residual=None, out=None):
+    """y (M, N) = x (M, K) . W (N, K)^T (+ bias) (+ residual), all fp32 (--precision 32-true, csrc/fp32.hip)."""
+    N, K = weight.shape
+    M = x.numel() // K
+    y = out if out is not None else torch.empty(M, N, dtype=torch.float32, device=x.device)
+    _check(load_library().lga_f32_linear(_dev(x, "x", torch.float32), _dev(weight, "weight", torch.float32),
+                                         _opt(bias, "bias", torch.float32), _opt(residual, "residual", torch.float32),
+                                         _dev(y, "y", torch.float32), M, N, K, _stream()))
+    return y
 
 
 def argmax_embed(logits, table, emb_out, out_idx=None, token_out=None, pos_inout=None):

@@ -27,6 +27,7 @@ DEV = torch.device("cuda", 0)
 
 
 def _pythia(mode="bf16", max_seq=16 + 128):
+    """mode: "bf16" (bf16-true), "fp32" (32-true, the reference's config-1 precision) or a 4-bit quantize mode."""
     from lit_gpt import GPT, Config
     from lit_gpt.quantize import QuantizedPrecision
 
@@ -34,11 +35,12 @@ def _pythia(mode="bf16", max_seq=16 + 128):
     sd = synth.state_dict(cfg, seed=1234)
     model = GPT(cfg)
     model.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
-    model = model.to(device=DEV, dtype=torch.bfloat16)
-    if mode != "bf16":
+    dt = torch.float32 if mode == "fp32" else torch.bfloat16
+    model = model.to(device=DEV, dtype=dt)
+    if mode not in ("bf16", "fp32"):
         QuantizedPrecision(mode).convert_module(model, DEV)
     model.max_seq_length = max_seq
-    model.set_kv_cache(1, device=DEV)
+    model.set_kv_cache(1, device=DEV, dtype=dt)
     return cfg, sd, model.eval()
 
 
@@ -104,3 +106,43 @@ def test_pythia160m_greedy_generate_follows_reference():
         assert y[16 + i] == ref[16 + i], f"step {i}: {y[16 + i]} vs reference {ref[16 + i]}"
         checked += 1
     assert checked >= 4, checked
+
+
+FP32_TOL = 2e-5  # relative to max |logit|: fp32 summation-order differences over 12 blocks (measured ~1e-6)
+
+
+@torch.inference_mode()
+def test_pythia160m_fp32_step0_logits_match_reference_fixture(golden):
+    """BASELINE config 1 in its own precision (--precision 32-true, csrc/fp32.hip): the prefill's last-row logits
+    equal the reference's fp32 logits (fixture g1, generated by importing /root/reference) to fp32 summation-order
+    noise — no bf16 rounding anywhere on the path."""
+    g = golden("g1_pythia160m_greedy.npz")
+    cfg, sd, model = _pythia("fp32")
+    prompt = torch.from_numpy(g["prompt"]).long().view(1, -1).to(DEV)
+    lg = model(prompt, torch.arange(prompt.shape[1], device=DEV))[0, -1].cpu()
+    assert lg.dtype == torch.float32
+    ref = torch.from_numpy(g["step0_logits"]).float()
+    err = float((lg - ref).abs().max() / ref.abs().max())
+    assert err <= FP32_TOL, err
+
+
+@torch.inference_mode()
+def test_pythia160m_fp32_greedy_128_tokens_equal_reference():
+    """generate/base.py's loop in fp32 (prefill + HIP-graph decode, fp32 argmax on the device): the 128 greedy
+    tokens equal the reference's fp32 run (fixture) at every step up to the first whose reference top-1/top-2 margin
+    is within the fp32 noise bound (after which two correct fp32 executions may legitimately fork)."""
+    from generate.base import generate
+
+    g = np.load(__import__("pathlib").Path(__file__).parent / "golden" / "g1_pythia160m_greedy.npz")
+    cfg, sd, model = _pythia("fp32")
+    prompt = torch.from_numpy(g["prompt"]).to(DEV)
+    y = generate(model, prompt, 16 + 128, temperature=0.0).cpu().numpy()
+    ref, margins, absmax = g["tokens"], g["margins"], g["logits_absmax"]
+    checked = 0
+    for i in range(128):
+        if margins[i] <= 4 * FP32_TOL * absmax[i]:
+            break
+        assert y[16 + i] == ref[16 + i], f"step {i}: {y[16 + i]} vs reference {ref[16 + i]}"
+        checked += 1
+    assert checked >= 64, checked
+    print(f"fp32: {checked} of 128 greedy tokens checked against the reference's fp32 run")
