@@ -8,11 +8,10 @@
 // hs*2 contiguous bytes, read by a "row group" of hs/8 lanes at 16 B per lane.
 //
 // Work decomposition: grid (splits, G, T); a 256-thread workgroup owns one (split, query group, query row) and
-// all q_per_kv heads of that group (GQA/MQA read each K/V row once). Keys go to the splits in runs of one row per
-// row group, cyclically: the first blocks' addresses do not depend on the live position, so their loads fly while
-// input_pos and q are fetched, every split gets the same key count to within one run, and a captured HIP graph
-// stays valid as p grows. Inside, each row group streams UNR keys per block (2*UNR 16-B loads in flight per lane)
-// with an online softmax; row groups merge with shuffles, waves via LDS.
+// all q_per_kv heads of that group (GQA/MQA read each K/V row once). The split boundaries are computed in the
+// kernel from the live position (chunk = ceil((p+1)/splits)), so every split is busy whatever the context
+// length and a captured HIP graph stays valid as p grows. Inside, each row group streams UNR keys per step
+// (2*UNR 16-B loads in flight per lane) with an online softmax; row groups merge with shuffles, waves via LDS.
 // With splits > 1 every workgroup publishes (m, l, o) write-through (sc1) and bumps a per-(t, group) counter;
 // the workgroup that arrives last merges the splits and writes the bf16 output (flash-decoding combine inside
 // the same launch; MI355X_MICROARCH.md "Valid forms" row 1), then re-arms the counter for the next launch.
@@ -68,37 +67,14 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
   const int rg = wave * RGW + lane / LPR;
   const int sub = lane % LPR;
   LGA_TRACE(0);
-  const uint16_t* kbase = kc + (size_t)g * max_seq * HS + sub * 8;
-  const uint16_t* vbase = vc + (size_t)g * max_seq * HS + sub * 8;
-  // Keys are dealt to the splits in runs of RG (one per row group): key q * KS + split * RG + rg for q = 0, 1, ...
-  // (KS = RG * splits) belongs to row group rg of `split`. The first blocks' addresses therefore do not depend on
-  // the live position — their loads are issued before input_pos and q arrive, one load round trip earlier than
-  // position-derived chunks — and the splits' key counts differ by at most RG at every position. A wave's 4 row
-  // groups read 4 consecutive key rows (1 KB of K, 1 KB of V), a workgroup 16.
-  const int KS = RG * n_splits;
-  const int j_first = split * RG + rg;
-  // one block = UNR keys per row group, KS apart; rows clamped to jmax (rows past the live keys are masked in
-  // consume())
-  auto fetch = [&](uint4 (&kv)[UNR], uint4 (&vv)[UNR], int j0, int jmax) {
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int j = max(min(j0 + u * KS, jmax), 0);
-      kv[u] = ld_kv(kbase + (size_t)j * HS);
-      vv[u] = ld_kv(vbase + (size_t)j * HS);
-    }
-  };
-  uint4 ka[UNR], va[UNR], kb[UNR], vb[UNR];
-  if (PIPE) {
-    fetch(ka, va, j_first, max_seq - 1);
-    fetch(kb, vb, j_first + UNR * KS, max_seq - 1);
-  }
   const long p = input_pos[t];
   const int L = (int)min(p + 1, (long)max_seq);  // keys 0..p (never past the cache)
+  const int chunk = (L + n_splits - 1) / n_splits;
+  const int k_lo = split * chunk;
+  const int k_hi = min(k_lo + chunk, L);
   LGA_TRACE(1);
-  const int k_end = FUSED ? min(L, (int)p) : L;  // fused: key p is scored from registers below
-  const bool owns_new = FUSED && p < max_seq && (int)((p / RG) % n_splits) == split;
-  const int nq = k_end > split * RG ? (k_end - split * RG + KS - 1) / KS : 0;  // key rows q of this split
-  const int nb = (nq + UNR - 1) / UNR;                                         // ... in blocks of UNR
+  const bool owns_new = FUSED && p < max_seq && k_lo <= p && p < k_hi;
+  const int k_end = FUSED ? min(k_hi, (int)p) : k_hi;  // fused: key p is scored from registers below
   const float* cr = nullptr;
   const float* sr = nullptr;
   if (FUSED) {
@@ -126,8 +102,9 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[h][i] = 0.0f;
   }
-  // one block = UNR keys per row group: scores, online-softmax rescale, P.V (masked keys score -inf; a row group
-  // whose keys are all masked so far keeps m = -inf, l = 0, o = 0)
+  const uint16_t* kbase = kc + (size_t)g * max_seq * HS + sub * 8;
+  const uint16_t* vbase = vc + (size_t)g * max_seq * HS + sub * 8;
+  // one step = UNR keys per row group: scores, online-softmax rescale, P.V (masked keys score -inf)
   auto consume = [&](const uint4 (&kv)[UNR], const uint4 (&vv)[UNR], int j0) {
 #pragma unroll
     for (int h = 0; h < QPK; ++h) {
@@ -141,17 +118,16 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
 #pragma unroll
         for (int i = 0; i < 8; ++i) d = fmaf(qf[h][i], kf[i], d);
         const float sd = row_group_sum<LPR>(d) * scale;  // whole row group active: DPP stays inside it
-        s[u] = (j0 + u * KS < k_end) ? sd : -INFINITY;
+        s[u] = (j0 + u * RG < k_end) ? sd : -INFINITY;
         mx = fmaxf(mx, s[u]);
       }
-      const float mref = mx == -INFINITY ? 0.0f : mx;  // all masked so far: exp(-inf - 0) = 0, no NaN
-      const float c = expf(m[h] - mref);               // m = -inf (first live step) -> 0
+      const float c = expf(m[h] - mx);  // m = -inf (first step) -> 0
       l[h] *= c;
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[h][i] *= c;
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const float e = expf(s[u] - mref);  // masked keys: exp(-inf) = 0
+        const float e = expf(s[u] - mx);  // masked keys: exp(-inf) = 0
         l[h] += e;
         float vf[8];
         unpack8(vv[u], vf);
@@ -161,24 +137,34 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
       m[h] = mx;
     }
   };
-  if (PIPE) {
-    // two blocks in flight: block i + 2's loads are issued right after block i is consumed, so they stream under
-    // block i + 1's math
-    const int bstride = UNR * KS;
-    for (int i = 0; i < nb; i += 2) {
-      const int j0 = j_first + i * bstride;
-      consume(ka, va, j0);
-      if (i + 2 < nb) fetch(ka, va, j0 + 2 * bstride, k_end - 1);
-      if (i + 1 < nb) {
-        consume(kb, vb, j0 + bstride);
-        if (i + 3 < nb) fetch(kb, vb, j0 + 3 * bstride, k_end - 1);
-      }
+  // clamped duplicate rows (past k_end) are masked in consume() and hit in cache
+  auto fetch = [&](uint4 (&kv)[UNR], uint4 (&vv)[UNR], int j0) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int j = max(min(j0 + u * RG, k_end - 1), 0);
+      kv[u] = ld_kv(kbase + (size_t)j * HS);
+      vv[u] = ld_kv(vbase + (size_t)j * HS);
     }
-  } else {
-    for (int i = 0; i < nb; ++i) {
-      const int j0 = j_first + i * UNR * KS;
-      fetch(ka, va, j0, k_end - 1);
+  };
+  const int j_first = k_lo + rg;
+  if (PIPE && k_lo < k_end) {
+    // software pipeline: the next step's 2*UNR loads are issued before this step's math, so every row group
+    // keeps 2-4 steps of K/V in flight and a split costs one load round trip plus its streaming time
+    uint4 ka[UNR], va[UNR], kb[UNR], vb[UNR];
+    fetch(ka, va, j_first);
+    int j0 = j_first;
+    for (; j0 + RG * UNR < k_end; j0 += 2 * RG * UNR) {
+      fetch(kb, vb, j0 + RG * UNR);
       consume(ka, va, j0);
+      if (j0 + 2 * RG * UNR < k_end) fetch(ka, va, j0 + 2 * RG * UNR);
+      consume(kb, vb, j0 + RG * UNR);
+    }
+    if (j0 < k_end) consume(ka, va, j0);
+  } else {
+    for (int j0 = j_first; j0 < k_end; j0 += RG * UNR) {
+      uint4 kv[UNR], vv[UNR];
+      fetch(kv, vv, j0);
+      consume(kv, vv, j0);
     }
   }
   LGA_TRACE(3);

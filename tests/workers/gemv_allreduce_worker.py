@@ -34,6 +34,8 @@ def main():
     c = comm.XgmiAllReduce(device=DEV)
     if "--late-peer" in sys.argv:
         return late_peer(c, out, world, rank)
+    if "--time" in sys.argv:
+        return timing(c, out, world, rank)
     bad = []
     # (N, K per rank, mode, bias): 7B attn.proj / mlp.proj shards at this world size, 70B-like widths, fp4 / nf4
     cases = [(4096, 4096 // world, "int4-g128", False), (4096, 11008 // world, "int4-g128", False),
@@ -95,6 +97,54 @@ def main():
     c.close()
     if rank == 0:
         Path(out).write_text("ok" if not bad and err == 0 else f"FAIL err={err} {bad[:5]}")
+    dist.destroy_process_group()
+
+
+def timing(c, out, world, rank):
+    """us per call, graph-captured (32 calls per replay), of the fused launch vs GEMV + all-reduce for the 7B
+    attn.proj / mlp.proj shards at this world size — every rank on one GPU, so both forms share the device: a
+    relative number, not a multi-GPU one (tools/tp_fused_time.py)."""
+    res_lines = []
+    for name, N, K in (("attn.proj", 4096, 4096 // world), ("mlp.proj", 4096, 11008 // world)):
+        lin = QuantLinear.from_float(rnd((N, K), 5 + rank, 0.02).bfloat16().to(DEV), None, "int4-g128", DEV)
+        x = rnd((K,), 11 + rank).bfloat16().to(DEV)
+        res = rnd((N,), 12).bfloat16().to(DEV)
+        ys = [torch.empty(N, dtype=torch.bfloat16, device=DEV) for _ in range(2)]
+        part = torch.empty(1, N, dtype=torch.bfloat16, device=DEV)
+        times = {}
+        for form in ("fused", "two"):
+            def call():
+                if form == "fused":
+                    c.gemv_all_reduce(lin, x, res, out=ys[0])
+                else:
+                    from lit_gpt import ops
+                    ops.q4_gemv(x, lin.qweight, lin.scales, N, K, lin.group, lin.fmt, out=part.view(-1))
+                    c.all_reduce(part.view(-1), residual=res, out=ys[1])
+            for _ in range(4):
+                call()
+            torch.cuda.synchronize()
+            dist.barrier()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for _ in range(32):
+                    call()
+            best = 1e9
+            for _ in range(5):
+                torch.cuda.synchronize()
+                dist.barrier()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                g.replay()
+                e.record()
+                e.synchronize()
+                best = min(best, s.elapsed_time(e) * 1e3 / 32)
+            times[form] = best
+        res_lines.append(f"world {world} {name} N={N} K={K}: fused {times['fused']:.2f} us, "
+                         f"gemv + all-reduce {times['two']:.2f} us per call (rank {rank})")
+    dist.barrier()
+    c.close()
+    if rank == 0:
+        Path(out).write_text("\n".join(res_lines) + "\n")
     dist.destroy_process_group()
 
 
