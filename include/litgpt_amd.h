@@ -193,7 +193,7 @@ int lga_allreduce_bf16(const void* x, const void* residual, void* y, int n, void
  * lga_q4_gemv(x, W, bias) over the ranks (+ residual), bit for bit — each workgroup pushes its partial rows into
  * every rank's mailbox, the last-arriving workgroup of the rank raises the flags, waits for the peers and sums in
  * rank order. Same mailboxes / sequence counter / error word as lga_allreduce_bf16 (calls of the two may be mixed);
- * arrive_counter: 1 uint32 zeroed once (re-armed by the kernel). N % 8 == 0, N <= cap. Graph-capturable. */
+ * arrive_counter: 576 uint32 (9 counters at a 256-B stride) zeroed once (re-armed by the kernel). N % 8 == 0, N <= cap. Graph-capturable. */
 int lga_q4_gemv_allreduce(const void* x, const uint8_t* qweight, const void* scales, const void* bias,
                           const void* residual, void* y, int N, int K, int group, int fmt, void* const* mailboxes,
                           int rank, int world, int cap, unsigned* seq_counter, unsigned* arrive_counter,

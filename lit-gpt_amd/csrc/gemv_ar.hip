@@ -22,11 +22,16 @@ struct ArArgs {
   Peers peers;
   int rank, world, cap;
   unsigned* seq;     // call sequence (shared with lga_allreduce_bf16)
-  unsigned* arrive;  // arrival counter, zero between launches (the last arriver re-arms it)
+  unsigned* arrive;  // kArriveWords arrival counters, zero between launches (each last arriver re-arms its own)
   unsigned* err;
   const uint16_t* residual;  // [N] or null
   uint16_t* y;               // [N]
 };
+
+// Arrivals go through one counter per blockIdx % 8 class (a class shares an XCD under round-robin placement; that is
+// speed only, never correctness), each 256 B apart, and the last arriver of each class bumps the top counter: 8 + 32
+// serialized device-scope atomics instead of 256 on one word (MI355X_MICROARCH.md "fanin": ≈12 ns each).
+constexpr int kArriveStride = 64;  // uint32 (256 B)
 
 template <int RPR, int CPT, int FMT>
 __global__ void __launch_bounds__(256) gemv_q4_ar_kernel(GemvArgs a, ArArgs c) {
@@ -48,11 +53,22 @@ __global__ void __launch_bounds__(256) gemv_q4_ar_kernel(GemvArgs a, ArArgs c) {
   // the pushes are complete (uncached mailboxes: acknowledged = visible) before this workgroup arrives
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (t == 0) s_last = __hip_atomic_fetch_add(c.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) {
+    const unsigned cls = blockIdx.x & 7, classes = min(gridDim.x, 8u);
+    const unsigned in_cls = (gridDim.x - cls + 7) / 8;  // workgroups of this class
+    unsigned* cc = c.arrive + cls * kArriveStride;
+    unsigned last = 0;
+    if (__hip_atomic_fetch_add(cc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_cls - 1) {
+      __hip_atomic_store(cc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm: the class is complete
+      unsigned* top = c.arrive + 8 * kArriveStride;
+      last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == classes - 1;
+      if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_last = last;
+  }
   __syncthreads();
-  if (s_last != gridDim.x - 1) return;
+  if (!s_last) return;
   // ---- the last arriver: every row of this rank is in every mailbox ----
-  if (t == 0) __hip_atomic_store(c.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   raise_flags(c.peers, c.rank, c.world, seq, t);
   wait_flags(c.peers, c.rank, c.world, seq, c.err, t);
   __syncthreads();

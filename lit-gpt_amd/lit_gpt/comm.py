@@ -70,7 +70,8 @@ class XgmiAllReduce:
                 ptrs.append(p.value)
         self.seq = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.arrive = torch.zeros(64, dtype=torch.int32, device=self.device)  # lga_q4_gemv_allreduce's counter
+        # lga_q4_gemv_allreduce's arrival counters (9 words at a 256-B stride)
+        self.arrive = torch.zeros(9 * 64, dtype=torch.int32, device=self.device)
         self._agree(failure, "mailbox mapping")
         self._mailboxes = (ctypes.c_void_p * self.world)(*ptrs)
         self._self_test()
