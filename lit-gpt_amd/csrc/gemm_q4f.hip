@@ -40,6 +40,19 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int BK = 64, NT = 512;
+
+#ifdef LGA_Q4F_TRACE  // lab builds only (tools/gemm_trace.py): per-workgroup phase timestamps, 100 MHz clock
+__device__ unsigned long long g_q4f_trace[8192 * 4];
+#define LGA_QTRACE(i)                                                                                  \
+  do {                                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < 8192)                                                         \
+      g_q4f_trace[(size_t)blockIdx.x * 4 + (i)] = __builtin_amdgcn_s_memrealtime();                    \
+  } while (0)
+#else
+#define LGA_QTRACE(i) \
+  do {                \
+  } while (0)
+#endif
 constexpr int MAX_SPLITS = 8;  // K-slices per tile (split-K for short prompts)
 
 template <int BM_, int BN_>
@@ -146,6 +159,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
   static_assert(!DUAL || FJ % 2 == 0, "SwiGLU needs fc_1 and fc_2 fragments in pairs");
   __shared__ __attribute__((aligned(1024))) unsigned char lds[T::LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63;
+  LGA_QTRACE(0);
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (scalar branches on it)
   const int wm = wave % T::WM, wn = wave / T::WM;
   const int split = blockIdx.x % a.splits;
@@ -396,6 +410,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
       dequant(0);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
+      LGA_QTRACE(1);
       // iteration lk: the dequant reads of raw(lk+1) and sub 0's 8 fragment reads; group lk+D {A(lk+D),
       // raw(lk+D+1)} issued under their latency (it fills buffers read one step earlier); sub 0's 16 MFMAs with
       // sub 1's 8 reads two per 4 MFMAs; raw(lk+1) dequantized between them and sub 1's MFMAs; WB(lk+1) stored;
@@ -437,6 +452,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
     }
   }
 
+  LGA_QTRACE(2);
   // ---- split-K: slabs, then the tile's last slice sums them in slice order ----
   if (a.splits > 1) {
     constexpr int NJ = FJ;
@@ -547,6 +563,10 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
       }
     }
   }
+#ifdef LGA_Q4F_TRACE
+  if (tid == 0) __builtin_amdgcn_s_waitcnt(0);  // thread 0's epilogue stores retired
+#endif
+  LGA_QTRACE(3);
 }
 
 }  // namespace pf
@@ -638,6 +658,17 @@ int lga::preload_gemm_q4f() {
 #undef LGA_PRE
   return bad;
 }
+
+#ifdef LGA_Q4F_TRACE
+extern "C" int lga_q4f_trace_read(unsigned long long* host, int n) {
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(lga::pf::g_q4f_trace), (size_t)n * sizeof(unsigned long long));
+  void* dptr = nullptr;
+  if (e == hipSuccess) e = hipGetSymbolAddress(&dptr, HIP_SYMBOL(lga::pf::g_q4f_trace));
+  if (e == hipSuccess) e = hipMemset(dptr, 0, sizeof(lga::pf::g_q4f_trace));
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  return (int)e;
+}
+#endif
 
 extern "C" int lga_q4f_fits(int M, int N, int K, int group, int fmt) { return q4f_fits(M, N, K, group, fmt) ? 1 : 0; }
 
