@@ -10,7 +10,9 @@
 //
 // MI355X design (CDNA4 playbook §5, "Pipelining across barriers"):
 //  * 8 waves per workgroup, 64 rows per wave; tiles <BM, BN> = <256, 128> for long prompts (4 (M) x 2 (N) waves,
-//    64 x 64 per wave = 4 x 4 `v_mfma_f32_16x16x32_bf16`) and <64, 128> / <64, 256> for short ones (1 x 8 waves);
+//    64 x 64 per wave = 4 x 4 `v_mfma_f32_16x16x32_bf16`), <256, 256> (64 x 128 per wave, one K-step of prefetch
+//    to fit LDS) where its rounds fill the CUs better (fc_1 || fc_2 at 2048 tokens: 11 % faster), and <64, 128> /
+//    <64, 256> for short ones (1 x 8 waves);
 //    the weight rows are the A operand, so a lane's accumulators are 4 consecutive output columns of one row
 //    (8-byte stores).
 //  * X tiles and the packed weight / scale tiles reach LDS by LDS-DMA (`global_load_lds_dwordx4`, source-swizzled so
@@ -68,7 +70,7 @@ struct Tile {
   // prefetch depth: X (and bf16 weight) tiles D K-steps ahead, packed weights D + 1 ahead. The 64-row tiles of
   // short prompts do little MFMA work per K-step, so they hide the DMA latency with depth instead (D = 4; the
   // 64 x 256 SwiGLU tile has no LDS for it)
-  static constexpr int D = BM == 64 && BN == 128 ? 4 : 2;
+  static constexpr int D = BM == 64 && BN == 128 ? 4 : (BM == 256 && BN == 256 ? 1 : 2);
   static constexpr int NA = D + 1, NRAW = D + 2, NWB = 2;
   // LDS, 4-bit weights: A[NA] | RAW[NRAW] | SC[NRAW] | WB[2] | misc ; bf16 weights: A[NA] | B[NA] | misc
   static constexpr int OFF_RAW = NA * A_BYTES;
@@ -100,6 +102,7 @@ struct Args {
   int splits;                // K-slices per tile (1: no split)
   unsigned* counters;        // split-K: one per tile, zero between launches (the last arriver re-zeroes it)
   float* slabs;              // split-K: [splits][M][N] fp32 partial products
+  int ldy = 0;               // row stride of y / residual (0: N) — a launch over a column range of a wider output
   int cb = 0;                // codebook row of kCode4 (FMT 1): 0 nf4, 1 fp4
 };
 
@@ -512,6 +515,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
   }
 
   // ---- epilogue: lane holds columns (fk * 4 + r) of weight fragment j for X row fr of fragment i ----
+  const size_t ldy = a.ldy ? a.ldy : a.N;
   if (DUAL) {
 #pragma unroll
     for (int j = 0; j < FJ / 2; ++j) {
@@ -532,7 +536,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
           }
           o[r / 2] = pack2(g[0], g[1]);
         }
-        *(uint2*)(a.y + (size_t)m * a.N + n) = make_uint2(o[0], o[1]);
+        *(uint2*)(a.y + (size_t)m * ldy + n) = make_uint2(o[0], o[1]);
       }
     }
   } else {
@@ -553,13 +557,13 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[j][i][r] + b[r];
         if (a.residual) {  // bf16(bf16(x W^T + b) + residual): Block's `x + attn(...)` after the Linear's rounding
-          const uint2 rv = *(const uint2*)(a.residual + (size_t)m * a.N + n);
+          const uint2 rv = *(const uint2*)(a.residual + (size_t)m * ldy + n);
           v[0] = round_bf(v[0]) + bflo(rv.x);
           v[1] = round_bf(v[1]) + bfhi(rv.x);
           v[2] = round_bf(v[2]) + bflo(rv.y);
           v[3] = round_bf(v[3]) + bfhi(rv.y);
         }
-        *(uint2*)(a.y + (size_t)m * a.N + n) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        *(uint2*)(a.y + (size_t)m * ldy + n) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
     }
   }
@@ -590,6 +594,16 @@ Plan q4f_plan(int M, int N, int K, bool dual) {
   Plan p;
   p.bm = M <= 128 ? 64 : 256;
   p.bn = p.bm == 64 ? (dual ? 256 : 128) : 128;
+  if (p.bm == 256) {
+    // 256 x 256 tiles (64 x 128 outputs per wave: a third less LDS fragment traffic per FLOP) where their rounds
+    // fill the CUs: a 256 x 256 tile-round costs ~1.74 256 x 128 tile-rounds (tools/gemm_rates.py: qkv 261 us in
+    // 1.5 big rounds vs 237 in 3 small; fc_1 || fc_2 368 in 2.7 big vs 413 in 5.4 small)
+    const int mt = (M + 255) / 256;
+    const long small = (long)mt * ((N + (dual ? 63 : 127)) / (dual ? 64 : 128));
+    const long big = (long)mt * ((N + (dual ? 127 : 255)) / (dual ? 128 : 256));
+    if ((big + 255) / 256 * 174 < (small + 255) / 256 * 100) p.bn = 256;
+    if (const char* e = getenv("LGA_Q4F_BN")) p.bn = atoi(e) == 256 ? 256 : 128;
+  }
   p.mt = (M + p.bm - 1) / p.bm;
   p.tn = dual ? p.bn / 2 : p.bn;
   p.tiles = p.mt * ((N + p.tn - 1) / p.tn);
@@ -613,6 +627,7 @@ int launch_tile(Args a, const Plan& p, hipStream_t stream) {
 
 template <int FMT, bool DUAL>
 int launch_q4f(Args a, const Plan& p, hipStream_t stream) {
+  if (p.bm == 256 && p.bn == 256) return launch_tile<FMT, DUAL, 256, 256>(a, p, stream);
   if (p.bm == 256) return launch_tile<FMT, DUAL, 256, 128>(a, p, stream);
   if (DUAL || p.bn == 256) return launch_tile<FMT, DUAL, 64, 256>(a, p, stream);
   return launch_tile<FMT, false, 64, 128>(a, p, stream);
@@ -623,7 +638,51 @@ size_t ws_need(const Plan& p, int M, int N, bool dual) {
   return 4096 + (size_t)p.splits * (dual ? 2 : 1) * M * N * 4;
 }
 
+// Long prompts, one weight matrix: the first columns as whole rounds of 256 x 256 tiles, the rest as 256 x 128 —
+// two launches over column ranges of the same output (Llama-2-7B qkv at 2048 tokens: one big round over 8192 columns
+// + one small round over 4096, instead of three small rounds). Returns the big-tile column count (0: no split).
+int q4f_big_columns(int M, int N, int K) {
+  if (M <= 128 || getenv("LGA_Q4F_BN")) return 0;
+  const int mt = (M + 255) / 256;
+  if (256 % mt || K / lga::pf::BK < 8) return 0;
+  const int cols_per_round = 256 / mt * 256;
+  auto rounds = [](long tiles) { return (tiles + 255) / 256; };
+  const long small_only = rounds((long)mt * ((N + 127) / 128)) * 100;
+  long best = small_only;
+  int best_cols = 0;
+  for (int rb = 1; (long)rb * cols_per_round < N; ++rb) {
+    const long cost = rb * 174L + rounds((long)mt * ((N - rb * cols_per_round + 127) / 128)) * 100;
+    if (cost < best) {
+      best = cost;
+      best_cols = rb * cols_per_round;
+    }
+  }
+  return best_cols;
+}
+
+int run_tiles(Args a, int fmt, bool dual, int bn, hipStream_t stream);
+
 int run(Args a, int fmt, bool dual, void* ws, size_t ws_bytes, hipStream_t stream) {
+  if (!dual) {
+    const int nb = q4f_big_columns(a.M, a.N, a.K);
+    if (nb > 0) {
+      const int kf = lga::kernel_fmt(fmt);
+      const size_t row_bytes = kf == 2 ? (size_t)a.K * 2 : (size_t)a.K / 2;
+      const size_t sc_bytes = kf == 2 ? 0 : (size_t)(a.K / a.G) * (kf == 0 ? 2 : 4);
+      Args b = a, c = a;
+      b.N = nb;
+      b.ldy = a.N;
+      c.N = a.N - nb;
+      c.ldy = a.N;
+      c.w = (const unsigned char*)a.w + (size_t)nb * row_bytes;
+      if (sc_bytes) c.sc = (const unsigned char*)a.sc + (size_t)nb * sc_bytes;
+      if (a.bias) c.bias = a.bias + nb;
+      if (a.residual) c.residual = a.residual + nb;
+      c.y = a.y + nb;
+      const int rc = run_tiles(b, fmt, false, 256, stream);
+      return rc ? rc : run_tiles(c, fmt, false, 128, stream);
+    }
+  }
   const Plan p = q4f_plan(a.M, a.N, a.K, dual);
   if (p.splits > 1) {
     LGA_CHECK_ARG(ws && ws_bytes >= ws_need(p, a.M, a.N, dual) && p.tiles <= 1024,
@@ -641,13 +700,33 @@ int run(Args a, int fmt, bool dual, void* ws, size_t ws_bytes, hipStream_t strea
     default: return launch_q4f<2, true>(a, p, stream);
   }
 }
+// one launch over the tiles of a (sub-)problem with a fixed tile width, no split-K (long prompts only)
+int run_tiles(Args a, int fmt, bool dual, int bn, hipStream_t stream) {
+  Plan p;
+  p.bm = 256;
+  p.bn = bn;
+  p.mt = (a.M + 255) / 256;
+  p.tn = dual ? bn / 2 : bn;
+  p.tiles = p.mt * ((a.N + p.tn - 1) / p.tn);
+  p.splits = 1;
+  a.cb = lga::codebook_of(fmt);
+  switch (lga::kernel_fmt(fmt) * 2 + (dual ? 1 : 0)) {
+    case 0: return launch_q4f<0, false>(a, p, stream);
+    case 1: return launch_q4f<0, true>(a, p, stream);
+    case 2: return launch_q4f<1, false>(a, p, stream);
+    case 3: return launch_q4f<1, true>(a, p, stream);
+    case 4: return launch_q4f<2, false>(a, p, stream);
+    default: return launch_q4f<2, true>(a, p, stream);
+  }
+}
 }  // namespace
 
 int lga::preload_gemm_q4f() {
   using namespace lga::pf;
   int bad = 0;
 #define LGA_PRE(F, D)                                                                                         \
-  bad += lga::preload(gemm_q4f_kernel<F, D, 256, 128>) + lga::preload(gemm_q4f_kernel<F, D, 64, 256>) +  \
+  bad += lga::preload(gemm_q4f_kernel<F, D, 256, 128>) + lga::preload(gemm_q4f_kernel<F, D, 256, 256>) +  \
+         lga::preload(gemm_q4f_kernel<F, D, 64, 256>) +                                                  \
          lga::preload(gemm_q4f_kernel<F, false, 64, 128>)
   LGA_PRE(0, false);
   LGA_PRE(0, true);

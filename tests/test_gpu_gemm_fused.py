@@ -99,7 +99,7 @@ def test_fused_swiglu_matches_oracle(ops, fmt, group, M, N, K):
     assert np.max(err) <= 0.0, float(np.max(err))
 
 
-@pytest.mark.parametrize("M,N,K", [(2048, 4096, 4096), (2048, 4096, 11008), (257, 12288, 4096)])
+@pytest.mark.parametrize("M,N,K", [(2048, 4096, 4096), (2048, 4096, 11008), (257, 12288, 4096), (2048, 12288, 4096)])
 def test_fused_gemm_llama7b_shapes(ops, M, N, K):
     """Full-size layer shapes: vs the fp32 product of the bit-exact dequantized weight (lga_q4_dequantize)."""
     g = torch.Generator(device=DEV).manual_seed(M + N + K)
@@ -182,3 +182,50 @@ def test_fused_gemm_rejects_unsupported_shapes(ops):
     sc = torch.zeros(128, 3, dtype=torch.bfloat16, device=DEV)
     with pytest.raises(RuntimeError, match="K % 64"):
         ops.q4_gemm_fused(x, qw, sc, 128, 96, 32, 0)
+
+
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (3, 64)])
+@pytest.mark.parametrize("M,N,K", [(300, 392, 1024), (513, 520, 704)])
+def test_fused_gemm_256x256_tiles(ops, fmt, group, M, N, K, monkeypatch):
+    """The 256 x 256 tile (64 x 128 outputs per wave, one K-step of prefetch; the planner picks it where its rounds
+    fill the CUs better, e.g. fc_1 || fc_2 at 2048 tokens) forced on: plain with bias + residual, and SwiGLU."""
+    monkeypatch.setenv("LGA_Q4F_BN", "256")
+    w = _w(N, K, "bt")
+    qw, sc, wd = _quant(ops, w, fmt, group)
+    x = bf16_np(synth.normal((M, K), f"btx{M}x{K}", 5, 1.0))
+    res = bf16_np(synth.normal((M, N), "btres", 5, 1.0))
+    bias = bf16_np(synth.normal((N,), "btb", 5, 0.1))
+    y = ops.q4_gemm_fused(to_dev(x), qw, sc, N, K, group, fmt, bias=to_dev(bias),
+                          residual=to_dev(res)).float().cpu().numpy()
+    h = x.astype(np.float64) @ wd.astype(np.float64).T + bias
+    ref = bf16_np(h.astype(np.float32)) + res
+    assert np.max(np.abs(y - ref) - (np.abs(ref) + np.abs(h)) * 2 ** -7) <= 2e-3
+    w2 = _w(N, K, "bt2")
+    q2, s2, d2 = _quant(ops, w2, fmt, group)
+    g = ops.q4_gemm_swiglu(to_dev(x), qw, sc, q2, s2, N, K, group, fmt).float().cpu().numpy()
+    h1 = x.astype(np.float64) @ wd.astype(np.float64).T
+    h2 = x.astype(np.float64) @ d2.astype(np.float64).T
+    a = bf16_np(h1.astype(np.float32))
+    gref = bf16_np(bf16_np(_silu(a.astype(np.float64)).astype(np.float32)) * bf16_np(h2.astype(np.float32)))
+    assert np.max(np.abs(g - gref) - _swiglu_tol(a, bf16_np(h2.astype(np.float32)), gref)) <= 0.0
+
+
+@pytest.mark.parametrize("fmt", [0, 1, 3])
+def test_fused_gemm_column_split(ops, fmt):
+    """Long prompt, one wide matrix (the 7B qkv shape class): columns [0, 8192) run as a round of 256 x 256 tiles,
+    the rest as 256 x 128 tiles — two launches over column ranges of one output (row stride N, offset weights /
+    scales / bias / residual). Checked against the fp32 product of the bit-exact dequantized weight."""
+    M, N, K = 2048, 12288, 1024
+    group = 128 if fmt == 0 else 64
+    g = torch.Generator(device=DEV).manual_seed(fmt + 5)
+    w = torch.randn(N, K, generator=g, device=DEV) * 0.02
+    qw, sc = ops.quantize(w, fmt, group)
+    wd = ops.q4_dequantize(qw, sc, N, K, group, fmt)
+    x = torch.randn(M, K, generator=g, device=DEV).to(torch.bfloat16)
+    res = torch.randn(M, N, generator=g, device=DEV).to(torch.bfloat16)
+    bias = (torch.randn(N, generator=g, device=DEV) * 0.1).to(torch.bfloat16)
+    y = ops.q4_gemm_fused(x, qw, sc, N, K, group, fmt, bias=bias, residual=res).float()
+    h = x.float() @ wd.float().t() + bias.float()
+    ref = h.to(torch.bfloat16).float() + res.float()
+    err = (y - ref).abs() - (ref.abs() + h.abs()) * 2 ** -7
+    assert float(err.max()) <= 2e-3
