@@ -21,8 +21,9 @@
 //    per K-step after a COUNTED `s_waitcnt vmcnt`, so the DMAs stay in flight across the barrier (never
 //    `__syncthreads()`, whose vmcnt(0) would drain them); all LDS in one `__shared__` array; no other global loads
 //    inside the loop.
-//  * split-K for short prompts (few tiles): the K-slices of a tile write fp32 slabs, the last to arrive (agent
-//    release / acquire on a per-tile counter) sums them in slice order — deterministic — and runs the epilogue.
+//  * split-K for short prompts (few tiles): the K-slices of a tile write fp32 slabs write-through, the last to
+//    arrive on a per-tile counter reads them past the L2 and sums them in slice order — deterministic — and runs
+//    the epilogue (no agent fences).
 //  * dequantization, int4-g: one `v_cvt_f32_ubyteN` per nibble, fma(n, s, -8 s) (exact: (n - 8) s needs 12
 //    significant bits) and `v_cvt_pk_bf16_f32` (round to nearest even) — the reference's bf16((n - 8) * s).
 //    nf4: bf16(NF4[n] * absmax) (fp32 product, as bnb's kernel) from an LDS table.
@@ -107,6 +108,17 @@ struct Args {
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
+
+// split-K slab traffic at agent coherence: 16-B buffer stores / loads with the sc1 cache-policy bit (write-through,
+// past the L2: the form a relaxed agent-scope atomic takes), compiler-visible intrinsics so the vmcnt accounting
+// stays exact; no fences are needed around them. Offsets are bytes from the slab base.
+constexpr int kSc1 = 16;  // gfx940+ cache-policy aux bit SC1
+__device__ __forceinline__ void st_wt16(__amdgpu_buffer_rsrc_t r, unsigned off, f32x4_t v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), r, off, 0, kSc1);
+}
+__device__ __forceinline__ f32x4_t ld_wt16(__amdgpu_buffer_rsrc_t r, unsigned off) {
+  return __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSc1));
+}
 
 // LDS byte address of a __shared__ pointer (the low 32 bits of its generic address)
 __device__ __forceinline__ unsigned lds_addr(const void* p) { return (unsigned)(uintptr_t)p; }
@@ -459,32 +471,30 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
   // ---- split-K: slabs, then the tile's last slice sums them in slice order ----
   if (a.splits > 1) {
     constexpr int NJ = FJ;
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        a.slabs, (short)0, (int)((size_t)a.splits * (DUAL ? 2 : 1) * a.M * a.N * 4), 0x00020000);
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       // column in the slab's [N] (SwiGLU: fc_1 and fc_2 partials side by side, [2][M][N])
       const int jj = DUAL ? j % (FJ / 2) : j;
       const int n = n0 + (DUAL ? wn * (WC / 2) : wn * WC) + jj * 16 + fk * 4;
       if (n >= a.N) continue;
-      float* slab = a.slabs + ((size_t)split * (DUAL ? 2 : 1) + (DUAL ? j / (FJ / 2) : 0)) * a.M * a.N;
+      const size_t slab = ((size_t)split * (DUAL ? 2 : 1) + (DUAL ? j / (FJ / 2) : 0)) * a.M * a.N;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * 64 + i * 16 + fr;
-        if (m < a.M) *(f32x4_t*)(slab + (size_t)m * a.N + n) = acc[j][i];
+        if (m < a.M) st_wt16(srs, (unsigned)((slab + (size_t)m * a.N + n) * 4), acc[j][i]);
       }
     }
+    // the slabs went out write-through (sc1): drained, they are visible to the tile's last slice, which reads them
+    // with sc1 loads — no agent release / acquire fences (an L2 write-back per slice and an invalidate per tile)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     unsigned* last = (unsigned*)(lds + OFF_MISC + 64);
     if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       const unsigned old = __hip_atomic_fetch_add(a.counters + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const bool is_last = old == (unsigned)a.splits - 1;
-      if (is_last) {
-        a.counters[tile] = 0u;  // ready for the next launch (stream-ordered after this one)
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (is_last) __hip_atomic_store(a.counters + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
       *last = is_last ? 1u : 0u;
     }
     __syncthreads();
@@ -503,8 +513,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
 #pragma unroll
         for (int s2 = 0; s2 < MAX_SPLITS; ++s2) {
           const int sc = min(s2, a.splits - 1);
-          const float* slab = a.slabs + ((size_t)sc * (DUAL ? 2 : 1) + mat) * a.M * a.N;
-          v[s2] = *(const f32x4_t*)(slab + (size_t)m * a.N + n);
+          const size_t slab = ((size_t)sc * (DUAL ? 2 : 1) + mat) * a.M * a.N;
+          v[s2] = ld_wt16(srs, (unsigned)((slab + (size_t)m * a.N + n) * 4));
         }
         f32x4_t t = v[0];
 #pragma unroll
