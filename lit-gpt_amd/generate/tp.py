@@ -112,9 +112,17 @@ def init_distributed(allreduce: Optional[str] = None) -> Fabric:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for a one-GPU box (never set in production): every rank on cuda:0, gloo for the host-side
+    # collectives (RCCL refuses two ranks on one device); the decode all-reduces stay on the xGMI kernel
+    if os.environ.get("LGA_ONE_DEVICE") == "1":
+        local = 0
+    backend = os.environ.get("LGA_DIST_BACKEND", "nccl")
     torch.cuda.set_device(local)
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     mode = allreduce or os.environ.get("LGA_TP_ALLREDUCE", "xgmi")
     if mode not in ("xgmi", "rccl"):
         raise ValueError(f"allreduce must be 'xgmi' or 'rccl', got {mode!r}")
