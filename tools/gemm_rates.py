@@ -15,7 +15,7 @@ sys.path[:0] = [str(REPO / "lit-gpt_amd"), str(REPO)]
 from lit_gpt import ops  # noqa: E402
 
 M = int(sys.argv[1]) if len(sys.argv) > 1 else 2048
-if len(sys.argv) > 2:  # an alternative build of the library (lab A/B)
+if len(sys.argv) > 2 and sys.argv[2]:  # an alternative build of the library (lab A/B)
     ops._lib = ops.load_library(Path(sys.argv[2]))
 ONLY = sys.argv[3].split(",") if len(sys.argv) > 3 else None
 dev = torch.device("cuda")
