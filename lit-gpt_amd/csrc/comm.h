@@ -18,15 +18,28 @@ __device__ __forceinline__ uint16_t* slot_ptr(unsigned char* mb, int slot, int s
   return (uint16_t*)(mb + kFlagBytes) + ((size_t)slot * kMaxRanks + src) * cap;
 }
 
+// The flag protocol follows the memory model (LGA_COMM_FORMAL=1, default): a system-scope release before each flag,
+// an acquire after the wait. Mailboxes are UNCACHED device memory (lga_comm_alloc: hipDeviceMallocUncached), so
+// LGA_COMM_FORMAL=0 builds the form that relies on that instead (drains + barriers, no cache maintenance); on one
+// GPU shared by the ranks the two measured the same per call (tools/tp_fused_time.py), across GPUs it is unmeasured.
+#ifndef LGA_COMM_FORMAL
+#define LGA_COMM_FORMAL 1
+#endif
+
 // Raise this rank's flag for call `seq` in every peer's mailbox (threads t < world), after the calling workgroup's
 // data stores are complete: each storing wave drained (asm vmcnt(0)) and the workgroup barrier ordered them before
-// the flag writers, which publish with a system-scope RELEASE store behind an explicit drain.
+// the flag writers, which drain again and store the flag (system scope).
 __device__ __forceinline__ void raise_flags(const Peers& peers, int rank, int world, unsigned seq, int t) {
   if (t < world && t != rank) {
     unsigned* f = (unsigned*)peers.mb[t] + rank * kFlagStride;
+#if LGA_COMM_FORMAL
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(f, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+#else
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(f, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
   }
 }
 
@@ -48,7 +61,11 @@ __device__ __forceinline__ void wait_flags(const Peers& peers, int rank, int wor
         break;
       }
     }
+#if LGA_COMM_FORMAL
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+#else
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // compiler ordering; the mailbox reads go to memory
+#endif
   }
 }
 
