@@ -310,7 +310,7 @@ typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 // exp(m_old - m_new) is a per-lane scalar, skipped when no row max of the wave moved. Causal masking only on the
 // tiles that cross a row's position (a 32-bit compare + select per element, on those tiles only); the scores stay
 // raw — the max runs on them and one fma(s, scale log2 e, -m) per element feeds v_exp_f32 (max(s) c == max(s c) for
-// c > 0). K / V tiles are staged by buffer loads (a per-thread 32-bit offset plus a scalar per tile; rows past the
+// c > 0). K / V tiles are staged by buffer loads (the whole row offset in the per-thread voffset; rows past the
 // cache read as zeros by the range check) and every LDS address is a per-lane base plus a compile-time offset (the
 // tile loop is unrolled by the two buffers). Grid: 1-D, `order` 1 pairs the two workgroups a CU holds — the first
 // half walks query blocks nblk-1 .. nblk/2, the second half blocks 0 .. nblk/2-1, so workgroups i and i + half sum
@@ -397,12 +397,15 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(const uint16_t* __
   int soff[LPT];
 #pragma unroll
   for (int i = 0; i < LPT; ++i) soff[i] = kv_off<HS>(tid / CH + RPI * i, tid % CH);
+  // the whole byte offset rides in voffset: the buffer range check covers voffset only (soffset is added after
+  // it), so rows past max_seq — the last partial tile and the one-tile-ahead prefetch — read as zeros instead of
+  // past the group's cache
   auto gload = [&](int k0) {
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
-      const int so = (k0 + RPI * i) * HS * 2;
-      kr[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, gvoff, so, 0);
-      vr[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, gvoff, so, 0);
+      const int off = gvoff + (k0 + RPI * i) * HS * 2;
+      kr[i] = __builtin_amdgcn_raw_buffer_load_b128(krs, off, 0, 0);
+      vr[i] = __builtin_amdgcn_raw_buffer_load_b128(vrs, off, 0, 0);
     }
   };
   auto lstore = [&](int buf) {

@@ -58,12 +58,26 @@ __global__ void __launch_bounds__(256) gemv_q4_ar_kernel(GemvArgs a, ArArgs c) {
     const unsigned in_cls = (gridDim.x - cls + 7) / 8;  // workgroups of this class
     unsigned* cc = c.arrive + cls * kArriveStride;
     unsigned last = 0;
-    if (__hip_atomic_fetch_add(cc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_cls - 1) {
+#if LGA_COMM_FORMAL
+    // memory-model form: every workgroup's arrival is a system-scope release of its pushes (fence, then an asm
+    // drain the compiler cannot drop behind a provably empty scoreboard: MI355X_MICROARCH.md "Compiler hazard"),
+    // the counters' RMW chain carries them to the last arriver, whose system-scope acquire precedes its flag
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    if (__hip_atomic_fetch_add(cc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == in_cls - 1) {
       __hip_atomic_store(cc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm: the class is complete
       unsigned* top = c.arrive + 8 * kArriveStride;
-      last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == classes - 1;
+#if LGA_COMM_FORMAL
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "");  // what the class's arrivals released, released on
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == classes - 1;
       if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+#if LGA_COMM_FORMAL
+    if (last) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // every workgroup's pushes happen-before the flags
+#endif
     s_last = last;
   }
   __syncthreads();

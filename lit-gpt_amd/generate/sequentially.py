@@ -34,7 +34,7 @@ if str(wd) not in sys.path:
 
 import generate.base as generate_base  # noqa: E402
 from lit_gpt import GPT, Config  # noqa: E402
-from lit_gpt.model import Block, KVCache, build_mask_cache  # noqa: E402
+from lit_gpt.model import Block, CausalMask, KVCache  # noqa: E402
 
 
 @torch.inference_mode()
@@ -66,7 +66,7 @@ def sequential(model: GPT, root: torch.device, max_seq_length: int, devices: int
     # reference rebuilds them under ``with root:`` only, outside fabric.init_tensor, so positions stay fp32
     model.max_seq_length = max_seq_length
     model.cos, model.sin = model.rope_cache(device=root)
-    model.mask_cache = build_mask_cache(max_seq_length, root)
+    model.mask_cache = CausalMask(max_seq_length, root)  # reference sequentially.py:58 builds the tensor; no kernel reads it
     for name, sub in model.named_modules():
         if isinstance(sub, Block) or any(name.startswith(p + ".") for p in mapping):
             continue

@@ -218,7 +218,7 @@ class GPT(nn.Module):
             block.attn.kv_cache = block.attn.build_kv_cache(batch_size, self.max_seq_length, rope_cache_length,
                                                             device, dtype)
         if self.mask_cache is None or self.mask_cache.size(3) != self.max_seq_length:
-            self.mask_cache = build_mask_cache(self.max_seq_length, device or self.transformer.wte.weight.device)
+            self.mask_cache = CausalMask(self.max_seq_length, device or self.transformer.wte.weight.device)
 
     def clear_kv_cache(self) -> None:
         self.mask_cache = None
@@ -582,3 +582,33 @@ def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.T
 def build_mask_cache(max_seq_length: int, device: Optional[torch.device] = None) -> torch.Tensor:
     ones = torch.ones((max_seq_length, max_seq_length), device=device, dtype=torch.bool)
     return torch.tril(ones).unsqueeze(0).unsqueeze(0)
+
+
+class CausalMask:
+    """``GPT.mask_cache`` without the (1, 1, S, S) bool tensor (reference model.py:551-554,802-804 build it in
+    ``set_kv_cache``): no kernel reads it — attention derives the mask row from ``input_pos`` — and at Mixtral's
+    S = 32768 it would hold 1 GiB of HBM per rank. It keeps the reference's shape for ``size()`` / ``shape`` and
+    materialises the tril tensor only if a caller indexes it (``mask_cache.index_select(2, input_pos)`` style)."""
+
+    def __init__(self, max_seq_length: int, device: Optional[torch.device] = None) -> None:
+        self.max_seq_length = max_seq_length
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self._t: Optional[torch.Tensor] = None
+
+    @property
+    def shape(self) -> torch.Size:
+        return torch.Size((1, 1, self.max_seq_length, self.max_seq_length))
+
+    def size(self, dim: Optional[int] = None):
+        return self.shape if dim is None else self.shape[dim]
+
+    def tensor(self) -> torch.Tensor:
+        if self._t is None:
+            self._t = build_mask_cache(self.max_seq_length, self.device)
+        return self._t
+
+    def __getitem__(self, item):
+        return self.tensor()[item]
+
+    def index_select(self, dim: int, index: torch.Tensor) -> torch.Tensor:
+        return self.tensor().index_select(dim, index)

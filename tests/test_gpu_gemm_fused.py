@@ -229,3 +229,40 @@ def test_fused_gemm_column_split(ops, fmt):
     ref = h.to(torch.bfloat16).float() + res.float()
     err = (y - ref).abs() - (ref.abs() + h.abs()) * 2 ** -7
     assert float(err.max()) <= 2e-3
+
+
+@pytest.mark.parametrize("M,bn", [(1, None), (64, None), (128, None), (200, "128"), (200, "256")])
+@pytest.mark.parametrize("splits", [2, 4, 8])
+def test_fused_gemm_split_k_handoff_stress(ops, M, bn, splits, monkeypatch):
+    """The split-K hand-off (csrc/gemm_q4f.hip: write-through sc1 slab stores, drain, barrier, a relaxed agent
+    counter; the last slice reads the slabs with sc1 loads, no fences) across all four tile shapes (64 x 128,
+    64 x 256, 256 x 128, 256 x 256) and 2 / 4 / 8 slices over many tiles: A, then B, then A again on the same slab
+    workspace — a slab read that saw the previous call's partials would make the two A results differ or leave
+    the fp32 product's rounding bound. Both the plain and the SwiGLU form."""
+    N, K = 4096, 4096
+    monkeypatch.setenv("LGA_Q4F_SPLITS", str(splits))
+    if bn is not None:
+        monkeypatch.setenv("LGA_Q4F_BN", bn)
+    g = torch.Generator(device=DEV).manual_seed(M * 31 + splits)
+    w = torch.randn(N, K, generator=g, device=DEV) * 0.02
+    w2 = torch.randn(N, K, generator=g, device=DEV) * 0.02
+    qw, sc = ops.quantize(w, 0, 128)
+    q2, s2 = ops.quantize(w2, 0, 128)
+    xa = torch.randn(M, K, generator=g, device=DEV).to(torch.bfloat16)
+    xb = torch.randn(M, K, generator=g, device=DEV).to(torch.bfloat16) * 3
+    ya = ops.q4_gemm_fused(xa, qw, sc, N, K, 128, 0)
+    yb = ops.q4_gemm_fused(xb, qw, sc, N, K, 128, 0)
+    ya2 = ops.q4_gemm_fused(xa, qw, sc, N, K, 128, 0)
+    assert torch.equal(ya, ya2)
+    wd = ops.q4_dequantize(qw, sc, N, K, 128, 0).float()
+    for x, y in ((xa, ya), (xb, yb)):
+        h = x.float() @ wd.t()
+        assert float(((y.float() - h).abs() - h.abs() * 2 ** -7).max()) <= 2e-3
+    ga = ops.q4_gemm_swiglu(xa, qw, sc, q2, s2, N, K, 128, 0)
+    ops.q4_gemm_swiglu(xb, qw, sc, q2, s2, N, K, 128, 0)
+    ga2 = ops.q4_gemm_swiglu(xa, qw, sc, q2, s2, N, K, 128, 0)
+    assert torch.equal(ga, ga2)
+    h1 = (xa.float() @ wd.t()).to(torch.bfloat16)
+    h2 = (xa.float() @ ops.q4_dequantize(q2, s2, N, K, 128, 0).float().t()).to(torch.bfloat16)
+    ref = ops.swiglu(h1.contiguous(), h2.contiguous()).float()
+    assert float((ga.float() - ref).abs().sub(_swiglu_tol(h1.float(), h2.float(), ref)).max()) <= 0.0

@@ -381,6 +381,41 @@ def test_prefill_flash_attention_matches_reference(ops, H, G, hs, T, start):
     assert np.max(err) <= 5e-3, float(np.max(err))
 
 
+@pytest.mark.parametrize("S,T,start", [(100, 100, 0), (150, 40, 110), (77, 77, 0), (200, 16, 184)])
+def test_prefill_flash_attention_partial_last_tile_stays_in_cache(ops, S, T, start):
+    """max_seq % 64 != 0 and the prompt ends in the last partial key tile, with the K / V caches views at the start
+    of a larger NaN-filled allocation: the tile loads past max_seq (and the one-tile-ahead prefetch) must read
+    zeros through the buffer range check, never the bytes after the last group's cache (a NaN there times P = 0
+    poisons the output). Finite and equal to the fp64 reference."""
+    H, G, hs = 8, 2, 128
+    q = bf16_np(synth.normal((T, H, hs), "tq", 11, 1.0))
+    k = bf16_np(synth.normal((G, S, hs), "tk", 11, 1.0))
+    v = bf16_np(synth.normal((G, S, hs), "tv", 11, 1.0))
+    n = G * S * hs
+    bufs = []
+    for a in (k, v):  # NaN rows right after the last group's cache
+        b = torch.full((n + 256 * hs,), float("nan"), dtype=torch.bfloat16, device=DEV)
+        view = b[:n].view(G, S, hs)
+        view.copy_(to_dev_bf16(a))
+        bufs.append((b, view))
+    positions = list(range(start, start + T))
+    pos = torch.tensor(positions, dtype=torch.int64)
+    scale = 1.0 / math.sqrt(hs)
+    y = ops.attention(to_dev_bf16(q), bufs[0][1], bufs[1][1], pos.to(DEV), H, G, hs, scale,
+                      n_splits=1).float().cpu().numpy().reshape(T, H, hs)
+    assert np.all(np.isfinite(y))
+    qpk = H // G
+    ref = np.zeros((T, H, hs))
+    for t, p in enumerate(positions):
+        for h in range(H):
+            kk, vv = k[h // qpk, : p + 1].astype(np.float64), v[h // qpk, : p + 1].astype(np.float64)
+            s = kk @ q[t, h].astype(np.float64) * scale
+            e = np.exp(s - s.max())
+            ref[t, h] = (e / e.sum()) @ vv
+    err = np.abs(y - ref) - np.abs(ref) * 2 ** -6
+    assert np.max(err) <= 5e-3, float(np.max(err))
+
+
 @pytest.mark.parametrize("H,G", [(32, 32), (64, 8), (8, 1), (16, 8)])
 @pytest.mark.parametrize("p", [0, 1, 37, 2047, 2303])
 @pytest.mark.parametrize("splits", [1, 7, 36])
