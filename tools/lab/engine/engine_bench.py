@@ -8,7 +8,8 @@ import torch
 from generate.base import build_model
 from lit_gpt import Config, ops
 from lit_gpt.runtime import DecodeGraph
-from engine import DecodeEngine
+import importlib, os
+DecodeEngine = importlib.import_module(os.environ.get("LGA_ENGINE_MOD", "engine2")).DecodeEngine
 
 dev = torch.device("cuda", 0)
 T, STEPS = 2048, 64

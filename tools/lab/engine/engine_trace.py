@@ -42,6 +42,9 @@ with torch.inference_mode():
             pos.fill_(T)
     eng.check()
 tr = buf.reshape(NCU, TR_OPS, TR_EV).astype(np.int64)
+out = Path(os.environ.get("GRAFT_REPO_ROOT", REPO)) / "gpurun_out" / "engine_trace.npy"
+out.parent.mkdir(exist_ok=True)
+np.save(out, tr)
 nops = L * 5 + 1
 t0 = tr[:, 0, 0][tr[:, 0, 0] > 0].min()
 rel = lambda v: (v - t0) / 100.0  # us
@@ -55,3 +58,19 @@ for k in list(range(min(nops, 12))) + [nops - 6, nops - 5, nops - 4, nops - 3, n
     print(f"{k:3d} {name:6s} {med(0):9.1f} {med(1):8.1f} {med(2):9.1f} {med(3):10.1f} {mx(4):10.1f} | "
           f"{np.median(e[:,1]-e[:,0])/100:5.2f} {np.median(e[:,2]-e[:,1])/100:5.2f} {np.median(e[:,3]-e[:,2])/100:6.2f} | "
           f"{med(5):8.1f} .. {med(6):8.1f}")
+
+# per-CU skew: which CUs finish each op's units last, and is it the same CUs every op
+print("\nper-op spread of unitsDone over CUs (us after the median) and the 8 latest CUs")
+late_count = np.zeros(NCU, dtype=int)
+for k in range(nops):
+    d = rel(tr[:, k, 3])
+    d = d - np.median(d)
+    order = np.argsort(d)[::-1]
+    late_count[order[:16]] += 1
+    if k < 15 or k >= nops - 6:
+        print(f"{k:3d} {(names[k % 5] if k < L * 5 else 'lm'):6s} p90 {np.percentile(d, 90):6.2f} p99 {np.percentile(d, 99):6.2f} "
+              f"max {d.max():6.2f} | late CUs {list(order[:8])}")
+top = np.argsort(late_count)[::-1][:24]
+print("CUs most often among the 16 latest (count over", nops, "ops):", [(int(c), int(late_count[c])) for c in top])
+print("by blockIdx % 8:", [int(late_count[np.arange(NCU) % 8 == x].sum()) for x in range(8)])
+print("attention split of the late CUs (c // G):", [int(c) // 32 for c in top])
