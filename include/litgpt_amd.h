@@ -171,6 +171,27 @@ int lga_q4_gemv_swiglu_experts(const void* x, const uint8_t* qweight1, const voi
  * (the `y[token_idx] += probs * expert(...)` loop, model.py:739-742, then Block's residual add model.py:592). */
 int lga_moe_combine(const void* expert_out, const void* probs, const int32_t* expert_ids, const void* residual,
                     void* y, int T, int k, int C, lga_stream_t stream);
+/* Grouped sparse-MoE prefill (T > 1): replaces the per-expert loop of LLaMAMoE.forward (model.py:740-742:
+ * torch.where(indices == e) per expert, then the expert MLP on the gathered rows). lga_moe_group sorts the T * k
+ * (token, slot) pairs by expert on the device (stable: (token, slot) order inside an expert) into a table of
+ * m-tiles of bm rows (bm 64 or 256): tiles = {n_tiles, (expert, first row, rows) x n_tiles}, capacity
+ * 1 + 3 * lga_moe_group_tiles(T * k, n_expert, bm) ints; x_rows[r] = token of permuted row r, y_rows[r] =
+ * token * k + slot. lga_q4_gemm_swiglu_grouped computes g[r] = bf16(silu(bf16(x[x_rows[r]] W1_e^T))) *
+ * bf16(x[x_rows[r]] W2_e^T) for every permuted row r in ONE launch (the experts' weights stacked with strides
+ * w_stride / s_stride bytes, as lga_q4_gemv_experts); lga_q4_gemm_grouped computes y[y_rows[r]] =
+ * x[x_rows ? x_rows[r] : r] W_e^T (y_rows NULL: row r). No host synchronisation: the launches are sized by the
+ * table's capacity and surplus tiles exit. */
+int lga_moe_group_tiles(int rows, int n_expert, int bm);
+int lga_moe_group(const int32_t* expert_ids, int T, int k, int n_expert, int bm, int32_t* tiles, int32_t* x_rows,
+                  int32_t* y_rows, lga_stream_t stream);
+int lga_q4_gemm_swiglu_grouped(const void* x, const void* qweight1, const void* scales1, const void* qweight2,
+                               const void* scales2, long long w_stride, long long s_stride, const int32_t* tiles,
+                               const int32_t* x_rows, void* y, int rows, int N, int K, int group, int fmt, int bm,
+                               int n_expert, lga_stream_t stream);
+int lga_q4_gemm_grouped(const void* x, const void* qweight, const void* scales, long long w_stride,
+                        long long s_stride, const int32_t* tiles, const int32_t* x_rows, const int32_t* y_rows,
+                        void* y, int rows, int N, int K, int group, int fmt, int bm, int n_expert,
+                        lga_stream_t stream);
 
 /* -- tensor-parallel all-reduce of decode activations (generate/tp.py:73-74 `all_reduce(outs, "sum", ranks)`,
  *    the forward hook after every attention / MLP, :53,57,70) over xGMI peer memory -----------------------------

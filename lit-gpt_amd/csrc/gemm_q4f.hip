@@ -105,6 +105,14 @@ struct Args {
   float* slabs;              // split-K: [splits][M][N] fp32 partial products
   int ldy = 0;               // row stride of y / residual (0: N) — a launch over a column range of a wider output
   int cb = 0;                // codebook row of kCode4 (FMT 1): 0 nf4, 1 fp4
+  // grouped (sparse-MoE prefill, lga_q4_gemm_grouped): m-tile i of the launch is entry i of the device table grp =
+  // {n_tiles, then (expert, first row, rows) per tile} built by lga_moe_group; its weights are expert e's
+  // (w / w2 + e * ew bytes, sc / sc2 + e * es bytes); its X rows are gathered through xrow (null: contiguous) and
+  // its Y rows scattered through yrow (null: contiguous). M bounds the row indices of the permuted list.
+  const int32_t* grp = nullptr;
+  const int32_t* xrow = nullptr;
+  const int32_t* yrow = nullptr;
+  long long ew = 0, es = 0;
 };
 
 __device__ __forceinline__ int swz(int row, int chunk) { return row * 128 + 16 * (chunk ^ (row & 7)); }
@@ -167,6 +175,17 @@ __device__ __forceinline__ void glds_rows8(const uint16_t* src, int ld, int row,
 // columns of each; the weight tile's rows [0, BN/2) are fc_1's, [BN/2, BN) fc_2's).
 template <int FMT, bool DUAL, int BM_, int BN_>
 __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
+  if (a.grp) {  // grouped: this m-tile's expert and row range (surplus tiles of the launch's upper bound exit here)
+    const int mi = (blockIdx.x / a.splits) % a.mt;
+    if (mi >= a.grp[0]) return;
+    const long long e = a.grp[1 + 3 * mi];
+    a.w = (const unsigned char*)a.w + e * a.ew;
+    if (a.sc) a.sc = (const unsigned char*)a.sc + e * a.es;
+    if (DUAL) {
+      a.w2 = (const unsigned char*)a.w2 + e * a.ew;
+      if (a.sc2) a.sc2 = (const unsigned char*)a.sc2 + e * a.es;
+    }
+  }
   using T = Tile<BM_, BN_>;
   constexpr int BM = T::BM, BN = T::BN, NA = T::NA, NRAW = T::NRAW, FJ = T::FJ, WC = T::WC;
   constexpr int A_BYTES = T::A_BYTES, B_BYTES = T::B_BYTES, RAW_BYTES = T::RAW_BYTES, SC_BYTES = T::SC_BYTES;
@@ -179,7 +198,9 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
   const int wm = wave % T::WM, wn = wave / T::WM;
   const int split = blockIdx.x % a.splits;
   const int tile = blockIdx.x / a.splits;
-  const int m0 = (tile % a.mt) * BM;
+  // rows [m0, mend) of the (permuted) row list
+  const int m0 = a.grp ? a.grp[2 + 3 * (tile % a.mt)] : (tile % a.mt) * BM;
+  const int mend = a.grp ? m0 + a.grp[3 + 3 * (tile % a.mt)] : a.M;
   constexpr int TN = DUAL ? BN / 2 : BN;  // output columns per tile
   const int n0 = (tile / a.mt) * TN;
   const int nk_all = a.K / BK;
@@ -220,7 +241,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
   for (int i = 0; i < T::APW; ++i) {
     const int r = (wave * T::APW + i) * 8 + (lane >> 3);
     const int lc = (lane & 7) ^ (r & 7);
-    xsrc[i] = (const unsigned char*)(a.x + (size_t)min(m0 + r, a.M - 1) * a.K + (size_t)kt0 * BK + lc * 8);
+    const int mr = min(m0 + r, mend - 1);
+    xsrc[i] = (const unsigned char*)(a.x + (size_t)(a.xrow ? a.xrow[mr] : mr) * a.K + (size_t)kt0 * BK + lc * 8);
   }
   auto issue_a = [&](int lk) {
     unsigned char* A = lds + (lk % NA) * A_BYTES;
@@ -534,7 +556,8 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * 64 + i * 16 + fr;
-        if (m >= a.M) continue;
+        if (m >= mend) continue;
+        const size_t my = a.yrow ? (size_t)a.yrow[m] : (size_t)m;
         uint32_t o[2];
 #pragma unroll
         for (int r = 0; r < 4; r += 2) {
@@ -546,7 +569,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
           }
           o[r / 2] = pack2(g[0], g[1]);
         }
-        *(uint2*)(a.y + (size_t)m * ldy + n) = make_uint2(o[0], o[1]);
+        *(uint2*)(a.y + my * ldy + n) = make_uint2(o[0], o[1]);
       }
     }
   } else {
@@ -562,18 +585,19 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = m0 + wm * 64 + i * 16 + fr;
-        if (m >= a.M) continue;
+        if (m >= mend) continue;
+        const size_t my = a.yrow ? (size_t)a.yrow[m] : (size_t)m;
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[j][i][r] + b[r];
         if (a.residual) {  // bf16(bf16(x W^T + b) + residual): Block's `x + attn(...)` after the Linear's rounding
-          const uint2 rv = *(const uint2*)(a.residual + (size_t)m * ldy + n);
+          const uint2 rv = *(const uint2*)(a.residual + my * ldy + n);
           v[0] = round_bf(v[0]) + bflo(rv.x);
           v[1] = round_bf(v[1]) + bfhi(rv.x);
           v[2] = round_bf(v[2]) + bflo(rv.y);
           v[3] = round_bf(v[3]) + bfhi(rv.y);
         }
-        *(uint2*)(a.y + (size_t)m * ldy + n) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
+        *(uint2*)(a.y + my * ldy + n) = make_uint2(pack2(v[0], v[1]), pack2(v[2], v[3]));
       }
     }
   }
@@ -793,4 +817,70 @@ extern "C" int lga_q4_gemm_swiglu(const void* x, const void* qw1, const void* sc
   Args a{(const uint16_t*)x, qw1, sc1, qw2, sc2, nullptr, nullptr, (uint16_t*)y, M, N, K, fmt == 2 ? 64 : group, 1,
          1, nullptr, nullptr};
   return run(a, fmt, true, workspace, workspace_bytes, stream);
+}
+
+// ---- grouped (sparse-MoE prefill): every active expert's rows in ONE launch ------------------------------------
+// Replaces the reference's per-expert loop of LLaMAMoE.forward for T > 1 (lit_gpt/model.py:740-742: for each expert,
+// torch.where(indices == e), then expert(x[token_idx]) — fc_1, fc_2, silu * mul, proj — on the gathered rows) by two
+// launches over a device-built tile table (lga_moe_group): no host synchronisation, no gathered or scattered copies.
+namespace {
+int run_grouped(Args a, int fmt, bool dual, int bm, int max_tiles, hipStream_t stream) {
+  Plan p;
+  p.bm = bm;
+  p.bn = bm == 64 && dual ? 256 : 128;
+  p.mt = max_tiles;
+  p.tn = dual ? p.bn / 2 : p.bn;
+  p.tiles = p.mt * ((a.N + p.tn - 1) / p.tn);
+  p.splits = 1;
+  a.cb = lga::codebook_of(fmt);
+  switch (lga::kernel_fmt(fmt) * 2 + (dual ? 1 : 0)) {
+    case 0: return launch_q4f<0, false>(a, p, stream);
+    case 1: return launch_q4f<0, true>(a, p, stream);
+    case 2: return launch_q4f<1, false>(a, p, stream);
+    case 3: return launch_q4f<1, true>(a, p, stream);
+    case 4: return launch_q4f<2, false>(a, p, stream);
+    default: return launch_q4f<2, true>(a, p, stream);
+  }
+}
+}  // namespace
+
+// upper bound on the m-tiles of `rows` permuted rows over n_expert groups (the tile table's capacity)
+extern "C" int lga_moe_group_tiles(int rows, int n_expert, int bm) {
+  return bm > 0 ? (rows + bm - 1) / bm + n_expert : 0;
+}
+
+extern "C" int lga_q4_gemm_grouped(const void* x, const void* weight, const void* scales, long long w_stride,
+                                   long long s_stride, const int32_t* tiles, const int32_t* x_rows,
+                                   const int32_t* y_rows, void* y, int rows, int N, int K, int group, int fmt, int bm,
+                                   int n_expert, hipStream_t stream) {
+  LGA_CHECK_ARG(x && weight && y && tiles && (fmt == 2 || scales), "lga_q4_gemm_grouped: null pointer");
+  LGA_CHECK_ARG(fmt >= 0 && fmt <= 3 && (bm == 64 || bm == 256) && n_expert > 0 && rows > 0,
+                "lga_q4_gemm_grouped: fmt 0-3, bm 64 or 256");
+  LGA_CHECK_ARG(q4f_fits(rows, N, K, group, fmt), "lga_q4_gemm_grouped: needs N % 8 == 0, K % 64 == 0, group >= 64");
+  Args a{(const uint16_t*)x, weight, scales, nullptr, nullptr, nullptr, nullptr, (uint16_t*)y, rows, N, K,
+         fmt == 2 ? 64 : group, 1, 1, nullptr, nullptr};
+  a.grp = tiles;
+  a.xrow = x_rows;
+  a.yrow = y_rows;
+  a.ew = w_stride;
+  a.es = s_stride;
+  return run_grouped(a, fmt, false, bm, lga_moe_group_tiles(rows, n_expert, bm), stream);
+}
+
+extern "C" int lga_q4_gemm_swiglu_grouped(const void* x, const void* qw1, const void* sc1, const void* qw2,
+                                          const void* sc2, long long w_stride, long long s_stride,
+                                          const int32_t* tiles, const int32_t* x_rows, void* y, int rows, int N,
+                                          int K, int group, int fmt, int bm, int n_expert, hipStream_t stream) {
+  LGA_CHECK_ARG(x && qw1 && qw2 && y && tiles && (fmt == 2 || (sc1 && sc2)), "lga_q4_gemm_swiglu_grouped: null pointer");
+  LGA_CHECK_ARG(fmt >= 0 && fmt <= 3 && (bm == 64 || bm == 256) && n_expert > 0 && rows > 0,
+                "lga_q4_gemm_swiglu_grouped: fmt 0-3, bm 64 or 256");
+  LGA_CHECK_ARG(q4f_fits(rows, N, K, group, fmt),
+                "lga_q4_gemm_swiglu_grouped: needs N % 8 == 0, K % 64 == 0, group >= 64");
+  Args a{(const uint16_t*)x, qw1, sc1, qw2, sc2, nullptr, nullptr, (uint16_t*)y, rows, N, K, fmt == 2 ? 64 : group, 1,
+         1, nullptr, nullptr};
+  a.grp = tiles;
+  a.xrow = x_rows;
+  a.ew = w_stride;
+  a.es = s_stride;
+  return run_grouped(a, fmt, true, bm, lga_moe_group_tiles(rows, n_expert, bm), stream);
 }

@@ -161,3 +161,70 @@ extern "C" int lga_moe_combine(const void* expert_out, const void* probs, const 
                                                     (const uint16_t*)residual, (uint16_t*)y, k, C);
   LGA_LAUNCH_RETURN();
 }
+
+// ---- grouped prefill: the tile table of lga_q4_gemm_grouped -------------------------------------------------------
+// One workgroup: a stable counting sort of the T * k (token, slot) pairs by expert (the reference's per-expert token
+// groups, lit_gpt/model.py:740-741, in (token, slot) order within each expert), then the m-tiles of bm rows per
+// expert. Outputs: tiles = {n_tiles, (expert, first row, rows) x n_tiles}, x_rows[r] = token of permuted row r,
+// y_rows[r] = token * k + slot (the row of the (T, k, C) expert-output tensor moe_combine reads).
+namespace lga {
+__global__ void __launch_bounds__(1024) moe_group_kernel(const int32_t* __restrict__ ids, int n, int k, int E, int bm,
+                                                         int32_t* __restrict__ tiles, int32_t* __restrict__ x_rows,
+                                                         int32_t* __restrict__ y_rows) {
+  __shared__ int cnt[8], base[8], run[8], wtot[16][8];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  if (tid < 8) cnt[tid] = run[tid] = 0;
+  __syncthreads();
+  for (int i = tid; i < n; i += 1024) atomicAdd(&cnt[min(max(ids[i], 0), E - 1)], 1);
+  __syncthreads();
+  if (tid == 0) {
+    int b = 0, t = 0;
+    for (int e = 0; e < E; ++e) {
+      base[e] = b;
+      for (int r = 0; r < cnt[e]; r += bm) {
+        tiles[1 + 3 * t] = e;
+        tiles[2 + 3 * t] = b + r;
+        tiles[3 + 3 * t] = min(bm, cnt[e] - r);
+        ++t;
+      }
+      b += cnt[e];
+    }
+    tiles[0] = t;
+  }
+  __syncthreads();
+  const unsigned long long lt = (1ull << lane) - 1ull;  // lanes below this one
+  for (int c0 = 0; c0 < n; c0 += 1024) {
+    const int i = c0 + tid;
+    const int e = i < n ? min(max(ids[i], 0), E - 1) : -1;
+    int rank = 0;
+    for (int x = 0; x < E; ++x) {
+      const unsigned long long m = __ballot(e == x);
+      if (e == x) rank = __popcll(m & lt);
+      if (lane == 0) wtot[wave][x] = __popcll(m);
+    }
+    __syncthreads();
+    if (e >= 0) {
+      int before = 0;
+      for (int w = 0; w < wave; ++w) before += wtot[w][e];
+      const int pos = base[e] + run[e] + before + rank;
+      x_rows[pos] = i / k;
+      y_rows[pos] = i;
+    }
+    __syncthreads();
+    if (tid < E) {
+      int tot = 0;
+      for (int w = 0; w < 16; ++w) tot += wtot[w][tid];
+      run[tid] += tot;
+    }
+    __syncthreads();
+  }
+}
+}  // namespace lga
+
+extern "C" int lga_moe_group(const int32_t* expert_ids, int T, int k, int n_expert, int bm, int32_t* tiles,
+                             int32_t* x_rows, int32_t* y_rows, hipStream_t stream) {
+  LGA_CHECK_ARG(expert_ids && tiles && x_rows && y_rows, "lga_moe_group: null pointer");
+  LGA_CHECK_ARG(T > 0 && k > 0 && n_expert > 0 && n_expert <= 8 && bm > 0, "lga_moe_group: needs n_expert <= 8");
+  lga::moe_group_kernel<<<1, 1024, 0, stream>>>(expert_ids, T * k, k, n_expert, bm, tiles, x_rows, y_rows);
+  LGA_LAUNCH_RETURN();
+}

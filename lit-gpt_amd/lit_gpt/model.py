@@ -480,6 +480,16 @@ class LLaMAMoE(nn.Module):
         self._stacks = out
         return out
 
+    def _grouped_ok(self, C: int) -> bool:
+        """The grouped prefill GEMMs take 4-bit experts whose shapes the fused MFMA kernel covers (else the loop)."""
+        from lit_gpt.quantize import QuantLinear
+
+        f1, pj = self.experts[0].fc_1, self.experts[0].proj
+        if not isinstance(f1, QuantLinear) or not isinstance(pj, QuantLinear):
+            return False
+        return bool(ops.q4f_fits(64, f1.out_features, C, f1.group, f1.fmt)
+                    and ops.q4f_fits(64, pj.out_features, pj.in_features, pj.group, pj.fmt))
+
     def _expert_hooks(self, x: torch.Tensor, eout: torch.Tensor) -> torch.Tensor:
         hooks = [list(e._forward_hooks.values()) for e in self.experts]
         if any(len(h) != len(hooks[0]) for h in hooks):
@@ -513,15 +523,25 @@ class LLaMAMoE(nn.Module):
             n = x2 if norm is None else norm(x2)
             router = _lin(self.gate, n)
             ids, probs = ops.moe_route(router.contiguous(), k)
-            eout = torch.empty(T, k, C, dtype=torch.bfloat16, device=x2.device)
-            for e in range(E):  # the reference's per-expert token groups (model.py:740-742)
-                tok, slot = torch.where(ids == e)
-                if tok.numel() == 0:
-                    continue
-                xe = n.index_select(0, tok)
-                ex = self.experts[e]
-                g = ops.swiglu(_lin(ex.fc_1, xe).contiguous(), _lin(ex.fc_2, xe).contiguous())
-                eout[tok, slot] = _lin(ex.proj, g)
+            if self._grouped_ok(C):
+                # the reference's per-expert token groups (model.py:740-742) as two grouped launches over a
+                # device-built tile table: no torch.where host sync, no gathered / scattered copies
+                rows, bm = T * k, ops.moe_grouped_bm(T * k)
+                tiles, x_rows, y_rows = ops.moe_group(ids, E, bm)
+                g = ops.q4_gemm_swiglu_grouped(n.contiguous(), q1, s1, q2, s2, tiles, x_rows, rows,
+                                               f1.out_features, C, f1.group, f1.fmt, bm, E)
+                eout = ops.q4_gemm_grouped(g, qp, sp, tiles, y_rows, rows, pj.out_features, pj.in_features,
+                                           pj.group, pj.fmt, bm, E).view(T, k, C)
+            else:
+                eout = torch.empty(T, k, C, dtype=torch.bfloat16, device=x2.device)
+                for e in range(E):  # the reference's per-expert token groups (model.py:740-742)
+                    tok, slot = torch.where(ids == e)
+                    if tok.numel() == 0:
+                        continue
+                    xe = n.index_select(0, tok)
+                    ex = self.experts[e]
+                    g = ops.swiglu(_lin(ex.fc_1, xe).contiguous(), _lin(ex.fc_2, xe).contiguous())
+                    eout[tok, slot] = _lin(ex.proj, g)
         eout = self._expert_hooks(x2, eout)
         return ops.moe_combine(eout.contiguous(), probs, ids, residual=res).view(*lead, C)
 

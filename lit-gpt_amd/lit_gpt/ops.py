@@ -70,6 +70,12 @@ SIGNATURES = {
     "lga_q4_gemv_swiglu_experts": [_P, _P, _P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _F,
                                    _P, _I, _I, _I, _I, _I, _P],
     "lga_moe_combine": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
+    "lga_moe_group_tiles": [_I, _I, _I],
+    "lga_moe_group": [_P, _I, _I, _I, _I, _P, _P, _P, _P],
+    "lga_q4_gemm_swiglu_grouped": [_P, _P, _P, _P, _P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, _P, _I, _I, _I,
+                                   _I, _I, _I, _I, _P],
+    "lga_q4_gemm_grouped": [_P, _P, _P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, _P, _P, _I, _I, _I, _I, _I,
+                            _I, _I, _P],
     "lga_comm_mailbox_bytes": [_I],
     "lga_comm_alloc": [ctypes.c_size_t, ctypes.POINTER(_P), _P],
     "lga_comm_open": [_P, ctypes.POINTER(_P)],
@@ -568,6 +574,50 @@ def q4_gemv_swiglu_experts(x, qw1, sc1, qw2, sc2, ids, N, K, group, fmt, *, norm
         _dev(sc2, "sc2"), _dev(ids, "ids", torch.int32), k, qw1.size(0), ws, ss,
         _opt(norm_weight, "norm_weight", torch.bfloat16), float(eps), _dev(y, "y", torch.bfloat16), N, K, group, fmt,
         variant, _stream()))
+    return y
+
+
+def moe_group(ids, n_expert, bm):
+    """(T, k) int32 expert ids -> (tiles, x_rows, y_rows) of the grouped prefill GEMMs (lga_moe_group): the
+    (token, slot) pairs sorted by expert on the device, m-tiles of ``bm`` rows; no host synchronisation."""
+    T, k = ids.shape
+    lib = load_library()
+    cap = int(lib.lga_moe_group_tiles(T * k, int(n_expert), int(bm)))
+    tiles = torch.empty(1 + 3 * cap, dtype=torch.int32, device=ids.device)
+    x_rows = torch.empty(T * k, dtype=torch.int32, device=ids.device)
+    y_rows = torch.empty(T * k, dtype=torch.int32, device=ids.device)
+    _check(lib.lga_moe_group(_dev(ids, "ids", torch.int32), T, k, int(n_expert), int(bm), _dev(tiles, "tiles"),
+                             _dev(x_rows, "x_rows"), _dev(y_rows, "y_rows"), _stream()))
+    return tiles, x_rows, y_rows
+
+
+def moe_grouped_bm(rows: int) -> int:
+    """Tile height of the grouped prefill GEMMs for ``rows`` permuted rows (T * k)."""
+    return 64 if rows <= 512 else 256
+
+
+def q4_gemm_swiglu_grouped(x, w1, s1, w2, s2, tiles, x_rows, rows, N, K, group, fmt, bm, n_expert, *, out=None):
+    """g (rows, N): permuted row r = bf16(silu(bf16(x[x_rows[r]] W1_e^T))) * bf16(x[x_rows[r]] W2_e^T), e the row's
+    expert, W stacked (E, N, K/2) — every expert's rows in one launch."""
+    ws, ss = _expert_strides(w1, s1)
+    y = out if out is not None else torch.empty(rows, N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_q4_gemm_swiglu_grouped(
+        _dev(x, "x", torch.bfloat16), _dev(w1, "w1", torch.uint8), _dev(s1, "s1"), _dev(w2, "w2", torch.uint8),
+        _dev(s2, "s2"), ws, ss, _dev(tiles, "tiles", torch.int32), _dev(x_rows, "x_rows", torch.int32),
+        _dev(y, "y", torch.bfloat16), int(rows), int(N), int(K), int(group), int(fmt), int(bm), int(n_expert),
+        _stream()))
+    return y
+
+
+def q4_gemm_grouped(x, w, s, tiles, y_rows, rows, N, K, group, fmt, bm, n_expert, *, x_rows=None, out=None):
+    """y[y_rows[r]] = x[r] W_e^T for every permuted row r (x rows in permuted order unless ``x_rows``)."""
+    ws, ss = _expert_strides(w, s)
+    y = out if out is not None else torch.empty(rows, N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_q4_gemm_grouped(
+        _dev(x, "x", torch.bfloat16), _dev(w, "w", torch.uint8), _dev(s, "s"), ws, ss,
+        _dev(tiles, "tiles", torch.int32), _opt(x_rows, "x_rows", torch.int32), _opt(y_rows, "y_rows", torch.int32),
+        _dev(y, "y", torch.bfloat16), int(rows), int(N), int(K), int(group), int(fmt), int(bm), int(n_expert),
+        _stream()))
     return y
 
 

@@ -266,3 +266,62 @@ def test_fused_gemm_split_k_handoff_stress(ops, M, bn, splits, monkeypatch):
     h2 = (xa.float() @ ops.q4_dequantize(q2, s2, N, K, 128, 0).float().t()).to(torch.bfloat16)
     ref = ops.swiglu(h1.contiguous(), h2.contiguous()).float()
     assert float((ga.float() - ref).abs().sub(_swiglu_tol(h1.float(), h2.float(), ref)).max()) <= 0.0
+
+
+# ------------------------------------------------------------------------------------------------ grouped MoE prefill
+def _group_reference(ids: np.ndarray, E: int, bm: int):
+    """CPU restatement of lga_moe_group: stable sort of the (token, slot) pairs by expert, m-tiles of bm rows."""
+    T, k = ids.shape
+    flat = ids.reshape(-1)
+    order = np.argsort(flat, kind="stable")
+    tiles, b = [], 0
+    for e in range(E):
+        c = int((flat == e).sum())
+        for r in range(0, c, bm):
+            tiles.append((e, b + r, min(bm, c - r)))
+        b += c
+    return tiles, (order // k).astype(np.int32), order.astype(np.int32)
+
+
+@pytest.mark.parametrize("T,k,E,bm", [(1, 2, 8, 64), (37, 2, 8, 64), (300, 2, 8, 256), (2048, 2, 8, 256), (50, 3, 5, 64)])
+def test_moe_group_table_matches_stable_sort(ops, T, k, E, bm):
+    rng = np.random.default_rng(T * 7 + E)
+    ids = np.stack([rng.choice(E, size=k, replace=False) for _ in range(T)]).astype(np.int32)
+    tiles, xr, yr = ops.moe_group(torch.from_numpy(ids).to(DEV), E, bm)
+    t_ref, xr_ref, yr_ref = _group_reference(ids, E, bm)
+    tl = tiles.cpu().numpy()
+    assert tl[0] == len(t_ref)
+    assert [tuple(tl[1 + 3 * i: 4 + 3 * i]) for i in range(tl[0])] == t_ref
+    assert np.array_equal(xr.cpu().numpy(), xr_ref) and np.array_equal(yr.cpu().numpy(), yr_ref)
+
+
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64)])
+@pytest.mark.parametrize("T", [5, 200, 700])
+def test_grouped_expert_gemms_equal_per_expert_gemms(ops, fmt, group, T, monkeypatch):
+    """The grouped prefill (fc_1 || fc_2 + SwiGLU over every expert's rows in one launch, then the grouped proj
+    scattered to (token, slot)) against the per-expert fused GEMMs on gathered rows — the reference's loop
+    (model.py:740-742) — bit for bit (no split-K on either side: each output's K-steps accumulate in order)."""
+    monkeypatch.setenv("LGA_Q4F_SPLITS", "1")
+    E, k, C, I = 4, 2, 512, 768
+    rng = np.random.default_rng(T + fmt)
+    ids = np.stack([rng.choice(E, size=k, replace=False) for _ in range(T)]).astype(np.int32)
+    g0 = torch.Generator(device=DEV).manual_seed(T)
+    q = {}
+    for name, (N, K) in (("fc1", (I, C)), ("fc2", (I, C)), ("proj", (C, I))):
+        ws = [ops.quantize(torch.randn(N, K, generator=g0, device=DEV) * 0.02, fmt, group) for _ in range(E)]
+        q[name] = (torch.stack([w for w, _ in ws]), torch.stack([s for _, s in ws]))
+    x = torch.randn(T, C, generator=g0, device=DEV).to(torch.bfloat16)
+    rows, bm = T * k, ops.moe_grouped_bm(T * k)
+    tiles, x_rows, y_rows = ops.moe_group(torch.from_numpy(ids).to(DEV), E, bm)
+    g = ops.q4_gemm_swiglu_grouped(x, *q["fc1"], *q["fc2"], tiles, x_rows, rows, I, C, group, fmt, bm, E)
+    eout = ops.q4_gemm_grouped(g, *q["proj"], tiles, y_rows, rows, C, I, group, fmt, bm, E).view(T, k, C)
+    ref = torch.empty(T, k, C, dtype=torch.bfloat16, device=DEV)
+    idt = torch.from_numpy(ids).to(DEV)
+    for e in range(E):
+        tok, slot = torch.where(idt == e)
+        if tok.numel() == 0:
+            continue
+        xe = x.index_select(0, tok).contiguous()
+        ge = ops.q4_gemm_swiglu(xe, q["fc1"][0][e], q["fc1"][1][e], q["fc2"][0][e], q["fc2"][1][e], I, C, group, fmt)
+        ref[tok, slot] = ops.q4_gemm_fused(ge, q["proj"][0][e], q["proj"][1][e], C, I, group, fmt)
+    assert torch.equal(eout, ref)

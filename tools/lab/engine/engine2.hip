@@ -47,7 +47,8 @@ constexpr int KEYS = 16;            // keys per attention tile (4 per 16-lane ro
 constexpr int HS = 128;
 constexpr unsigned long long TMO = 2000000ull;  // 20 ms of the 100 MHz clock
 constexpr size_t kArgsBytes = 8192;  // the Args block at the start of the scratch (counters follow)
-constexpr int LDS_MIN = 84 * 1024;  // > 80 KB: one workgroup per CU, all resident
+constexpr int LDS_MIN = 84 * 1024;
+constexpr int MAXJ = 8;             // output records per compute wave per op (fc_1 || fc_2: <= 6 tiles)  // > 80 KB: one workgroup per CU, all resident
 
 enum Kind { QKV = 0, ATT = 1, OPJ = 2, FC = 3, DN = 4, LM = 5 };
 
@@ -132,7 +133,7 @@ __host__ inline bool make_geo(const lga_engine_geom& g, Geo& o) {
   o.total = off;
   const int kmax = o.C > o.I ? o.C : o.I;
   o.sb = ((kmax * 2 + (kmax / 32) * 4) + 15) & ~15;
-  const int need = 1024 + 2 * o.sb + o.C * 2 + 3 * HS * 2 + NCW * (HS + 4) * 4 + 64;
+  const int need = 1024 + 2 * o.sb + o.C * 2 + 3 * HS * 2 + NCW * (HS + 4) * 4 + 2 * NCW * MAXJ * 16 + 64;
   o.lds = need > LDS_MIN ? need : LDS_MIN;
   return true;
 }
@@ -226,6 +227,8 @@ struct Ctl {
   __device__ unsigned* best(int cw) const { return w() + 16 + 2 * cw; }
   __device__ float* red(int par) const { return (float*)(w() + 32 + 4 * (par & 1)); }
   __device__ unsigned* last() const { return w() + 40; }
+  __device__ unsigned* edge() const { return w() + 41; }                  // op index + 1 whose input edge is complete
+  __device__ unsigned* rcnt(int k, int cw) const { return w() + 48 + 8 * (k & 1) + cw; }  // records per wave
 };
 struct Lds {
   int sb, C;
@@ -233,6 +236,11 @@ struct Lds {
   __device__ uint16_t* raw() const { return (uint16_t*)(e2_smem + 1024 + 2 * (size_t)sb); }  // residual input
   __device__ uint16_t* qst() const { return raw() + C; }  // roped q, roped k_new, v_new (bf16 heads)
   __device__ float* amrg() const { return (float*)(qst() + 3 * HS); }  // per compute wave: m, l, -, -, o[HS]
+  // op outputs of this CU for the gather waves to publish: per op parity, per compute wave, MAXJ records of
+  // {element offset, count (2 or 4), 4 bf16}; the wave's record count in rcnt
+  __device__ uint4* rec(int k, int w, int j) const {
+    return (uint4*)(amrg() + NCW * (HS + 4)) + ((size_t)(k & 1) * NCW + w) * MAXJ + j;
+  }
 };
 __device__ __forceinline__ unsigned lds_ld(const unsigned* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -639,10 +647,16 @@ __device__ __forceinline__ void consume(const Args& a, const Dyn& dy, const Ctx&
       break;
     }
   }
-  // write-through (sc1) stores: the consumers on other CUs read them with sc1 loads (MI355X_MICROARCH.md "Valid forms")
-  if (lane == 0) {
-    if (st8) __hip_atomic_store((gptr<uint64_t>)G(dst), val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else __hip_atomic_store((gptr<uint32_t>)G(dst), (uint32_t)val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the outputs go to an LDS record the gather waves publish (a compute wave's own stores could only be drained
+  // behind its in-flight tile loads: vmcnt is in order); lm_head logits (read by the host only) go out directly
+  if (lane == 0 && kind != ATT && !(kind == DN && (cur.j & 1) == 0)) {
+    if (kind == LM) {
+      __hip_atomic_store((gptr<uint64_t>)G(dst), val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      const int jr = kind == DN ? cur.j >> 1 : cur.j;
+      const uint32_t eoff = (uint32_t)(((const uint16_t*)dst) - act(a, 0));
+      *s.rec(cur.k, x.w, jr) = make_uint4(eoff, st8 ? 4u : 2u, (uint32_t)val, (uint32_t)(val >> 32));
+    }
   }
 }
 
@@ -683,22 +697,13 @@ __device__ __forceinline__ void cw_signal(const Args& a, const Ctx& x, const Lds
       ctl.best(x.w)[0] = __float_as_uint(st.best_v);
       ctl.best(x.w)[1] = (unsigned)st.best_i;
     }
-  } else {
-    unsigned old = 0;
-    if (lane == 0) old = lds_add(ctl.arr(k), 1u);
-    old = __shfl(old, 0);
-    if (old == (unsigned)(NCW * (k / 4 + 1) - 1) && lane == 0) {  // the CU's last wave on this op
-      const int c = x.c;
-      int slot;
-      switch (kind) {
-        case QKV: slot = g.c_qkv + l * g.G + c % g.G; break;
-        case OPJ: slot = g.c_xp + l * NSH + c % NSH; break;
-        case FC: slot = g.c_g + l * NSH + c % NSH; break;
-        default: slot = g.c_xo + l * NSH + c % NSH; break;
-      }
-      g_add_nr(ctr(a, slot), 1u);
-    }
   }
+  if (kind != ATT && kind != LM && lane == 0) {
+    const int n = my_tiles(g, k, x.c, x.w, x.sp);
+    *ctl.rcnt(k, x.w) = (unsigned)(kind == DN ? n / 2 : n);
+  }
+  // every op counts its compute waves in slot k % 4 (so slot k % 4 holds NCW per op k' <= k, k' = k mod 4)
+  if (lane == 0) lds_add(ctl.arr(k), 1u);
   if (lane == 0) lds_st(ctl.prog(x.w), (unsigned)(k + 1));
   if (x.w == 0) E2TRACE(k, 7);
 }
@@ -738,15 +743,11 @@ __device__ __forceinline__ void run_cw(const Args& a, const Dyn& dy, const Lds& 
   issue(a, x, nx, B);
   nx = next(nx);
   int done = 0;       // ops signalled
-  bool first_tile = true;
   bool aborted = false;
-  // before consuming a tile of op cur.k: every earlier op of this wave is finished (its stores drained by the
-  // vmcnt(16) — only the next tile's 16 loads may still fly), post them; then wait for op cur.k's input
+  // before consuming a tile of op cur.k: every earlier op of this wave is finished (its outputs are LDS records),
+  // post them; then wait for op cur.k's input
   auto boundary = [&](const Cur& c) -> bool {
-    if (done < c.k) {
-      if (!first_tile) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-      for (; done < c.k; ++done) cw_signal(a, x, s, ctl, done, st);
-    }
+    for (; done < c.k; ++done) cw_signal(a, x, s, ctl, done, st);
     if (!lds_wait(a, ctl, clk, ctl.ready(), (unsigned)(c.k + 1), 8u)) return false;
     if (w == 0 && c.j == 0) E2TRACE(c.k, 6);
     if (kind_of(g, c.k) == ATT && c.j == 0) {  // the roped query, once per attention op
@@ -756,7 +757,6 @@ __device__ __forceinline__ void run_cw(const Args& a, const Dyn& dy, const Lds& 
   };
   while (cur.k < nops) {
     if (!boundary(cur)) { aborted = true; break; }
-    first_tile = false;
     consume(a, dy, x, s, cur, A, st);
     issue(a, x, nx, A);
     nx = next(nx);
@@ -969,6 +969,49 @@ __device__ __forceinline__ bool gw_attention(const Args& a, const Lds& s, const 
   return true;
 }
 
+// gather wave 0: once every compute wave finished GEMV op k, store the CU's outputs (the LDS records) write-through,
+// drain, and arrive once on the op's agent-scope counter (MI355X_MICROARCH.md "Valid forms" row 1): this wave
+// streams nothing, so the drain waits only for these stores
+__device__ __forceinline__ bool gw_publish(const Args& a, const Lds& s, const Ctl& ctl, const Clock& clk, int k) {
+  const Geo& g = a.g;
+  const int kind = kind_of(g, k), l = k / OPS, lane = threadIdx.x & 63, c = blockIdx.x;
+  if (!lds_wait(a, ctl, clk, ctl.arr(k), (unsigned)(NCW * (k / 4 + 1)), 4096u)) return false;
+  const int w = lane / MAXJ, j = lane % MAXJ;
+  if ((unsigned)j < lds_ld(ctl.rcnt(k, w))) {
+    const uint4 r = *s.rec(k, w, j);
+    uint16_t* dst = act(a, 0) + r.x;
+    if (r.y == 4u)
+      __hip_atomic_store((gptr<uint64_t>)G((uint64_t*)dst), (uint64_t)r.z | ((uint64_t)r.w << 32), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    else
+      __hip_atomic_store((gptr<uint32_t>)G((uint32_t*)dst), r.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  drain();
+  if (lane == 0) {
+    int slot;
+    switch (kind) {
+      case QKV: slot = g.c_qkv + l * g.G + c % g.G; break;
+      case OPJ: slot = g.c_xp + l * NSH + c % NSH; break;
+      case FC: slot = g.c_g + l * NSH + c % NSH; break;
+      default: slot = g.c_xo + l * NSH + c % NSH; break;
+    }
+    g_add_nr(ctr(a, slot), 1u);
+  }
+  return true;
+}
+
+// op k's input edge: gather wave 0 polls the counters, the other gather waves wait for its LDS word
+__device__ __forceinline__ bool gw_edge(const Args& a, const Ctl& ctl, const Clock& clk, int k, int first, int n,
+                                        unsigned target, unsigned code) {
+  const int gw = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (gw == 0) {
+    if (!poll_ctrs(a, ctl, clk, first, n, 1, target, code)) return false;
+    if ((threadIdx.x & 63) == 0) lds_st(ctl.edge(), (unsigned)(k + 1));
+    return true;
+  }
+  return lds_wait(a, ctl, clk, ctl.edge(), (unsigned)(k + 1), code);
+}
+
 __device__ __forceinline__ void run_gw(const Args& a, const Dyn& dy, const Lds& s, const Ctl& ctl, const Clock& clk,
                                        long p, int nops, unsigned epoch) {
   const Geo& g = a.g;
@@ -986,31 +1029,35 @@ __device__ __forceinline__ void run_gw(const Args& a, const Dyn& dy, const Lds& 
       case LM: {
         const int li = kind == LM ? g.L : l;  // input = output of block li - 1 (or the embedding)
         const uint16_t* src = li == 0 ? (const uint16_t*)(a.scratch + g.o_x0) : act(a, li - 1) + g.a_x;
-        if (li > 0) ok = poll_ctrs(a, ctl, clk, g.c_xo + (li - 1) * NSH, NSH, 1, all32, 256u);
+        if (li > 0) ok = gw_edge(a, ctl, clk, k, g.c_xo + (li - 1) * NSH, NSH, all32, 256u);
         E2TRACE(k, 1);
         if (ok)
           ok = stage_op<2>(a, s, ctl, clk, ns, k, src, li > 0, g.C,
                            kind == LM ? a.ln_f : (const uint16_t*)Lp->norm1, kind == QKV);
+        if (ok && kind == QKV && gw == 0) ok = gw_publish(a, s, ctl, clk, k);
         break;
       }
       case ATT:
         if (gw == 0) ok = gw_attention(a, s, ctl, clk, k, p, epoch);
         break;
       case OPJ:
-        ok = poll_ctrs(a, ctl, clk, g.c_y + l * NSH, NSH, 1, (epoch + 1) * (unsigned)(g.G / NSH), 512u);
+        ok = gw_edge(a, ctl, clk, k, g.c_y + l * NSH, NSH, (epoch + 1) * (unsigned)(g.G / NSH), 512u);
         E2TRACE(k, 1);
         if (ok) ok = stage_op<2>(a, s, ctl, clk, ns, k, act(a, l) + g.a_y, true, g.C, nullptr, false);
+        if (ok && gw == 0) ok = gw_publish(a, s, ctl, clk, k);
         break;
       case FC:
-        ok = poll_ctrs(a, ctl, clk, g.c_xp + l * NSH, NSH, 1, all32, 1024u);
+        ok = gw_edge(a, ctl, clk, k, g.c_xp + l * NSH, NSH, all32, 1024u);
         E2TRACE(k, 1);
         if (ok)
           ok = stage_op<2>(a, s, ctl, clk, ns, k, act(a, l) + g.a_xp, true, g.C, (const uint16_t*)Lp->norm2, true);
+        if (ok && gw == 0) ok = gw_publish(a, s, ctl, clk, k);
         break;
       default:  // DN
-        ok = poll_ctrs(a, ctl, clk, g.c_g + l * NSH, NSH, 1, all32, 2048u);
+        ok = gw_edge(a, ctl, clk, k, g.c_g + l * NSH, NSH, all32, 2048u);
         E2TRACE(k, 1);
         if (ok) ok = stage_op<6>(a, s, ctl, clk, ns, k, act(a, l) + g.a_g, true, g.I, nullptr, false);
+        if (ok && gw == 0) ok = gw_publish(a, s, ctl, clk, k);
         break;
     }
     E2TRACE(k, 5);
@@ -1124,6 +1171,12 @@ const char* unsupported(const lga_engine_geom* g, lga::e2::Geo& o) {
   if (!make_geo(*g, o)) return "bad geometry";
   if (o.QT % 1 || (o.GQ % 4)) return "qkv rows per group must be a multiple of 4";
   if (o.lds > 163840) return "LDS budget exceeded";
+  {  // every compute wave's GEMV tiles of one op fit its MAXJ output records
+    const int S = NCW * o.P;
+    if ((o.I / 2 + S - 1) / S > MAXJ || (o.C / 4 + S - 1) / S > MAXJ || (o.C / 2 + S - 1) / S > MAXJ ||
+        (o.QT + o.SP * NCW - 1) / (o.SP * NCW) > MAXJ)
+      return "more GEMV tiles per compute wave than output records";
+  }
   return nullptr;
 }
 
