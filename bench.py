@@ -314,6 +314,59 @@ def cpu_baseline(cfg, threads: int, seconds: float = 15.0):
                       f"({per_token * 1e3:.1f} ms/token)"}
 
 
+def time_sampled_decode(model, first, T: int, warmup: int, steps: int, barrier, world: int):
+    """The reference's default sampling (generate/base.py:102-103: top_k 200, temperature 0.8) as captured decode
+    steps: the same positions as the greedy timed region, the argmax replaced by the fused top-k + softmax +
+    inverse-CDF sampler (ops.sample_topk inside DecodeGraph). Also the sampler launch alone on the step's logits."""
+    from generate.base import SamplerRNG
+    from lit_gpt import ops
+    from lit_gpt.runtime import DecodeGraph
+
+    dev = first.device
+    torch.manual_seed(1234)
+    rng = SamplerRNG(dev)
+    dg = DecodeGraph(model, first, T, chunk=CHUNK, temperature=0.8, top_k=200, rng=rng)
+
+    def run(n):
+        done = 0
+        while n - done >= CHUNK > 1:
+            dg.steps()
+            done += CHUNK
+        for _ in range(n - done):
+            dg.step()
+
+    run(warmup)
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    run(steps)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    logits = model(dg.token, dg.pos, last_token_only=True).reshape(-1).contiguous()
+    counter = torch.zeros(1, dtype=torch.int64, device=dev)
+    out = torch.zeros(1, dtype=torch.int64, device=dev)
+    for _ in range(5):
+        ops.sample_topk(logits, 200, 0.8, seed=rng.seed, counter=counter, out_idx=out)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(100):
+        ops.sample_topk(logits, 200, 0.8, seed=rng.seed, counter=counter, out_idx=out)
+    e1.record()
+    torch.cuda.synchronize()
+    return {"top_k": 200, "temperature": 0.8, "tokens_per_s": round(steps / elapsed, 2),
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "sampler_us": round(e0.elapsed_time(e1) * 10, 2),
+            "note": "generate/base.py's default sampling, captured: the greedy run's positions with the argmax "
+                    "replaced by lga_sample_topk (top-k radix select, bf16 softmax, inverse CDF on a counter-based "
+                    "uniform, embedding row gather); sampler_us = that launch alone on one step's logits"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -328,6 +381,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-sample", action="store_true",
+                    help="skip the sampled-decode line (top_k 200, temperature 0.8: generate/base.py's defaults)")
     ap.add_argument("--no-traffic", action="store_true", help="skip the rocprofv3 PMC pass for roofline.traffic")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-pos", type=int, default=PROMPT_LEN + 254, help=argparse.SUPPRESS)
@@ -433,6 +488,9 @@ def main():
         ms_step = elapsed / args.steps * 1e3
         avg_ms, kbytes = time_dominant_kernel(model)
         att_ms, att_bytes = time_attention(model, T + args.warmup + args.steps)
+        sampled = None
+        if use_graph and not args.no_sample and cfg.vocab_size <= 65536:
+            sampled = time_sampled_decode(model, first, T, args.warmup, args.steps, barrier, world)
 
     cfg_full = Config.from_name(args.model)
     pf_flops = prefill_flops(cfg_full, T, tp=world)
@@ -505,6 +563,7 @@ def main():
         "reference_style_tokens_per_s": round((args.steps + args.warmup + 1) / (prefill_s + elapsed * (
             args.steps + args.warmup + 1) / args.steps), 2),
         "load_s": round(load_s, 2),
+        "sampled_decode": sampled,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
         # the reference's CPU path on all the host cores this process may run on — the affinity set,

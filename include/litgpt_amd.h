@@ -230,6 +230,20 @@ int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, 
 int lga_argmax_embed(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
                      const void* table, int n_embd, int vocab, void* emb_out, lga_stream_t stream);
 
+/* -- temperature sampling (generate/base.py:30-41 with top_k and temperature > 0: torch.topk, scatter into -inf,
+ *    softmax(logits / temperature) in the logits' dtype, torch.multinomial(probs, 1)) in ONE launch --------------
+ * logits: n (<= 65536) bf16. Keeps the top_k (1..1024) largest (NaN largest, ties lowest index first),
+ * x = bf16(v / temperature), p = bf16(exp(x - max) / sum); the token is the first kept index (in index order) whose
+ * running fp32 sum of p divided by the total reaches u (torch's CPU inverse CDF). u = *uniform when uniform is
+ * given, else a counter-based hash of (seed, *counter) in (0, 1), and *counter advances by one (device state: the
+ * launch replays in a graph). Then lga_argmax's bookkeeping (out_idx, token_out, *pos_inout += 1) and, with emb_out,
+ * lga_argmax_embed's row gather. kept_out (top_k int32) / probs_out (top_k bf16), optional: the kept indices in
+ * index order and their probabilities. */
+int lga_sample_topk(const void* logits, int n, int top_k, float temperature, const float* uniform,
+                    unsigned long long seed, unsigned long long* counter, int64_t* out_idx, int32_t* token_out,
+                    int64_t* pos_inout, const void* table, int n_embd, int vocab, void* emb_out, int32_t* kept_out,
+                    void* probs_out, lga_stream_t stream);
+
 /* -- fp32 forward (the reference's --precision 32-true, generate/base.py:132; BASELINE config 1 pythia-160m fp32):
  *    float32 weights and activations, no bf16 rounding; plumbing-sized kernels (csrc/fp32.hip) -------------- */
 /* y (M, N) = x (M, K) . w (N, K)^T (+ bias[N]) (+ residual (M, N)) — F.linear (lit_gpt/model.py:519,619,656,699-702) */

@@ -25,7 +25,7 @@ wd = Path(__file__).parent.parent.resolve()
 if str(wd) not in sys.path:
     sys.path.append(str(wd))
 
-from generate.base import build_model, next_token  # noqa: E402
+from generate.base import SamplerRNG, build_model, graph_sampling, next_token  # noqa: E402
 from lit_gpt import GPT, Config  # noqa: E402
 
 
@@ -33,22 +33,24 @@ def _tokens(model: GPT, prompt: torch.Tensor, n: int, temperature: float, top_k:
             use_graph: bool) -> Iterator[torch.Tensor]:
     """Up to ``n`` new tokens, one at a time: prefill at arange(T), then single-token steps."""
     T = prompt.size(0)
+    rng = SamplerRNG(prompt.device) if temperature > 0.0 else None
     token = next_token(model, torch.arange(0, T, device=prompt.device), prompt.view(1, -1),
-                       temperature=temperature, top_k=top_k).clone()
+                       temperature=temperature, top_k=top_k, rng=rng).clone()
     yield token
     if n <= 1:
         return
-    if temperature == 0.0 and use_graph:
+    if use_graph and graph_sampling(model, temperature, top_k):
         from lit_gpt.runtime import DecodeGraph
 
-        dg = DecodeGraph(model, token, T)
+        dg = DecodeGraph(model, token, T, temperature=temperature, top_k=top_k, rng=rng)
         yield dg.token.view(-1)[:1].clone()
         for _ in range(n - 2):
             yield dg.step().view(-1)[:1].clone()
         return
     input_pos = torch.tensor([T], device=prompt.device)
     for _ in range(n - 1):
-        token = next_token(model, input_pos, token.view(1, -1), temperature=temperature, top_k=top_k).clone()
+        token = next_token(model, input_pos, token.view(1, -1), temperature=temperature, top_k=top_k,
+                           rng=rng).clone()
         yield token
         input_pos = input_pos.add_(1)
 

@@ -123,6 +123,171 @@ __global__ void __launch_bounds__(1024) argmax_f32_kernel(const float* __restric
   }
 }
 
+// ---- temperature > 0: top-k + softmax + multinomial on the device (generate/base.py:30-41) -----------------------
+// The reference's default invocation (generate/base.py:102-103: top_k 200, temperature 0.8) as ONE launch inside the
+// decode graph:
+//   v, i = torch.topk(logits, k); logits = full(-inf).scatter(i, v)      -> the kept set, in index order
+//   probs = softmax(logits / temperature) in the logits' dtype (bf16)     -> p = bf16(exp(x - max) / sum), x = bf16(v / T)
+//   multinomial(probs, 1)                                                 -> first index whose normalised running sum
+//                                                                            reaches a uniform u (torch's CPU inverse CDF)
+// Top-k is a two-pass radix select on the bf16 bits (256-bin LDS histograms) of a 16-bit order key (NaN highest, -0 ==
+// +0); ties at the k-th value are kept lowest-index first (CUDA torch.topk's order; the CPU one is the heap order of
+// std::partial_sort). u comes from `uniform` when given (tests: the reference's test patches the draw,
+// tests/test_generate.py:19-46), else from a counter-based hash of (seed, *counter) — the counter lives on the device
+// and advances per call, so the launch replays in a HIP graph. Then the argmax kernel's bookkeeping: token, input_pos,
+// the next step's embedding row.
+__device__ __forceinline__ unsigned order_key(uint16_t b) {
+  if ((b & 0x7F80u) == 0x7F80u && (b & 0x7Fu)) return 0xFFFFu;  // NaN: above everything
+  if (b == 0x8000u) b = 0;                                      // -0 == +0
+  return (b & 0x8000u) ? (~(unsigned)b & 0xFFFFu) : ((unsigned)b | 0x8000u);
+}
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {  // splitmix64 finaliser
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+constexpr int kMaxTopK = 1024;
+
+__global__ void __launch_bounds__(1024) topk_sample_kernel(
+    const uint16_t* __restrict__ logits, int n, int k, float temperature, const float* __restrict__ uniform,
+    unsigned long long seed, unsigned long long* __restrict__ counter, int64_t* __restrict__ out_idx,
+    int32_t* __restrict__ token_out, int64_t* __restrict__ pos_inout, const uint16_t* __restrict__ table, int C,
+    int V, uint16_t* __restrict__ emb_out, int32_t* __restrict__ kept_out, uint16_t* __restrict__ probs_out) {
+  __shared__ unsigned hist[256];
+  __shared__ unsigned scan[1024];
+  __shared__ int kidx[kMaxTopK];
+  __shared__ float kval[kMaxTopK];
+  __shared__ float red[16];
+  __shared__ unsigned s_b1, s_above, s_key, s_gt;
+  __shared__ int s_tok;
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  k = min(k, n);
+  const int ept = (n + 1023) / 1024, i0 = min(t * ept, n), i1 = min(i0 + ept, n);
+  // ---- radix select of the k-th largest key: high byte, then low byte ----
+  if (t < 256) hist[t] = 0;
+  __syncthreads();
+  for (int i = i0; i < i1; ++i) atomicAdd(&hist[order_key(logits[i]) >> 8], 1u);
+  __syncthreads();
+  if (t == 0) {
+    unsigned c = 0, b = 255;
+    for (;; --b) {
+      if (c + hist[b] >= (unsigned)k || b == 0) break;
+      c += hist[b];
+    }
+    s_b1 = b;
+    s_above = c;
+  }
+  __syncthreads();
+  if (t < 256) hist[t] = 0;
+  __syncthreads();
+  const unsigned b1 = s_b1;
+  for (int i = i0; i < i1; ++i) {
+    const unsigned key = order_key(logits[i]);
+    if ((key >> 8) == b1) atomicAdd(&hist[key & 255u], 1u);
+  }
+  __syncthreads();
+  if (t == 0) {
+    unsigned c = s_above, b = 255;
+    for (;; --b) {
+      if (c + hist[b] >= (unsigned)k || b == 0) break;
+      c += hist[b];
+    }
+    s_key = (b1 << 8) | b;
+    s_gt = c;  // keys strictly above the k-th
+  }
+  __syncthreads();
+  // ---- the kept set in index order: every key above the k-th, then ties lowest index first ----
+  const unsigned kth = s_key, need = (unsigned)k - s_gt;
+  unsigned ties = 0, above = 0;
+  for (int i = i0; i < i1; ++i) {
+    const unsigned key = order_key(logits[i]);
+    ties += key == kth;
+    above += key > kth;
+  }
+  auto block_scan = [&](unsigned v) -> unsigned {  // exclusive prefix over threads in index order
+    scan[t] = v;
+    __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+      const unsigned o = t >= off ? scan[t - off] : 0u;
+      __syncthreads();
+      scan[t] += o;
+      __syncthreads();
+    }
+    const unsigned incl = scan[t];
+    __syncthreads();
+    return incl - v;
+  };
+  const unsigned tie_before = block_scan(ties);
+  unsigned pos = block_scan(above + min(ties, need > tie_before ? need - tie_before : 0u));
+  unsigned tie_seen = tie_before;
+  for (int i = i0; i < i1; ++i) {
+    const uint16_t b = logits[i];
+    const unsigned key = order_key(b);
+    bool keep = key > kth;
+    if (key == kth) keep = tie_seen++ < need;
+    if (keep) {
+      kidx[pos] = i;
+      kval[pos] = bf2f(b);
+      ++pos;
+    }
+  }
+  __syncthreads();
+  // ---- softmax over the kept logits / temperature, in bf16 like the reference's bf16 tensor ops ----
+  const bool mine = t < k;
+  const float x = mine ? round_bf(kval[t] / temperature) : -INFINITY;
+  float m = wave_max(x);
+  if (lane == 0) red[wave] = m;
+  __syncthreads();
+  m = red[0];
+  for (int w = 1; w < 16; ++w) m = fmaxf(m, red[w]);
+  __syncthreads();
+  const float e = mine ? expf(x - m) : 0.0f;
+  float sum = wave_sum(e);
+  if (lane == 0) red[wave] = sum;
+  __syncthreads();
+  sum = 0.0f;
+  for (int w = 0; w < 16; ++w) sum += red[w];
+  const float p = mine ? round_bf(e / sum) : 0.0f;
+  if (mine) kval[t] = p;
+  if (mine && kept_out) kept_out[t] = kidx[t];
+  if (mine && probs_out) probs_out[t] = f2bf(p);
+  __syncthreads();
+  // ---- multinomial: torch's CPU inverse CDF (running fp32 sum in index order, normalised, first >= u) ----
+  if (t == 0) {
+    float u;
+    if (uniform) {
+      u = *uniform;
+    } else {
+      const unsigned long long c = *counter;
+      *counter = c + 1;
+      u = ((float)(mix64(seed ^ (c * 0xD1B54A32D192ED03ull)) >> 40) + 0.5f) * 0x1.0p-24f;  // in (0, 1)
+    }
+    float tot = 0.0f;
+    for (int j = 0; j < k; ++j) tot += kval[j];
+    float cum = 0.0f;
+    int pick = kidx[k - 1];
+    for (int j = 0; j < k; ++j) {
+      cum += kval[j];
+      if (cum / tot >= u) {
+        pick = kidx[j];
+        break;
+      }
+    }
+    if (out_idx) *out_idx = pick;
+    if (token_out) *token_out = pick;
+    if (pos_inout) *pos_inout += 1;
+    s_tok = pick;
+  }
+  if (emb_out) {
+    __syncthreads();
+    const long id = min(max(s_tok, 0), V - 1);
+    const uint4* src = (const uint4*)(table + (size_t)id * C);
+    for (int i = t; i < C / 8; i += 1024) ((uint4*)emb_out)[i] = src[i];
+  }
+}
+
 }  // namespace lga
 
 int lga::preload_sample() {
@@ -158,5 +323,22 @@ extern "C" int lga_argmax_f32(const float* logits, int n, int64_t* out_idx, int3
                               hipStream_t stream) {
   LGA_CHECK_ARG(logits && n > 0, "lga_argmax_f32: bad arguments");
   lga::argmax_f32_kernel<<<1, 1024, 0, stream>>>(logits, n, out_idx, token_out, pos_inout);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_sample_topk(const void* logits, int n, int top_k, float temperature, const float* uniform,
+                               unsigned long long seed, unsigned long long* counter, int64_t* out_idx,
+                               int32_t* token_out, int64_t* pos_inout, const void* table, int n_embd, int vocab,
+                               void* emb_out, int32_t* kept_out, void* probs_out, hipStream_t stream) {
+  LGA_CHECK_ARG(logits && n > 0 && n <= 1024 * 64, "lga_sample_topk: needs 0 < n <= 65536 logits");
+  LGA_CHECK_ARG(top_k >= 1 && top_k <= lga::kMaxTopK, "lga_sample_topk: top_k must be in [1, 1024]");
+  LGA_CHECK_ARG(temperature > 0.0f, "lga_sample_topk: temperature must be > 0 (0 is lga_argmax)");
+  LGA_CHECK_ARG(uniform || counter, "lga_sample_topk: needs a uniform or an RNG counter");
+  LGA_CHECK_ARG(!emb_out || (table && n_embd > 0 && n_embd % 8 == 0 && vocab > 0 && ((uintptr_t)table & 15) == 0 &&
+                             ((uintptr_t)emb_out & 15) == 0),
+                "lga_sample_topk: the embedding gather needs a 16-B aligned table and emb_out, n_embd % 8 == 0");
+  lga::topk_sample_kernel<<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, top_k, temperature, uniform, seed, counter,
+                                                  out_idx, token_out, pos_inout, (const uint16_t*)table, n_embd, vocab,
+                                                  (uint16_t*)emb_out, kept_out, (uint16_t*)probs_out);
   LGA_LAUNCH_RETURN();
 }

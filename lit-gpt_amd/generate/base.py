@@ -4,8 +4,11 @@ Same functions and semantics as /root/reference/generate/base.py: ``multinomial_
 ``sample`` (:30-41), ``next_token`` (:44-47), ``generate`` (:50-93: prefill at ``arange(T)``, then one-token
 steps at ``input_pos = T, T+1, ...``, stop on ``eos_id``, ``NotImplementedError`` when ``max_seq_length`` is too
 short) and ``main`` (:96-187) with the same flags and the same stderr timing line. Differences:
-  * greedy decoding (``temperature == 0``) runs each step as one HIP graph replay (lit_gpt/runtime.py) with the
-    argmax on the device — the role ``--compile`` (CUDA graphs) plays in the reference;
+  * greedy decoding (``temperature == 0``) and top-k sampling (``top_k`` <= 1024, the reference's default 200 at
+    temperature 0.8) run each step as one HIP graph replay (lit_gpt/runtime.py) with the argmax / the fused
+    top-k + softmax + inverse-CDF sampler on the device — the role ``--compile`` (CUDA graphs) plays in the
+    reference; the sampler's uniforms come from a counter-based RNG seeded from torch's generator, so a seed
+    reproduces a run but not the reference's exact torch.multinomial draws;
   * ``--quantize`` takes this build's formats (int4-g128, nf4 / bnb.nf4 / bnb.nf4-dq, bnb.fp4 / bnb.fp4-dq); without it the Linears
     stay bf16 ``nn.Linear`` (BASELINE config 2) and run on the bf16 GEMV / GEMM kernels;
   * ``--synthetic NAME`` builds a random-init model of a registered config (no checkpoint, no tokenizer): the
@@ -34,17 +37,39 @@ def multinomial_num_samples_1(probs: torch.Tensor) -> torch.Tensor:
     return torch.multinomial(probs, num_samples=1)
 
 
-def sample(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] = None) -> torch.Tensor:
-    """logits (1, T, V) on the GPU -> (1,) token. Greedy runs the HIP argmax (lowest index on ties; top-k
-    cannot change the arg-max); temperature > 0 follows the reference's top-k + softmax + multinomial."""
+class SamplerRNG:
+    """State of the fused sampler's counter-based RNG (csrc/sample.hip): a 64-bit seed drawn from torch's default
+    generator, so ``torch.manual_seed`` makes a run repeatable (generate/base.py:174), and a device counter the
+    kernel advances once per draw, so a captured decode step draws a fresh uniform at every replay."""
+
+    def __init__(self, device: torch.device, seed: Optional[int] = None) -> None:
+        self.seed = int(torch.randint(0, 2**62, (1,))) if seed is None else int(seed)
+        self.counter = torch.zeros(1, dtype=torch.int64, device=device)
+
+
+def device_sampling(temperature: float, top_k: Optional[int], dtype: torch.dtype) -> bool:
+    """Whether ``sample`` at this setting runs as the one-launch HIP sampler (ops.sample_topk): temperature > 0 with
+    top_k in [1, 1024] over bf16 logits — the reference's defaults (top_k 200, temperature 0.8) included."""
+    return temperature > 0.0 and top_k is not None and 1 <= top_k <= ops.MAX_TOP_K and dtype == torch.bfloat16
+
+
+def sample(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] = None,
+           rng: Optional[SamplerRNG] = None) -> torch.Tensor:
+    """logits (1, T, V) on the GPU -> (1,) token (generate/base.py:30-41). Greedy runs the HIP argmax (lowest index
+    on ties; top-k cannot change the arg-max); temperature > 0 with top_k <= 1024 over bf16 logits runs the HIP
+    top-k + softmax + inverse-CDF sampler in one launch (``rng`` carries its RNG state; a fresh one is drawn from
+    torch's generator when omitted); other settings follow the reference's torch ops, softmax in the logits' dtype."""
     logits = logits[0, -1]
     if not logits.is_cuda:
         raise RuntimeError("sample: logits must be on the GPU (this build has no CPU path)")
     if temperature > 0.0:
+        if device_sampling(temperature, top_k, logits.dtype):
+            rng = rng if rng is not None else SamplerRNG(logits.device)
+            return ops.sample_topk(logits.contiguous(), top_k, temperature, seed=rng.seed, counter=rng.counter)
         if top_k is not None:
             v, i = torch.topk(logits, min(top_k, logits.size(-1)))
             logits = torch.full_like(logits, float("-inf")).scatter_(-1, i, v)
-        probs = torch.nn.functional.softmax(logits.float() / temperature, dim=-1)
+        probs = torch.nn.functional.softmax(logits / temperature, dim=-1)
         return multinomial_num_samples_1(probs)
     return ops.argmax((logits if logits.dtype == torch.float32 else logits.to(torch.bfloat16)).contiguous())
 
@@ -52,6 +77,12 @@ def sample(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] 
 def next_token(model: GPT, input_pos: torch.Tensor, x: torch.Tensor, **kwargs: Any) -> torch.Tensor:
     logits = model(x, input_pos, last_token_only=True)
     return sample(logits, **kwargs).to(dtype=x.dtype)
+
+
+def graph_sampling(model: GPT, temperature: float, top_k: Optional[int]) -> bool:
+    """Whether decode steps at this setting run as captured HIP graphs (lit_gpt/runtime.py DecodeGraph): greedy, or
+    the device sampler (``device_sampling``) over the model's bf16 logits."""
+    return temperature == 0.0 or device_sampling(temperature, top_k, model.transformer.wte.weight.dtype)
 
 
 DECODE_CHUNK = 8  # greedy decode steps per graph launch (lit_gpt/runtime.py DecodeGraph.steps)
@@ -67,19 +98,21 @@ def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temp
         raise NotImplementedError(f"max_seq_length {model.max_seq_length} needs to be >= {max_returned_tokens - 1}")
     device = prompt.device
     tokens = [prompt]
+    rng = SamplerRNG(device) if temperature > 0.0 else None
     token = next_token(model, torch.arange(0, T, device=device), prompt.view(1, -1), temperature=temperature,
-                       top_k=top_k).clone()
+                       top_k=top_k, rng=rng).clone()
     tokens.append(token)
     n_steps = max_returned_tokens - T - 1
     if n_steps <= 0:
         return torch.cat(tokens)
-    if temperature == 0.0 and use_graph:
+    if use_graph and graph_sampling(model, temperature, top_k):
         from lit_gpt.runtime import DecodeGraph
 
         # (the prefill's token is never tested against eos: the reference's loop only tests the decoded ones,
         # generate/base.py:86-92)
         # runs the first decode step eagerly, then captures the step (and DECODE_CHUNK steps as one graph)
-        dg = DecodeGraph(model, token, T, chunk=DECODE_CHUNK if n_steps > DECODE_CHUNK else 1)
+        dg = DecodeGraph(model, token, T, chunk=DECODE_CHUNK if n_steps > DECODE_CHUNK else 1,
+                         temperature=temperature, top_k=top_k, rng=rng)
         out = torch.empty(n_steps, dtype=prompt.dtype, device=device)
         out[0] = dg.token.view(-1)[0]
         produced = 1
@@ -104,7 +137,8 @@ def generate(model: GPT, prompt: torch.Tensor, max_returned_tokens: int, *, temp
         return torch.cat(tokens)
     input_pos = torch.tensor([T], device=device)
     for _ in range(n_steps):
-        token = next_token(model, input_pos, token.view(1, -1), temperature=temperature, top_k=top_k).clone()
+        token = next_token(model, input_pos, token.view(1, -1), temperature=temperature, top_k=top_k,
+                           rng=rng).clone()
         tokens.append(token)
         if eos_id is not None and int(token) == eos_id:
             break

@@ -89,6 +89,7 @@ SIGNATURES = {
     "lga_f32_rope_kv_append": [_P, _P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _I, _P],
     "lga_f32_attention": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _F, _P],
     "lga_argmax_f32": [_P, _I, _P, _P, _P, _P],
+    "lga_sample_topk": [_P, _I, _I, _F, _P, ctypes.c_ulonglong, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P],
     "lga_q4_gemv_allreduce": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P, _P,
                               _P],
 }
@@ -528,6 +529,34 @@ def argmax_embed(logits, table, emb_out, out_idx=None, token_out=None, pos_inout
                                            _opt(token_out, "token_out", torch.int32),
                                            _opt(pos_inout, "pos_inout", torch.int64), _dev(table, "table", torch.bfloat16),
                                            C, V, _dev(emb_out, "emb_out", torch.bfloat16), _stream()))
+    return idx
+
+
+MAX_TOP_K = 1024  # lga_sample_topk keeps at most this many logits
+
+
+def sample_topk(logits, top_k, temperature, *, uniform=None, seed=0, counter=None, out_idx=None, token_out=None,
+                pos_inout=None, table=None, emb_out=None, kept_out=None, probs_out=None):
+    """generate/base.py:30-41 at temperature > 0 with top_k (1..1024) in ONE launch (csrc/sample.hip
+    topk_sample_kernel): top-k (ties lowest index first), softmax(logits / temperature) in bf16, inverse-CDF draw.
+    ``uniform`` (1,) fp32 on the device fixes the draw (tests); otherwise ``counter`` (1,) int64 on the device is the
+    RNG state (hash of ``seed`` and the counter; advanced per call, so the launch replays in a HIP graph). With
+    ``table``/``emb_out`` the chosen token's embedding row is gathered as ``argmax_embed`` does. Returns out_idx."""
+    n = logits.numel()
+    if not 1 <= top_k <= MAX_TOP_K:
+        raise ValueError(f"sample_topk: top_k must be in [1, {MAX_TOP_K}], got {top_k}")
+    if uniform is None and counter is None:
+        raise ValueError("sample_topk: needs uniform or an RNG counter")
+    idx = out_idx if out_idx is not None else torch.empty(1, dtype=torch.int64, device=logits.device)
+    V, C = (table.shape if table is not None else (0, 0))
+    if emb_out is not None and (table is None or emb_out.numel() != C):
+        raise ValueError("sample_topk: emb_out needs the embedding table and one row of it")
+    _check(load_library().lga_sample_topk(
+        _dev(logits, "logits", torch.bfloat16), n, int(top_k), float(temperature), _opt(uniform, "uniform", torch.float32),
+        int(seed) & (2**64 - 1), _opt(counter, "counter", torch.int64), _dev(idx, "out_idx", torch.int64),
+        _opt(token_out, "token_out", torch.int32), _opt(pos_inout, "pos_inout", torch.int64),
+        _opt(table, "table", torch.bfloat16), C, V, _opt(emb_out, "emb_out", torch.bfloat16),
+        _opt(kept_out, "kept_out", torch.int32), _opt(probs_out, "probs_out", torch.bfloat16), _stream()))
     return idx
 
 

@@ -1,4 +1,4 @@
-"""Decode-step executor: one HIP graph per greedy decode step.
+"""Decode-step executor: one HIP graph per decode step (greedy, or top-k sampling at temperature > 0).
 
 The reference gets launch-overhead relief from ``torch.compile(next_token, mode="reduce-overhead")``
 (generate/base.py:161-166), i.e. CUDA graphs over Inductor/Triton kernels. Here the step is already a short
@@ -19,14 +19,19 @@ import torch
 from lit_gpt import ops
 
 class DecodeGraph:
-    def __init__(self, model, first_token: torch.Tensor, first_pos: int, chunk: int = 1) -> None:
+    def __init__(self, model, first_token: torch.Tensor, first_pos: int, chunk: int = 1, *,
+                 temperature: float = 0.0, top_k: Optional[int] = None, rng=None) -> None:
         """Runs one real decode step eagerly (token ``first_token`` at position ``first_pos``) to warm up, then
         captures the step. Afterwards ``self.token`` holds the newest token and ``self.pos`` its position.
         ``chunk`` > 1 also captures ``chunk`` consecutive steps as one graph (``steps()``): the argmax of step i
         writes its token into ``self.history[i]`` as well, and one launch replaces ``chunk`` (≈9 us of
-        graph-launch gap per step on MI355X, profiles/r02b_*)."""
+        graph-launch gap per step on MI355X, profiles/r02b_*). ``temperature`` > 0 replaces the argmax with the
+        fused top-k sampler (ops.sample_topk, ``top_k`` 1..1024, RNG state ``rng``: generate.base.SamplerRNG)."""
         dev = first_token.device
         self.model = model
+        self.temperature, self.top_k, self.rng = float(temperature), top_k, rng
+        if self.temperature > 0.0 and (rng is None or top_k is None or not 1 <= top_k <= ops.MAX_TOP_K):
+            raise ValueError("DecodeGraph: sampling needs top_k in [1, 1024] and an rng (generate.base.SamplerRNG)")
         self.token = first_token.reshape(1, 1).to(torch.int32).clone()
         self.pos = torch.tensor([first_pos], dtype=torch.int64, device=dev)
         self.chunk = max(1, int(chunk))
@@ -53,13 +58,19 @@ class DecodeGraph:
             self.chunk_graph = gc
 
     def _step_body(self, idx_out: Optional[torch.Tensor] = None, embedded: bool = True) -> None:
-        if not self.fuse_embedding:
-            logits = self.model(self.token, self.pos, last_token_only=True)
-            ops.argmax(logits.reshape(-1), out_idx=idx_out, token_out=self.token.view(-1), pos_inout=self.pos)
-            return
-        logits = self.model(self.token, self.pos, last_token_only=True, embedded=self.x_emb if embedded else None)
-        ops.argmax_embed(logits.reshape(-1), self.model.transformer.wte.weight, self.x_emb, out_idx=idx_out,
-                         token_out=self.token.view(-1), pos_inout=self.pos)
+        fuse = self.fuse_embedding
+        logits = self.model(self.token, self.pos, last_token_only=True,
+                            embedded=self.x_emb if (fuse and embedded) else None).reshape(-1)
+        table = self.model.transformer.wte.weight if fuse else None
+        if self.temperature > 0.0:
+            ops.sample_topk(logits, self.top_k, self.temperature, seed=self.rng.seed, counter=self.rng.counter,
+                            out_idx=idx_out, token_out=self.token.view(-1), pos_inout=self.pos, table=table,
+                            emb_out=self.x_emb)
+        elif fuse:
+            ops.argmax_embed(logits, table, self.x_emb, out_idx=idx_out, token_out=self.token.view(-1),
+                             pos_inout=self.pos)
+        else:
+            ops.argmax(logits, out_idx=idx_out, token_out=self.token.view(-1), pos_inout=self.pos)
 
     def _step_eager(self) -> None:
         self._step_body(embedded=False)  # embeds first_token itself; its argmax leaves x_emb for the graphs

@@ -265,6 +265,34 @@ def sample(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] 
     return torch.argmax(logits, dim=-1, keepdim=True)
 
 
+def inverse_cdf(probs: np.ndarray, u: float) -> int:
+    """torch.multinomial(probs, 1) on the CPU given its uniform draw u (generate/base.py:27, 40): the fp32 running sum
+    in index order, divided by its total, and the first index whose value reaches u (ATen's CPU multinomial
+    cumulative distribution + binary search). The specification of lga_sample_topk's draw."""
+    cum = np.cumsum(np.asarray(probs, dtype=np.float32), dtype=np.float32)
+    cdf = (cum / cum[-1]).astype(np.float32)
+    return int(np.searchsorted(cdf, np.float32(u), side="left"))
+
+
+def sample_topk_spec(logits_bf16: torch.Tensor, top_k: int, temperature: float, u: float):
+    """generate/base.py:30-41 (top_k, temperature > 0) on 1-D bf16 logits, stated as lga_sample_topk computes it:
+    the kept set is torch.topk's (ties at the k-th value kept lowest index first), probabilities are the bf16
+    softmax of bf16(v / temperature) over the kept set, the token is inverse_cdf of those probabilities.
+    Returns (kept indices in index order, their probabilities (fp32 holding bf16 values), token)."""
+    x = logits_bf16.float()
+    n = x.numel()
+    k = min(top_k, n)
+    xs = x.tolist()
+    # NaN above everything, then value descending (-0 == +0), then index ascending
+    order = sorted(range(n), key=lambda i: (not math.isnan(xs[i]), -xs[i] if not math.isnan(xs[i]) else 0.0, i))
+    kept = sorted(order[:k])
+    v = (x[kept] / temperature).to(torch.bfloat16).float()
+    e = torch.exp(v - v.max())
+    p = (e / e.sum()).to(torch.bfloat16).float()
+    j = inverse_cdf(p.numpy(), u)
+    return kept, p, kept[j]
+
+
 def generate(model: OracleGPT, prompt: torch.Tensor, max_returned_tokens: int, *, temperature: float = 1.0,
              top_k: Optional[int] = None, eos_id: Optional[int] = None,
              multinomial=None, record_logits: Optional[list] = None) -> torch.Tensor:
