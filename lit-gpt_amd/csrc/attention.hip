@@ -16,6 +16,7 @@
 // the workgroup that arrives last merges the splits and writes the bf16 output (flash-decoding combine inside
 // the same launch; MI355X_MICROARCH.md "Valid forms" row 1), then re-arms the counter for the next launch.
 #include <cstdlib>
+#include <type_traits>
 
 #include "decode_ops.h"
 
@@ -400,7 +401,11 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(const uint16_t* __
   // the whole byte offset rides in voffset: the buffer range check covers voffset only (soffset is added after
   // it), so rows past max_seq — the last partial tile and the one-tile-ahead prefetch — read as zeros instead of
   // past the group's cache
+#ifndef LGA_FA_EXP
+#define LGA_FA_EXP 0  // lab only (tools/prefill_attn_bench.py): 1 no tile math, 2 no global loads, 3 neither
+#endif
   auto gload = [&](int k0) {
+    if (LGA_FA_EXP & 2) return;
 #pragma unroll
     for (int i = 0; i < LPT; ++i) {
       const int off = gvoff + (k0 + RPI * i) * HS * 2;
@@ -437,6 +442,7 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(const uint16_t* __
   const float sl2 = scale * 1.4426950408889634f;
 
   auto tile = [&](const unsigned char* K, const unsigned char* V, int k0) {
+    if (LGA_FA_EXP & 1) return;
     // S^T of the two 32-key halves as two interleaved accumulation chains
     f32x16_t sacc[2];
 #pragma unroll
@@ -542,6 +548,297 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(const uint16_t* __
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Prefill, paired form (default): one 512-thread workgroup per (head, block pair) holds query blocks hi = nblk-1-p
+// (waves 0-3) and lo = p (waves 4-7) of 128 rows and streams the head's K / V ONCE for both — key tile t serves
+// every wave whose rows reach it (26 % fewer L2 -> LDS bytes than a workgroup per block at T = 2048, and every SIMD
+// holds one hi and one lo wave: 2 (nblk + 1) key tiles per SIMD whatever p). K / V tiles reach LDS by LDS-DMA
+// (`buffer_load_dwordx4 ... lds`, range-checked: rows past the cache land as zeros) into a 4-stage ring, three tiles
+// ahead of the math, with no staging registers; a raw s_barrier per tile after a counted vmcnt. The LDS reads are
+// inline asm with counted lgkmcnt waits (hipcc would wait for every DMA in flight before a compiler-visible LDS
+// read, not telling the stages apart). Per wave the arithmetic is attn_prefill_kernel's, op for op.
+template <int HS>
+__global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_t* __restrict__ q,
+                                                                   const uint16_t* __restrict__ kc,
+                                                                   const uint16_t* __restrict__ vc,
+                                                                   const int64_t* __restrict__ input_pos,
+                                                                   uint16_t* __restrict__ y, int T, int n_head, int G,
+                                                                   int max_seq, float scale) {
+  constexpr int KT = 64;           // keys per tile
+  constexpr int CH = HS / 8;       // 16-B chunks per key row
+  constexpr int DK = HS / 16;      // 32x32x16 k-steps over the head dim (S^T)
+  constexpr int DT = HS / 32;      // 32-row tiles of O^T
+  constexpr int TB = KT * HS * 2;  // bytes of one K or V tile image
+  constexpr int NS = 4;            // ring stages
+  constexpr int PIECES = 2 * TB / 1024 / 8;  // 1-KB DMA pieces per wave per tile (K and V)
+  static_assert(PIECES * 8 * 1024 == 2 * TB, "pieces");
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[NS][2][TB];  // [stage][K | V]
+  __shared__ int s_pos[2][8];
+
+  const int tid = threadIdx.x, lane = tid & 63, hh = lane >> 5, lq = lane & 31;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int nblk = (T + 127) / 128;
+  const int head = blockIdx.x % n_head, pr = blockIdx.x / n_head, g = head / (n_head / G);
+  const int hi = nblk - 1 - pr, lo = pr;
+  const int blk = wave < 4 ? hi : (lo < hi ? lo : -1);  // odd nblk: the middle block has no partner
+  const int q0 = blk * 128 + (wave & 3) * 32;
+  const int t = q0 + lq;
+  const bool valid = blk >= 0 && t < T;
+  const int mypos = valid ? (int)input_pos[t] : -1;
+  {
+    int mx = mypos, mn = valid ? mypos : INT_MAX;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      mx = max(mx, __shfl_xor(mx, o));
+      mn = min(mn, __shfl_xor(mn, o));
+    }
+    if (lane == 0) {
+      s_pos[0][wave] = mx;
+      s_pos[1][wave] = mn;
+    }
+  }
+  bf16x8_t qb[DK];  // Q^T fragments (B operand): lane l holds Q[t][ks*16 + 8*hh .. +8]
+  {
+    const uint16_t* qr = q + ((size_t)min(max(t, 0), T - 1) * n_head + head) * HS + 8 * hh;
+#pragma unroll
+    for (int ks = 0; ks < DK; ++ks) qb[ks] = *(const bf16x8_t*)(qr + ks * 16);
+  }
+  // the Q fragments and positions are in before any DMA is counted; redefining them through an asm tells hipcc so
+  // (it would otherwise wait for "their" loads — i.e. for every DMA in flight — at each use inside the loop)
+#pragma unroll
+  for (int ks = 0; ks < DK; ++ks) asm volatile("" : "+v"(qb[ks]));
+  int mpos = mypos;
+  asm volatile("" : "+v"(mpos));
+  __syncthreads();
+  const int wmax = s_pos[0][wave], wmin = s_pos[1][wave];
+  int bmax = s_pos[0][0];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) bmax = max(bmax, s_pos[0][w]);
+  bmax = min(bmax, max_seq - 1);
+  const int ntiles = (bmax + 1 + KT - 1) / KT;
+
+  // DMA: wave w moves pieces w * PIECES .. +PIECES of the tile (K pieces first, then V); lane L of a piece lands at
+  // +16 L = row r0 + L / CH, physical chunk L % CH, so it fetches logical chunk (L % CH) ^ sw(row) (kv_off's swizzle)
+  const __amdgpu_buffer_rsrc_t krs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(kc + (size_t)g * max_seq * HS), (short)0, max_seq * HS * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(vc + (size_t)g * max_seq * HS), (short)0, max_seq * HS * 2, 0x00020000);
+  constexpr int RPP = 1024 / (HS * 2);  // key rows per piece
+  int dvoff[PIECES];
+#pragma unroll
+  for (int i = 0; i < PIECES; ++i) {
+    const int piece = (wave * PIECES + i) % (TB / 1024);
+    const int r = piece * RPP + lane / CH;
+    const int phys = lane % CH;
+    const int sw = CH == 16 ? (((r & 3) << 2) | ((r >> 2) & 3)) : (((r & 3) << 1) | ((r >> 2) & 1));
+    dvoff[i] = (r * HS + (phys ^ sw) * 8) * 2;
+  }
+  auto issue = [&](int tt) {  // tile tt into stage tt % NS (every wave, every tile: the vmcnt counts stay uniform)
+    unsigned char* st = &lds[tt % NS][0][0];
+    const int kb = tt * KT * HS * 2;
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const int gp = wave * PIECES + i;
+      const bool isv = gp >= TB / 1024;
+      unsigned char* dst = st + (isv ? TB : 0) + (gp % (TB / 1024)) * 1024;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(isv ? vrs : krs, (__attribute__((address_space(3))) void*)dst, 16,
+                                               kb + dvoff[i], 0, 0, 0);
+    }
+  };
+
+  // LDS read addresses: K row lq (+ 32 st), chunk 2 ks + hh; V^T transposed reads (16-lane group grp, quad qq, pair pp)
+  const unsigned lbase = (unsigned)(uintptr_t)&lds[0][0][0];
+  unsigned koff[DK];
+#pragma unroll
+  for (int ks = 0; ks < DK; ++ks) koff[ks] = lbase + kv_off<HS>(lq, 2 * ks + hh);
+  const int gi = lane & 15, qq = gi >> 2, pp = gi & 3, grp = lane >> 4;
+  unsigned voff0[DT], voff1[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) {
+    const int ch = ((dt * 32 + 16 * (grp & 1)) >> 3) + (pp >> 1);
+    voff0[dt] = lbase + TB + kv_off<HS>(8 * (grp >> 1) + qq, ch) + 8 * (pp & 1);
+    voff1[dt] = lbase + TB + kv_off<HS>(8 * (grp >> 1) + 4 + qq, ch) + 8 * (pp & 1);
+  }
+
+  f32x16_t o[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.0f;
+  float m = -INFINITY, l = 0.0f;
+  const float sl2 = scale * 1.4426950408889634f;
+
+  typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));
+  // K fragments of batch b (2 k-steps x 2 halves) of the stage at byte offset sb
+  auto kread = [&](unsigned sb, int b, u32x4_t (&f)[4]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ks = 2 * b + (j >> 1), st = j & 1;
+      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[j]) : "v"(koff[ks] + sb), "i"(st * 32 * HS * 2) : "memory");
+    }
+  };
+  auto kmfma = [&](int b, const u32x4_t (&f)[4], f32x16_t (&acc)[2]) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int ks = 2 * b + (j >> 1), st = j & 1;
+      acc[st] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, f[j]), qb[ks], acc[st], 0, 0, 0);
+    }
+  };
+  auto vread = [&](unsigned sb, int kk, u32x2_t (&f)[DT][2]) {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f[dt][0]) : "v"(voff0[dt] + sb), "i"(kk * 16 * HS * 2) : "memory");
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f[dt][1]) : "v"(voff1[dt] + sb), "i"(kk * 16 * HS * 2) : "memory");
+    }
+  };
+  // tie the fragments to a counted wait so no use moves above it
+#define LGA_KW(N, f) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(f[0]), "+v"(f[1]), "+v"(f[2]), "+v"(f[3]))
+#define LGA_VW4(N, f)                                                                                             \
+  asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(f[0][0]), "+v"(f[0][1]), "+v"(f[1][0]), "+v"(f[1][1]), "+v"(f[2][0]), \
+               "+v"(f[2][1]), "+v"(f[3][0]), "+v"(f[3][1]))
+#define LGA_VW2(N, f) asm volatile("s_waitcnt lgkmcnt(" #N ")" : "+v"(f[0][0]), "+v"(f[0][1]), "+v"(f[1][0]), "+v"(f[1][1]))
+
+  // S^T = K . Q^T of the tile at sb: 16 K fragments in 4 batches of 4, one batch read ahead
+  auto s_tile = [&](unsigned sb, f32x16_t (&sacc)[2]) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sacc[st][r] = 0.0f;
+    u32x4_t kf[2][4];
+    kread(sb, 0, kf[0]);
+#pragma unroll
+    for (int b = 0; b < DK / 2; ++b) {
+      if (b + 1 < DK / 2) {
+        kread(sb, b + 1, kf[(b + 1) & 1]);
+        LGA_KW(4, kf[b & 1]);
+      } else {
+        LGA_KW(0, kf[b & 1]);
+      }
+      kmfma(b, kf[b & 1], sacc);
+    }
+  };
+  // the online softmax of S(t) (sacc) and O += P . V(t) from the stage at sbv
+  auto pv_tile = [&](unsigned sbv, int k0, f32x16_t (&sacc)[2]) {
+    u32x2_t vf[2][DT][2];
+    vread(sbv, 0, vf[0]);
+    if (__builtin_amdgcn_readfirstlane(k0 + KT - 1 > wmin)) {  // a row of this wave ends inside the tile
+#pragma unroll
+      for (int st = 0; st < 2; ++st)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (k0 + st * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh > mpos) sacc[st][r] = -INFINITY;
+    }
+    float tmax = -INFINITY;
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) tmax = fmaxf(tmax, sacc[st][r]);
+    {
+      const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(tmax), __float_as_uint(tmax), false, false);
+      tmax = fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
+    }
+    const float mnew = fmaxf(m, tmax * sl2);
+    const float mref = mnew == -INFINITY ? 0.0f : mnew;
+    if (!__all(mnew == m)) {
+      const float c = __builtin_amdgcn_exp2f(m - mref);
+      l *= c;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] *= c;
+    }
+    m = mnew;
+    float rs = 0.0f;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      const int st = kk >> 1, r0 = 8 * (kk & 1);
+      if (kk + 1 < 4) vread(sbv, kk + 1, vf[(kk + 1) & 1]);
+      float x[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        x[e] = __builtin_amdgcn_exp2f(__builtin_fmaf(sacc[st][r0 + e], sl2, -mref));
+        rs += x[e];
+      }
+      const uint32_t w0 = pack2(x[0], x[1]), w1 = pack2(x[2], x[3]);
+      const uint32_t w2 = pack2(x[4], x[5]), w3 = pack2(x[6], x[7]);
+      const auto a = __builtin_amdgcn_permlane32_swap(w0, w2, false, false);
+      const auto b = __builtin_amdgcn_permlane32_swap(w1, w3, false, false);
+      const u32x4_t f = {a[0], b[0], a[1], b[1]};
+      const bf16x8_t pb = __builtin_bit_cast(bf16x8_t, f);
+      auto& cur = vf[kk & 1];
+      if (kk + 1 < 4) {  // V(kk+1)'s 2 DT reads are newer than V(kk)
+        if constexpr (DT == 4) LGA_VW4(8, cur); else LGA_VW2(4, cur);
+      } else {
+        if constexpr (DT == 4) LGA_VW4(0, cur); else LGA_VW2(0, cur);
+      }
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt) {
+        const u32x4_t vv = {cur[dt][0][0], cur[dt][0][1], cur[dt][1][0], cur[dt][1][1]};
+        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, vv), pb, o[dt], 0, 0, 0);
+      }
+    }
+    l += rs;
+  };
+
+#ifndef LGA_FA_LAG
+#define LGA_FA_LAG 1
+#endif
+  // Ring: tiles in flight ahead of the math, then per tile: wait for it (the tiles issued after it may stay in
+  // flight), barrier (every wave's pieces landed; every wave done with the stage the next issue overwrites), issue,
+  // math. LAG: the lo waves run half a tile behind — at iteration t they finish tile t-1 (softmax + P.V) and then
+  // compute S(t) — so the two waves of a SIMD are in opposite phases (one on S's MFMAs while the other is in the
+  // exponential-heavy softmax) instead of in lock step after every barrier. Each wave keeps one S tile in registers
+  // across the barrier; stages t-1 and t are both live, so the issue runs NS-2 tiles ahead instead of NS-1.
+  constexpr int AHEAD = LGA_FA_LAG ? NS - 2 : NS - 1;
+  const bool lag = LGA_FA_LAG && wave >= 4;
+#pragma unroll
+  for (int i = 0; i < AHEAD; ++i)
+    if (i < ntiles) issue(i);
+  // two separate loops (the waves' roles are fixed), so each keeps its own register allocation
+  auto run = [&](auto lag_c) {
+    constexpr bool LAG = decltype(lag_c)::value;
+    f32x16_t sacc[2];
+    const int iters = ntiles + (LGA_FA_LAG ? 1 : 0);
+    for (int tt = 0; tt < iters; ++tt) {
+      const int after = min(AHEAD - 1, ntiles - 1 - tt);  // tiles issued after tt (negative past the last tile)
+      if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (tt + AHEAD < ntiles) issue(tt + AHEAD);
+      const int k0 = tt * KT;
+      const unsigned sb = (unsigned)((tt % NS) * 2 * TB);
+      if constexpr (LAG) {
+        if (tt >= 1 && k0 - KT <= wmax) pv_tile((unsigned)(((tt - 1) % NS) * 2 * TB), k0 - KT, sacc);
+        __builtin_amdgcn_sched_barrier(0);  // keep S(t) out of tile t-1's register lifetime
+        if (tt < ntiles && k0 <= wmax) s_tile(sb, sacc);
+      } else {
+        if (tt < ntiles && k0 <= wmax) {
+          s_tile(sb, sacc);
+          pv_tile(sb, k0, sacc);
+        }
+      }
+    }
+  };
+  if (lag) run(std::true_type{});
+  else run(std::false_type{});
+#undef LGA_KW
+#undef LGA_VW4
+#undef LGA_VW2
+  l += __shfl_xor(l, 32);
+  if (valid) {
+    const float inv = 1.0f / l;
+    uint16_t* yr = y + ((size_t)t * n_head + head) * HS;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const int d = dt * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        *(uint32_t*)(yr + d) = pack2(o[dt][r] * inv, o[dt][r + 1] * inv);
+      }
+  }
+}
+
 // (keys in flight per row group, waves per workgroup) by q_per_kv; -D overrides are for tools/attn_sweep.py
 #ifndef LGA_ATTN_Q1
 #define LGA_ATTN_Q1 4, 4
@@ -590,7 +887,8 @@ static int launch_hs(const void* q, void* kc, void* vc, const int64_t* pos, void
 }  // namespace lga
 
 int lga::preload_attention() {
-  return lga::preload(lga::attn_prefill_kernel<128>) + lga::preload(lga::attn_prefill_kernel<64>);
+  return lga::preload(lga::attn_prefill_kernel<128>) + lga::preload(lga::attn_prefill_kernel<64>) +
+         lga::preload(lga::attn_prefill_pair_kernel<128>) + lga::preload(lga::attn_prefill_pair_kernel<64>);
 }
 
 extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_cache, const int64_t* input_pos,
@@ -601,6 +899,21 @@ extern "C" int lga_attention(const void* q, const void* k_cache, const void* v_c
   LGA_CHECK_ARG(n_splits >= 1 && n_splits <= 256, "lga_attention: n_splits must be in [1, 256]");
   LGA_CHECK_ARG(n_splits == 1 || (workspace && counters), "lga_attention: split attention needs workspace + counters");
   if (T >= 16 && n_splits == 1 && (head_size == 128 || head_size == 64)) {  // prefill: flash attention on MFMA
+#ifndef LGA_FA_PAIR
+#define LGA_FA_PAIR 1
+#endif
+    if (LGA_FA_PAIR) {
+      const dim3 grid((((T + 127) / 128 + 1) / 2) * n_head);
+      if (head_size == 128)
+        lga::attn_prefill_pair_kernel<128><<<grid, 512, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+                                                                     (const uint16_t*)v_cache, input_pos, (uint16_t*)y,
+                                                                     T, n_head, n_query_groups, max_seq, scale);
+      else
+        lga::attn_prefill_pair_kernel<64><<<grid, 512, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,
+                                                                    (const uint16_t*)v_cache, input_pos, (uint16_t*)y,
+                                                                    T, n_head, n_query_groups, max_seq, scale);
+      LGA_LAUNCH_RETURN();
+    }
     const dim3 grid(((T + 127) / 128) * n_head);
     if (head_size == 128)
       lga::attn_prefill_kernel<128><<<grid, 256, 0, stream>>>((const uint16_t*)q, (const uint16_t*)k_cache,

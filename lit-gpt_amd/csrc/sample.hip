@@ -150,86 +150,151 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {  // 
 
 constexpr int kMaxTopK = 1024;
 
+__device__ __forceinline__ unsigned wave_max_u(unsigned v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, o));
+  return v;
+}
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned v, int lane) {
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned u = (unsigned)__shfl_up((int)v, o);
+    if (lane >= o) v += u;
+  }
+  return v;
+}
+
+// One workgroup of 1024 threads; thread t owns logits [t EPT, t EPT + EPT) (index order = thread order, so every
+// "in index order" below is a block prefix sum). The logits are staged once in LDS (coalesced), padded with -inf
+// (pads sit after every real index, so a tie rule that takes the lowest indices never reaches them: k <= n).
+template <int EPT>
 __global__ void __launch_bounds__(1024) topk_sample_kernel(
     const uint16_t* __restrict__ logits, int n, int k, float temperature, const float* __restrict__ uniform,
     unsigned long long seed, unsigned long long* __restrict__ counter, int64_t* __restrict__ out_idx,
     int32_t* __restrict__ token_out, int64_t* __restrict__ pos_inout, const uint16_t* __restrict__ table, int C,
     int V, uint16_t* __restrict__ emb_out, int32_t* __restrict__ kept_out, uint16_t* __restrict__ probs_out) {
-  __shared__ unsigned hist[256];
-  __shared__ unsigned scan[1024];
+  constexpr int NT = 1024, NW = 16;
+  static_assert(EPT % 8 == 0, "16-B LDS reads");
+  __shared__ __attribute__((aligned(16))) uint16_t sx[NT * EPT];
+  __shared__ __attribute__((aligned(16))) float kval[kMaxTopK];
+  __shared__ __attribute__((aligned(16))) float kcum[kMaxTopK];
   __shared__ int kidx[kMaxTopK];
-  __shared__ float kval[kMaxTopK];
-  __shared__ float red[16];
-  __shared__ unsigned s_b1, s_above, s_key, s_gt;
+  __shared__ unsigned hist[256];
+  __shared__ unsigned wsum[NW];
+  __shared__ float red[NW];
+  __shared__ unsigned s_kmax, s_sel, s_before, s_found;
+  __shared__ float s_tot, s_u;
   __shared__ int s_tok;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   k = min(k, n);
-  const int ept = (n + 1023) / 1024, i0 = min(t * ept, n), i1 = min(i0 + ept, n);
-  // ---- radix select of the k-th largest key: high byte, then low byte ----
-  if (t < 256) hist[t] = 0;
+  for (int i = t; i < NT * EPT; i += NT) sx[i] = i < n ? logits[i] : (uint16_t)0xFF80u;  // -inf pads
+  if (t == 0) s_found = 0;
   __syncthreads();
-  for (int i = i0; i < i1; ++i) atomicAdd(&hist[order_key(logits[i]) >> 8], 1u);
-  __syncthreads();
-  if (t == 0) {
-    unsigned c = 0, b = 255;
-    for (;; --b) {
-      if (c + hist[b] >= (unsigned)k || b == 0) break;
-      c += hist[b];
+  // this thread's order keys, two 16-bit keys per register (element 2j low, 2j+1 high); at 64 per thread they
+  // would not fit beside the rest (1024 threads: 128 VGPRs), so that form reads them from the LDS copy instead
+  constexpr bool REG = EPT <= 32;
+  uint32_t key2[REG ? EPT / 2 : 1];
+  if constexpr (REG) {
+    const uint4* src = (const uint4*)(sx + t * EPT);
+#pragma unroll
+    for (int c = 0; c < EPT / 8; ++c) {
+      const uint4 v = src[c];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int h = 0; h < 4; ++h)
+        key2[4 * c + h] = order_key((uint16_t)(w[h] & 0xFFFFu)) | (order_key((uint16_t)(w[h] >> 16)) << 16);
     }
-    s_b1 = b;
-    s_above = c;
   }
-  __syncthreads();
-  if (t < 256) hist[t] = 0;
-  __syncthreads();
-  const unsigned b1 = s_b1;
-  for (int i = i0; i < i1; ++i) {
-    const unsigned key = order_key(logits[i]);
-    if ((key >> 8) == b1) atomicAdd(&hist[key & 255u], 1u);
-  }
-  __syncthreads();
-  if (t == 0) {
-    unsigned c = s_above, b = 255;
-    for (;; --b) {
-      if (c + hist[b] >= (unsigned)k || b == 0) break;
-      c += hist[b];
-    }
-    s_key = (b1 << 8) | b;
-    s_gt = c;  // keys strictly above the k-th
-  }
-  __syncthreads();
-  // ---- the kept set in index order: every key above the k-th, then ties lowest index first ----
-  const unsigned kth = s_key, need = (unsigned)k - s_gt;
-  unsigned ties = 0, above = 0;
-  for (int i = i0; i < i1; ++i) {
-    const unsigned key = order_key(logits[i]);
-    ties += key == kth;
-    above += key > kth;
-  }
-  auto block_scan = [&](unsigned v) -> unsigned {  // exclusive prefix over threads in index order
-    scan[t] = v;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {
-      const unsigned o = t >= off ? scan[t - off] : 0u;
-      __syncthreads();
-      scan[t] += o;
-      __syncthreads();
-    }
-    const unsigned incl = scan[t];
-    __syncthreads();
-    return incl - v;
+  auto key = [&](int e) -> unsigned {
+    if constexpr (REG) return (key2[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
+    else return order_key(sx[t * EPT + e]);
   };
-  const unsigned tie_before = block_scan(ties);
-  unsigned pos = block_scan(above + min(ties, need > tie_before ? need - tie_before : 0u));
+  // exclusive prefix over the 1024 threads in index order
+  auto block_excl = [&](unsigned v) -> unsigned {
+    const unsigned inc = wave_incl_scan(v, lane);
+    if (lane == 63) wsum[wave] = inc;
+    __syncthreads();
+    unsigned base = 0;
+    for (int w = 0; w < wave; ++w) base += wsum[w];
+    __syncthreads();
+    return base + inc - v;
+  };
+  // one selection pass: a 256-bin histogram of digit d (d ascending = key descending) over the keys `digit` maps
+  // into [0, 256), then the bin where the running count from d = 0 first reaches `need` (s_sel) and the count
+  // before it (s_before); s_found stays 0 when the binned keys number fewer than `need`
+  auto select = [&](auto digit, unsigned need) {
+    if (t < 256) hist[t] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const unsigned d = digit(key(e));
+      if (d < 256u) atomicAdd(&hist[d], 1u);
+    }
+    __syncthreads();
+    const unsigned c = t < 256 ? hist[t] : 0u;
+    const unsigned inc = wave_incl_scan(c, lane);
+    if (lane == 63 && wave < 4) wsum[wave] = inc;
+    __syncthreads();
+    if (t < 256) {
+      unsigned pre = inc;
+      for (int w = 0; w < wave; ++w) pre += wsum[w];
+      if (pre >= need && pre - c < need) {
+        s_sel = t;
+        s_before = pre - c;
+        s_found = 1;
+      }
+    }
+    __syncthreads();
+  };
+  // ---- the k-th largest key. First the 256 keys just below the maximum (one pass, atomics only for the keys near
+  // the top: logits are dense around their mean, and the top-k of a vocabulary usually sits within two binades of
+  // the max); otherwise an MSD radix select on the high byte, then the low byte. ----
+  {
+    unsigned m = 0;
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) m = max(m, key(e));
+    m = wave_max_u(m);
+    if (lane == 0) wsum[wave] = m;
+    __syncthreads();
+    if (t == 0) {
+      unsigned mm = 0;
+      for (int w = 0; w < NW; ++w) mm = max(mm, wsum[w]);
+      s_kmax = mm;
+    }
+    __syncthreads();
+  }
+  const unsigned kmax = s_kmax;
+  unsigned kth, gt;
+  select([&](unsigned kk) { return kmax - kk; }, (unsigned)k);
+  if (s_found) {
+    kth = kmax - s_sel;
+    gt = s_before;
+  } else {
+    select([&](unsigned kk) { return 255u - (kk >> 8); }, (unsigned)k);
+    const unsigned hi = 255u - s_sel, above = s_before;
+    select([&](unsigned kk) { return (kk >> 8) == hi ? 255u - (kk & 255u) : 256u; }, (unsigned)k - above);
+    kth = (hi << 8) | (255u - s_sel);
+    gt = above + s_before;
+  }
+  // ---- the kept set in index order: every key above the k-th, then ties lowest index first ----
+  const unsigned need = (unsigned)k - gt;
+  unsigned ties = 0, above = 0;
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    ties += key(e) == kth;
+    above += key(e) > kth;
+  }
+  const unsigned tie_before = block_excl(ties);
+  unsigned pos = block_excl(above + min(ties, need > tie_before ? need - tie_before : 0u));
   unsigned tie_seen = tie_before;
-  for (int i = i0; i < i1; ++i) {
-    const uint16_t b = logits[i];
-    const unsigned key = order_key(b);
-    bool keep = key > kth;
-    if (key == kth) keep = tie_seen++ < need;
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const unsigned ke = key(e);
+    bool keep = ke > kth;
+    if (ke == kth) keep = tie_seen++ < need;
     if (keep) {
-      kidx[pos] = i;
-      kval[pos] = bf2f(b);
+      kidx[pos] = t * EPT + e;
+      kval[pos] = bf2f(sx[t * EPT + e]);
       ++pos;
     }
   }
@@ -241,50 +306,67 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
   if (lane == 0) red[wave] = m;
   __syncthreads();
   m = red[0];
-  for (int w = 1; w < 16; ++w) m = fmaxf(m, red[w]);
+  for (int w = 1; w < NW; ++w) m = fmaxf(m, red[w]);
   __syncthreads();
   const float e = mine ? expf(x - m) : 0.0f;
   float sum = wave_sum(e);
   if (lane == 0) red[wave] = sum;
   __syncthreads();
   sum = 0.0f;
-  for (int w = 0; w < 16; ++w) sum += red[w];
+  for (int w = 0; w < NW; ++w) sum += red[w];
   const float p = mine ? round_bf(e / sum) : 0.0f;
   if (mine) kval[t] = p;
   if (mine && kept_out) kept_out[t] = kidx[t];
   if (mine && probs_out) probs_out[t] = f2bf(p);
   __syncthreads();
-  // ---- multinomial: torch's CPU inverse CDF (running fp32 sum in index order, normalised, first >= u) ----
+  // ---- multinomial: torch's CPU inverse CDF — the running fp32 sum in index order (one thread: the order is the
+  // specification), normalised, the first index reaching u (every kept thread tests its own step) ----
   if (t == 0) {
+    float c = 0.0f;
+    for (int j = 0; j < k; j += 16) {
+      float4 v[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[q] = *(const float4*)&kval[j + 4 * q];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float f[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h)
+          if (j + 4 * q + h < k) {
+            c += f[h];
+            kcum[j + 4 * q + h] = c;
+          }
+      }
+    }
+    s_tot = c;
     float u;
     if (uniform) {
       u = *uniform;
     } else {
-      const unsigned long long c = *counter;
-      *counter = c + 1;
-      u = ((float)(mix64(seed ^ (c * 0xD1B54A32D192ED03ull)) >> 40) + 0.5f) * 0x1.0p-24f;  // in (0, 1)
+      const unsigned long long cn = *counter;
+      *counter = cn + 1;
+      u = ((float)(mix64(seed ^ (cn * 0xD1B54A32D192ED03ull)) >> 40) + 0.5f) * 0x1.0p-24f;  // in (0, 1)
     }
-    float tot = 0.0f;
-    for (int j = 0; j < k; ++j) tot += kval[j];
-    float cum = 0.0f;
-    int pick = kidx[k - 1];
-    for (int j = 0; j < k; ++j) {
-      cum += kval[j];
-      if (cum / tot >= u) {
-        pick = kidx[j];
-        break;
-      }
-    }
+    s_u = u;
+    s_tok = kidx[k - 1];
+  }
+  __syncthreads();
+  if (mine) {
+    const float tot = s_tot, u = s_u;
+    const float cdf = kcum[t] / tot, prev = t ? kcum[t - 1] / tot : -1.0f;
+    if (cdf >= u && prev < u) s_tok = kidx[t];
+  }
+  __syncthreads();
+  const int pick = s_tok;
+  if (t == 0) {
     if (out_idx) *out_idx = pick;
     if (token_out) *token_out = pick;
     if (pos_inout) *pos_inout += 1;
-    s_tok = pick;
   }
   if (emb_out) {
-    __syncthreads();
-    const long id = min(max(s_tok, 0), V - 1);
+    const long id = min(max(pick, 0), V - 1);
     const uint4* src = (const uint4*)(table + (size_t)id * C);
-    for (int i = t; i < C / 8; i += 1024) ((uint4*)emb_out)[i] = src[i];
+    for (int i = t; i < C / 8; i += NT) ((uint4*)emb_out)[i] = src[i];
   }
 }
 
@@ -337,8 +419,13 @@ extern "C" int lga_sample_topk(const void* logits, int n, int top_k, float tempe
   LGA_CHECK_ARG(!emb_out || (table && n_embd > 0 && n_embd % 8 == 0 && vocab > 0 && ((uintptr_t)table & 15) == 0 &&
                              ((uintptr_t)emb_out & 15) == 0),
                 "lga_sample_topk: the embedding gather needs a 16-B aligned table and emb_out, n_embd % 8 == 0");
-  lga::topk_sample_kernel<<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, top_k, temperature, uniform, seed, counter,
-                                                  out_idx, token_out, pos_inout, (const uint16_t*)table, n_embd, vocab,
-                                                  (uint16_t*)emb_out, kept_out, (uint16_t*)probs_out);
+#define LGA_TOPK(EPT)                                                                                           \
+  lga::topk_sample_kernel<EPT><<<1, 1024, 0, stream>>>((const uint16_t*)logits, n, top_k, temperature, uniform, seed, \
+                                                       counter, out_idx, token_out, pos_inout, (const uint16_t*)table,  \
+                                                       n_embd, vocab, (uint16_t*)emb_out, kept_out, (uint16_t*)probs_out)
+  if (n <= 1024 * 16) LGA_TOPK(16);
+  else if (n <= 1024 * 32) LGA_TOPK(32);
+  else LGA_TOPK(64);
+#undef LGA_TOPK
   LGA_LAUNCH_RETURN();
 }

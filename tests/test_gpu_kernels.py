@@ -355,7 +355,7 @@ def test_attention_matches_reference(ops, H, G, hs, T, positions, splits):
 
 
 @pytest.mark.parametrize("H,G,hs", [(8, 8, 128), (8, 2, 128), (4, 1, 64), (6, 3, 64)])
-@pytest.mark.parametrize("T,start", [(16, 0), (100, 0), (300, 0), (77, 500), (64, 1)])
+@pytest.mark.parametrize("T,start", [(16, 0), (100, 0), (300, 0), (77, 500), (64, 1), (1100, 0), (640, 37)])
 def test_prefill_flash_attention_matches_reference(ops, H, G, hs, T, start):
     """T >= 16 takes the MFMA flash-attention kernel: query t attends keys 0..start+t of the cache (keys beyond
     the query block and past max_seq masked), fp64 softmax reference; bf16 P/V products -> 2^-7 relative."""

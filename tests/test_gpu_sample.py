@@ -28,10 +28,18 @@ def ops():
 
 
 def _logits(n, seed, ties=False, scale=3.0):
+    """ties False / True (rounded: heavy ties) / "peaked" (one logit far above the rest: the k-th largest lies
+    outside the kernel's window below the max, so its radix fallback runs) / "ninf" (all but 5 logits -inf: the
+    k-th is a tie among -inf, taken lowest index first)."""
     g = torch.Generator().manual_seed(seed)
     x = torch.randn(n, generator=g) * scale
-    if ties:
+    if ties is True:
         x = x.round()
+    elif ties == "peaked":
+        x[n // 3] = 1000.0
+    elif ties == "ninf":
+        x = torch.full((n,), float("-inf"))
+        x[torch.randperm(n, generator=g)[:5]] = torch.randn(5, generator=g)
     return x.to(torch.bfloat16)
 
 
@@ -46,7 +54,8 @@ def _draw(ops, x, k, T, u):
 
 
 CASES = [(32000, 200, False), (32000, 200, True), (32000, 1, False), (32000, 1024, True), (50304, 200, True),
-         (1000, 1000, False), (7, 200, True), (65536, 64, True)]
+         (1000, 1000, False), (7, 200, True), (65536, 64, True), (32000, 200, "peaked"), (50304, 100, "peaked"),
+         (32000, 50, "ninf"), (3000, 7, "ninf")]
 
 
 @pytest.mark.parametrize("n,k,ties", CASES)
