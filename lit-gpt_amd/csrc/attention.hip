@@ -557,6 +557,15 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_kernel(const uint16_t* __
 // ahead of the math, with no staging registers; a raw s_barrier per tile after a counted vmcnt. The LDS reads are
 // inline asm with counted lgkmcnt waits (hipcc would wait for every DMA in flight before a compiler-visible LDS
 // read, not telling the stages apart). Per wave the arithmetic is attn_prefill_kernel's, op for op.
+// an LDS read at a compile-time offset (after unrolling) in inline asm; the host pass, which only type-checks the
+// kernel body, cannot take the "i" operand of a non-constant expression
+#ifdef __HIP_DEVICE_COMPILE__
+#define LGA_DS_READ(op, dst, addr, off) \
+  asm volatile(op " %0, %1 offset:%2" : "=v"(dst) : "v"(addr), "i"(off) : "memory")
+#else
+#define LGA_DS_READ(op, dst, addr, off) ((dst) = {}, (void)(addr), (void)(off))
+#endif
+
 template <int HS>
 __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_t* __restrict__ q,
                                                                    const uint16_t* __restrict__ kc,
@@ -641,8 +650,12 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_
       const int gp = wave * PIECES + i;
       const bool isv = gp >= TB / 1024;
       unsigned char* dst = st + (isv ? TB : 0) + (gp % (TB / 1024)) * 1024;
+#ifdef __HIP_DEVICE_COMPILE__  // (a device builtin: the host pass only type-checks the body)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(isv ? vrs : krs, (__attribute__((address_space(3))) void*)dst, 16,
                                                kb + dvoff[i], 0, 0, 0);
+#else
+      (void)dst, (void)kb, (void)isv;
+#endif
     }
   };
 
@@ -674,7 +687,7 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int ks = 2 * b + (j >> 1), st = j & 1;
-      asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(f[j]) : "v"(koff[ks] + sb), "i"(st * 32 * HS * 2) : "memory");
+      LGA_DS_READ("ds_read_b128", f[j], koff[ks] + sb, st * 32 * HS * 2);
     }
   };
   auto kmfma = [&](int b, const u32x4_t (&f)[4], f32x16_t (&acc)[2]) {
@@ -687,8 +700,8 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_
   auto vread = [&](unsigned sb, int kk, u32x2_t (&f)[DT][2]) {
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f[dt][0]) : "v"(voff0[dt] + sb), "i"(kk * 16 * HS * 2) : "memory");
-      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(f[dt][1]) : "v"(voff1[dt] + sb), "i"(kk * 16 * HS * 2) : "memory");
+      LGA_DS_READ("ds_read_b64_tr_b16", f[dt][0], voff0[dt] + sb, kk * 16 * HS * 2);
+      LGA_DS_READ("ds_read_b64_tr_b16", f[dt][1], voff1[dt] + sb, kk * 16 * HS * 2);
     }
   };
   // tie the fragments to a counted wait so no use moves above it
