@@ -18,7 +18,7 @@ extern "C" int lga_version(void) { return 1; }
 // builds the device objects of the prefill path's kernels now rather than at their first launch (common.h)
 extern "C" int lga_preload_kernels(void) {
   const int bad = lga::preload_gemm_q4f() + lga::preload_attention() + lga::preload_norm_rope() +
-                  lga::preload_sample() + lga::preload_gemv();
+                  lga::preload_sample() + lga::preload_gemv() + lga::preload_moe();
   if (bad) {
     lga_set_error("lga_preload_kernels: hipFuncGetAttributes failed");
     return 1;

@@ -88,6 +88,7 @@ int preload_attention();
 int preload_norm_rope();
 int preload_sample();
 int preload_gemv();
+int preload_moe();
 
 }  // namespace lga
 

@@ -228,3 +228,8 @@ extern "C" int lga_moe_group(const int32_t* expert_ids, int T, int k, int n_expe
   lga::moe_group_kernel<<<1, 1024, 0, stream>>>(expert_ids, T * k, k, n_expert, bm, tiles, x_rows, y_rows);
   LGA_LAUNCH_RETURN();
 }
+
+int lga::preload_moe() {  // the sparse-MoE prefill's routing, grouping and combine kernels
+  return lga::preload(lga::moe_route_kernel) + lga::preload(lga::moe_combine_kernel) +
+         lga::preload(lga::moe_group_kernel);
+}

@@ -373,7 +373,9 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
 }  // namespace lga
 
 int lga::preload_sample() {
-  return lga::preload(lga::argmax_kernel<true>) + lga::preload(lga::argmax_kernel<false>);
+  return lga::preload(lga::argmax_kernel<true>) + lga::preload(lga::argmax_kernel<false>) +
+         lga::preload(lga::topk_sample_kernel<16>) + lga::preload(lga::topk_sample_kernel<32>) +
+         lga::preload(lga::topk_sample_kernel<64>);
 }
 
 extern "C" int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,

@@ -209,6 +209,9 @@ def build_model(config: Config, *, quantize: Optional[str], device: torch.device
             tp.tensor_parallel_block(fabric, module)
         if precision is not None:
             precision.convert_module(module, device)
+            mlp = getattr(module, "mlp", None)
+            if hasattr(mlp, "_stack"):  # sparse MoE: the experts' packed weights stacked now, not in the first prompt
+                mlp._stack()
         else:  # bf16-true: the Linears stay nn.Linear; TP row shards are strided views -> own contiguous storage
             for mod in module.modules():
                 if isinstance(mod, torch.nn.Linear) and not mod.weight.is_contiguous():
