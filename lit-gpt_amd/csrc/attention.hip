@@ -16,7 +16,6 @@
 // the workgroup that arrives last merges the splits and writes the bf16 output (flash-decoding combine inside
 // the same launch; MI355X_MICROARCH.md "Valid forms" row 1), then re-arms the counter for the next launch.
 #include <cstdlib>
-#include <type_traits>
 
 #include "decode_ops.h"
 
@@ -633,15 +632,14 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_
   const __amdgpu_buffer_rsrc_t vrs =
       __builtin_amdgcn_make_buffer_rsrc((void*)(vc + (size_t)g * max_seq * HS), (short)0, max_seq * HS * 2, 0x00020000);
   constexpr int RPP = 1024 / (HS * 2);  // key rows per piece
-  int dvoff[PIECES];
-#pragma unroll
-  for (int i = 0; i < PIECES; ++i) {
+  // (recomputed per issue: a few VALU per tile instead of PIECES live registers)
+  auto dvoff = [&](int i) -> int {
     const int piece = (wave * PIECES + i) % (TB / 1024);
     const int r = piece * RPP + lane / CH;
     const int phys = lane % CH;
     const int sw = CH == 16 ? (((r & 3) << 2) | ((r >> 2) & 3)) : (((r & 3) << 1) | ((r >> 2) & 1));
-    dvoff[i] = (r * HS + (phys ^ sw) * 8) * 2;
-  }
+    return (r * HS + (phys ^ sw) * 8) * 2;
+  };
   auto issue = [&](int tt) {  // tile tt into stage tt % NS (every wave, every tile: the vmcnt counts stay uniform)
     unsigned char* st = &lds[tt % NS][0][0];
     const int kb = tt * KT * HS * 2;
@@ -652,9 +650,9 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_
       unsigned char* dst = st + (isv ? TB : 0) + (gp % (TB / 1024)) * 1024;
 #ifdef __HIP_DEVICE_COMPILE__  // (a device builtin: the host pass only type-checks the body)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(isv ? vrs : krs, (__attribute__((address_space(3))) void*)dst, 16,
-                                               kb + dvoff[i], 0, 0, 0);
+                                               kb + dvoff(i), 0, 0, 0);
 #else
-      (void)dst, (void)kb, (void)isv;
+      (void)dst, (void)kb, (void)isv, (void)dvoff;
 #endif
     }
   };
@@ -793,48 +791,29 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_
     l += rs;
   };
 
-#ifndef LGA_FA_LAG
-#define LGA_FA_LAG 1
-#endif
-  // Ring: tiles in flight ahead of the math, then per tile: wait for it (the tiles issued after it may stay in
-  // flight), barrier (every wave's pieces landed; every wave done with the stage the next issue overwrites), issue,
-  // math. LAG: the lo waves run half a tile behind — at iteration t they finish tile t-1 (softmax + P.V) and then
-  // compute S(t) — so the two waves of a SIMD are in opposite phases (one on S's MFMAs while the other is in the
-  // exponential-heavy softmax) instead of in lock step after every barrier. Each wave keeps one S tile in registers
-  // across the barrier; stages t-1 and t are both live, so the issue runs NS-2 tiles ahead instead of NS-1.
-  constexpr int AHEAD = LGA_FA_LAG ? NS - 2 : NS - 1;
-  const bool lag = LGA_FA_LAG && wave >= 4;
+  // Ring: tiles 0 .. NS-2 in flight, then per tile: wait for it (the tiles issued after it may stay in flight),
+  // barrier (every wave's pieces landed; every wave done with the stage the next issue overwrites), issue tile
+  // + NS - 1, math. (Round 4 also measured the lo waves half a tile behind the hi waves, so the two waves of a SIMD
+  // sit in opposite phases, and a software-pipelined form with S(t + 1)'s MFMAs under tile t's softmax and P.V:
+  // both slower)
 #pragma unroll
-  for (int i = 0; i < AHEAD; ++i)
+  for (int i = 0; i < NS - 1; ++i)
     if (i < ntiles) issue(i);
-  // two separate loops (the waves' roles are fixed), so each keeps its own register allocation
-  auto run = [&](auto lag_c) {
-    constexpr bool LAG = decltype(lag_c)::value;
-    f32x16_t sacc[2];
-    const int iters = ntiles + (LGA_FA_LAG ? 1 : 0);
-    for (int tt = 0; tt < iters; ++tt) {
-      const int after = min(AHEAD - 1, ntiles - 1 - tt);  // tiles issued after tt (negative past the last tile)
-      if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
-      else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (tt + AHEAD < ntiles) issue(tt + AHEAD);
-      const int k0 = tt * KT;
+  for (int tt = 0; tt < ntiles; ++tt) {
+    const int after = min(NS - 2, ntiles - 1 - tt);  // tiles issued after tt
+    if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PIECES) : "memory");
+    else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PIECES) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (tt + NS - 1 < ntiles) issue(tt + NS - 1);
+    const int k0 = tt * KT;
+    if (k0 <= wmax) {
+      f32x16_t sacc[2];
       const unsigned sb = (unsigned)((tt % NS) * 2 * TB);
-      if constexpr (LAG) {
-        if (tt >= 1 && k0 - KT <= wmax) pv_tile((unsigned)(((tt - 1) % NS) * 2 * TB), k0 - KT, sacc);
-        __builtin_amdgcn_sched_barrier(0);  // keep S(t) out of tile t-1's register lifetime
-        if (tt < ntiles && k0 <= wmax) s_tile(sb, sacc);
-      } else {
-        if (tt < ntiles && k0 <= wmax) {
-          s_tile(sb, sacc);
-          pv_tile(sb, k0, sacc);
-        }
-      }
+      s_tile(sb, sacc);
+      pv_tile(sb, k0, sacc);
     }
-  };
-  if (lag) run(std::true_type{});
-  else run(std::false_type{});
+  }
 #undef LGA_KW
 #undef LGA_VW4
 #undef LGA_VW2
