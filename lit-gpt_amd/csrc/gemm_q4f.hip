@@ -456,6 +456,16 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
       // order: hipcc would otherwise sink the reads next to their MFMAs (one LDS round trip exposed per 4 MFMAs),
       // and with at most 10 LDS reads in flight its counted lgkmcnt stays exact (the inline-asm dequant reads are
       // older than every fragment read they could be confused with).
+#ifndef LGA_Q4F_EXP
+#define LGA_Q4F_EXP 0  // lab only (tools/gemm_rates.py A/B): 1 no MFMAs, 2 no dequantization, 4 no fragment reads
+#endif
+      // (lab) the MFMAs' stand-in: an empty asm that keeps the fragment reads alive
+      auto use = [&](const Frags& f) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) asm volatile("" ::"v"(f.af[i]));
+#pragma unroll
+        for (int j = 0; j < FJ; ++j) asm volatile("" ::"v"(f.bfr[j]));
+      };
       for (int lk = 0; lk < nk; ++lk) {
         const bool full = lk + D + 1 < nk;
         const unsigned char* A = lds + (lk % NA) * A_BYTES;
@@ -463,25 +473,31 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
         raw_t wv;
         uint32_t sb, o[4 * NDW];
         Frags f0, f1;
-        dq_load(lk + 1, wv, sb);
+        if (!(LGA_Q4F_EXP & 2)) dq_load(lk + 1, wv, sb);
         __builtin_amdgcn_sched_barrier(0);
-        frag_read(A, B, 0, f0);
+        if (!(LGA_Q4F_EXP & 4)) frag_read(A, B, 0, f0);
+        else f0 = Frags{};
         __builtin_amdgcn_sched_barrier(0);
         if (lk + D < nk) issue_a(lk + D);
         if (full) issue_raw(lk + D + 1);
         __builtin_amdgcn_sched_barrier(0);
-        frag_read(A, B, 1, f1);
-        frag_mfma(f0);
+        if (!(LGA_Q4F_EXP & 4)) frag_read(A, B, 1, f1);
+        else f1 = Frags{};
+        if (LGA_Q4F_EXP & 1) use(f0);
+        else frag_mfma(f0);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // 4 MFMAs
           __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // 2 LDS reads
         }
         __builtin_amdgcn_sched_barrier(0);
-        dq_wait(wv, sb);
-        dq_math(wv, sb, o);
-        frag_mfma(f1);
-        dq_store(lk + 1, o);
+        if (!(LGA_Q4F_EXP & 2)) {
+          dq_wait(wv, sb);
+          dq_math(wv, sb, o);
+        }
+        if (LGA_Q4F_EXP & 1) use(f1);
+        else frag_mfma(f1);
+        if (!(LGA_Q4F_EXP & 2)) dq_store(lk + 1, o);
         if (full) wait_vm_lgkm<(D - 1) * G>();  // groups lk+2 .. lk+D, all full
         else wait_vm_lgkm<0>();
         __builtin_amdgcn_s_barrier();
