@@ -148,6 +148,18 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {  // 
   return x ^ (x >> 31);
 }
 
+#ifdef LGA_SAMPLE_TRACE  // lab builds only: phase timestamps of the sampler (100 MHz clock)
+__device__ unsigned long long g_sample_trace[16];
+#define LGA_STRACE(i)                                                   \
+  do {                                                                  \
+    if (threadIdx.x == 0) g_sample_trace[(i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define LGA_STRACE(i) \
+  do {                \
+  } while (0)
+#endif
+
 constexpr int kMaxTopK = 1024;
 
 __device__ __forceinline__ unsigned wave_max_u(unsigned v) {
@@ -179,17 +191,40 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
   __shared__ __attribute__((aligned(16))) float kval[kMaxTopK];
   __shared__ __attribute__((aligned(16))) float kcum[kMaxTopK];
   __shared__ int kidx[kMaxTopK];
-  __shared__ unsigned hist[256];
-  __shared__ unsigned wsum[NW];
-  __shared__ float red[NW];
-  __shared__ unsigned s_kmax, s_sel, s_before, s_found;
+  __shared__ unsigned hist[NW][256];  // one histogram per wave: 16x fewer atomics on one address
+  __shared__ unsigned wsum[NW], wsum2[NW], wmax_s[NW];
+  __shared__ float red[NW], red2[NW];
+  __shared__ unsigned s_sel, s_before, s_found;
   __shared__ float s_tot, s_u;
   __shared__ int s_tok;
   const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
   k = min(k, n);
-  for (int i = t; i < NT * EPT; i += NT) sx[i] = i < n ? logits[i] : (uint16_t)0xFF80u;  // -inf pads
+  float u0 = 0.0f;  // thread 0: the draw's uniform, fetched now so its global round trip overlaps the selection
+  if (t == 0) {
+    if (uniform) {
+      u0 = *uniform;
+    } else {
+      const unsigned long long cn = *counter;
+      *counter = cn + 1;
+      u0 = ((float)(mix64(seed ^ (cn * 0xD1B54A32D192ED03ull)) >> 40) + 0.5f) * 0x1.0p-24f;  // in (0, 1)
+    }
+  }
+  // stage the logits (pairs of bf16 per load when the row is 4-B aligned), -inf past n; clear the first histogram
+  if (((uintptr_t)logits & 3) == 0) {
+    for (int i2 = t; i2 < NT * EPT / 2; i2 += NT) {
+      const int i = 2 * i2;
+      uint32_t v = 0xFF80FF80u;
+      if (i + 1 < n) v = ((const uint32_t*)logits)[i2];
+      else if (i < n) v = (uint32_t)logits[i] | 0xFF800000u;
+      ((uint32_t*)sx)[i2] = v;
+    }
+  } else {
+    for (int i = t; i < NT * EPT; i += NT) sx[i] = i < n ? logits[i] : (uint16_t)0xFF80u;
+  }
+  for (int i = t; i < NW * 256; i += NT) (&hist[0][0])[i] = 0;
   if (t == 0) s_found = 0;
   __syncthreads();
+  LGA_STRACE(0);
   // this thread's order keys, two 16-bit keys per register (element 2j low, 2j+1 high); at 64 per thread they
   // would not fit beside the rest (1024 threads: 128 VGPRs), so that form reads them from the LDS copy instead
   constexpr bool REG = EPT <= 32;
@@ -209,29 +244,25 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
     if constexpr (REG) return (key2[e >> 1] >> (16 * (e & 1))) & 0xFFFFu;
     else return order_key(sx[t * EPT + e]);
   };
-  // exclusive prefix over the 1024 threads in index order
-  auto block_excl = [&](unsigned v) -> unsigned {
-    const unsigned inc = wave_incl_scan(v, lane);
-    if (lane == 63) wsum[wave] = inc;
-    __syncthreads();
-    unsigned base = 0;
-    for (int w = 0; w < wave; ++w) base += wsum[w];
-    __syncthreads();
-    return base + inc - v;
-  };
   // one selection pass: a 256-bin histogram of digit d (d ascending = key descending) over the keys `digit` maps
   // into [0, 256), then the bin where the running count from d = 0 first reaches `need` (s_sel) and the count
-  // before it (s_before); s_found stays 0 when the binned keys number fewer than `need`
-  auto select = [&](auto digit, unsigned need) {
-    if (t < 256) hist[t] = 0;
-    __syncthreads();
+  // before it (s_before); s_found stays 0 when the binned keys number fewer than `need`. `clear`: zero the
+  // histogram first (the first pass finds it cleared by the staging phase)
+  auto select = [&](auto digit, unsigned need, bool clear) {
+    if (clear) {
+      for (int i = t; i < NW * 256; i += NT) (&hist[0][0])[i] = 0;
+      __syncthreads();
+    }
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
       const unsigned d = digit(key(e));
-      if (d < 256u) atomicAdd(&hist[d], 1u);
+      if (d < 256u) atomicAdd(&hist[wave][d], 1u);
     }
     __syncthreads();
-    const unsigned c = t < 256 ? hist[t] : 0u;
+    unsigned c = 0;
+    if (t < 256)
+#pragma unroll
+      for (int w = 0; w < NW; ++w) c += hist[w][t];
     const unsigned inc = wave_incl_scan(c, lane);
     if (lane == 63 && wave < 4) wsum[wave] = inc;
     __syncthreads();
@@ -249,34 +280,41 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
   // ---- the k-th largest key. First the 256 keys just below the maximum (one pass, atomics only for the keys near
   // the top: logits are dense around their mean, and the top-k of a vocabulary usually sits within two binades of
   // the max); otherwise an MSD radix select on the high byte, then the low byte. ----
+  unsigned kmax;
   {
     unsigned m = 0;
+    if constexpr (REG) {  // two keys per v_pk_max_u16
+      typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+      u16x2 mm = __builtin_bit_cast(u16x2, key2[0]);
 #pragma unroll
-    for (int e = 0; e < EPT; ++e) m = max(m, key(e));
-    m = wave_max_u(m);
-    if (lane == 0) wsum[wave] = m;
-    __syncthreads();
-    if (t == 0) {
-      unsigned mm = 0;
-      for (int w = 0; w < NW; ++w) mm = max(mm, wsum[w]);
-      s_kmax = mm;
+      for (int j = 1; j < EPT / 2; ++j) mm = __builtin_elementwise_max(mm, __builtin_bit_cast(u16x2, key2[j]));
+      m = max((unsigned)mm[0], (unsigned)mm[1]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < EPT; ++e) m = max(m, key(e));
     }
+    m = wave_max_u(m);
+    if (lane == 0) wmax_s[wave] = m;
     __syncthreads();
+    kmax = wmax_s[0];
+    for (int w = 1; w < NW; ++w) kmax = max(kmax, wmax_s[w]);
   }
-  const unsigned kmax = s_kmax;
+  LGA_STRACE(1);
   unsigned kth, gt;
-  select([&](unsigned kk) { return kmax - kk; }, (unsigned)k);
+  select([&](unsigned kk) { return kmax - kk; }, (unsigned)k, false);
   if (s_found) {
     kth = kmax - s_sel;
     gt = s_before;
   } else {
-    select([&](unsigned kk) { return 255u - (kk >> 8); }, (unsigned)k);
+    select([&](unsigned kk) { return 255u - (kk >> 8); }, (unsigned)k, true);
     const unsigned hi = 255u - s_sel, above = s_before;
-    select([&](unsigned kk) { return (kk >> 8) == hi ? 255u - (kk & 255u) : 256u; }, (unsigned)k - above);
+    select([&](unsigned kk) { return (kk >> 8) == hi ? 255u - (kk & 255u) : 256u; }, (unsigned)k - above, true);
     kth = (hi << 8) | (255u - s_sel);
     gt = above + s_before;
   }
-  // ---- the kept set in index order: every key above the k-th, then ties lowest index first ----
+  LGA_STRACE(2);
+  // ---- the kept set in index order: every key above the k-th, then ties lowest index first. One block scan of
+  // (ties, above): before thread t sit above_before keys above the k-th and min(tie_before, need) taken ties ----
   const unsigned need = (unsigned)k - gt;
   unsigned ties = 0, above = 0;
 #pragma unroll
@@ -284,8 +322,23 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
     ties += key(e) == kth;
     above += key(e) > kth;
   }
-  const unsigned tie_before = block_excl(ties);
-  unsigned pos = block_excl(above + min(ties, need > tie_before ? need - tie_before : 0u));
+  unsigned tie_before, above_before;
+  {
+    const unsigned ti = wave_incl_scan(ties, lane), ai = wave_incl_scan(above, lane);
+    if (lane == 63) {
+      wsum[wave] = ti;
+      wsum2[wave] = ai;
+    }
+    __syncthreads();
+    unsigned tb = 0, ab = 0;
+    for (int w = 0; w < wave; ++w) {
+      tb += wsum[w];
+      ab += wsum2[w];
+    }
+    tie_before = tb + ti - ties;
+    above_before = ab + ai - above;
+  }
+  unsigned pos = above_before + min(tie_before, need);
   unsigned tie_seen = tie_before;
 #pragma unroll
   for (int e = 0; e < EPT; ++e) {
@@ -299,6 +352,7 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
     }
   }
   __syncthreads();
+  LGA_STRACE(3);
   // ---- softmax over the kept logits / temperature, in bf16 like the reference's bf16 tensor ops ----
   const bool mine = t < k;
   const float x = mine ? round_bf(kval[t] / temperature) : -INFINITY;
@@ -307,21 +361,23 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
   __syncthreads();
   m = red[0];
   for (int w = 1; w < NW; ++w) m = fmaxf(m, red[w]);
-  __syncthreads();
   const float e = mine ? expf(x - m) : 0.0f;
   float sum = wave_sum(e);
-  if (lane == 0) red[wave] = sum;
+  if (lane == 0) red2[wave] = sum;
   __syncthreads();
   sum = 0.0f;
-  for (int w = 0; w < NW; ++w) sum += red[w];
+  for (int w = 0; w < NW; ++w) sum += red2[w];
   const float p = mine ? round_bf(e / sum) : 0.0f;
-  if (mine) kval[t] = p;
+  if (t < ((k + 15) & ~15)) kval[t] = p;  // zero past k: the sequential sum below reads whole groups of 16
   if (mine && kept_out) kept_out[t] = kidx[t];
   if (mine && probs_out) probs_out[t] = f2bf(p);
   __syncthreads();
+  LGA_STRACE(4);
   // ---- multinomial: torch's CPU inverse CDF — the running fp32 sum in index order (one thread: the order is the
   // specification), normalised, the first index reaching u (every kept thread tests its own step) ----
   if (t == 0) {
+    // probabilities past k are zero (kval padded below), so whole float4 groups need no bounds test: the running
+    // sum stays put over them
     float c = 0.0f;
     for (int j = 0; j < k; j += 16) {
       float4 v[4];
@@ -329,25 +385,16 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
       for (int q = 0; q < 4; ++q) v[q] = *(const float4*)&kval[j + 4 * q];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const float f[4] = {v[q].x, v[q].y, v[q].z, v[q].w};
-#pragma unroll
-        for (int h = 0; h < 4; ++h)
-          if (j + 4 * q + h < k) {
-            c += f[h];
-            kcum[j + 4 * q + h] = c;
-          }
+        float4 o;
+        o.x = c += v[q].x;
+        o.y = c += v[q].y;
+        o.z = c += v[q].z;
+        o.w = c += v[q].w;
+        *(float4*)&kcum[j + 4 * q] = o;
       }
     }
     s_tot = c;
-    float u;
-    if (uniform) {
-      u = *uniform;
-    } else {
-      const unsigned long long cn = *counter;
-      *counter = cn + 1;
-      u = ((float)(mix64(seed ^ (cn * 0xD1B54A32D192ED03ull)) >> 40) + 0.5f) * 0x1.0p-24f;  // in (0, 1)
-    }
-    s_u = u;
+    s_u = u0;
     s_tok = kidx[k - 1];
   }
   __syncthreads();
@@ -357,6 +404,7 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
     if (cdf >= u && prev < u) s_tok = kidx[t];
   }
   __syncthreads();
+  LGA_STRACE(5);
   const int pick = s_tok;
   if (t == 0) {
     if (out_idx) *out_idx = pick;
@@ -431,3 +479,9 @@ extern "C" int lga_sample_topk(const void* logits, int n, int top_k, float tempe
 #undef LGA_TOPK
   LGA_LAUNCH_RETURN();
 }
+
+#ifdef LGA_SAMPLE_TRACE
+extern "C" int lga_sample_trace(unsigned long long* out) {  // lab: the last launch's phase timestamps
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(lga::g_sample_trace), sizeof(unsigned long long) * 16);
+}
+#endif
