@@ -9,6 +9,8 @@
 #   @tests:TAG   the whole -m gpu suite                @smoke:TAG  __graft_entry__.smoke()
 #   @bench:TAG   bench.py (driver defaults)            @prof:TAG   rocprofv3 kernel trace + stats of bench.py
 #   @last:TAG    tests + smoke + bench + prof: the last check of a committed tree
+#   @tp:TAG      the driver's multi-GPU bench invocation rehearsed with 2 ranks on the one GPU (LGA_ONE_DEVICE=1, gloo
+#                host collectives, xGMI-kernel decode all-reduces): the TP path end to end, NOT a scaling number
 # e.g. /usr/local/graft/bin/gpurun --timeout 1200 -- 'bash tools/gpu_session.sh @last:r04z'
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -23,6 +25,7 @@ expand() {  # preset:tag -> step specs, one per line
     @bench) echo "$tag/bench:400:python -u bench.py" ;;
     @prof) echo "$tag/prof:400:$PROF -d gpurun_out/$tag/prof -o bench -- python bench.py --no-traffic --no-cpu-baseline" ;;
     @last) expand "@tests:$tag"; expand "@smoke:$tag"; expand "@bench:$tag"; expand "@prof:$tag" ;;
+    @tp) echo "$tag/bench_tp2:400:LGA_ONE_DEVICE=1 LGA_DIST_BACKEND=gloo OMP_NUM_THREADS=2 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29561 bench.py --gpus 2 --steps 16 --warmup 8 --no-cpu-baseline" ;;
     *) echo "unknown preset $p" >&2; return 1 ;;
   esac
 }
