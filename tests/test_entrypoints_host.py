@@ -101,3 +101,35 @@ def test_chat_prompt_config():
     # the reference's regex (chat/base.py:326) does not match Mixtral: plain template
     assert prompt_config(Path("checkpoints/mistralai/Mixtral-8x7B-Instruct-v0.1"), Tok()) == ("{prompt}", ([2],))
     assert prompt_config(Path("checkpoints/meta-llama/Llama-2-7b-hf"), Tok()) == ("{prompt}", ([2],))
+
+
+def test_sampling_route_and_rng_state():
+    """generate/base.py's sample() routing (reference :30-41): the reference's default (top_k 200, temperature 0.8)
+    and any top_k in [1, 1024] over bf16 logits go to the one-launch device sampler (and so into the decode graph);
+    top_k None / > 1024, fp32 logits and greedy do not. SamplerRNG draws its seed from torch's generator, so
+    torch.manual_seed reproduces a run, and keeps a device counter starting at zero."""
+    from generate.base import SamplerRNG, device_sampling
+
+    bf, f32 = torch.bfloat16, torch.float32
+    assert device_sampling(0.8, 200, bf)
+    assert device_sampling(1.0, 1, bf) and device_sampling(1.0, 1024, bf)
+    assert not device_sampling(0.8, None, bf)
+    assert not device_sampling(0.8, 1025, bf)
+    assert not device_sampling(0.8, 0, bf)
+    assert not device_sampling(0.8, 200, f32)
+    assert not device_sampling(0.0, 200, bf)
+    torch.manual_seed(1234)
+    a = SamplerRNG(torch.device("cpu"))
+    torch.manual_seed(1234)
+    b = SamplerRNG(torch.device("cpu"))
+    c = SamplerRNG(torch.device("cpu"))
+    assert a.seed == b.seed != c.seed
+    assert a.counter.dtype == torch.int64 and int(a.counter) == 0
+    assert SamplerRNG(torch.device("cpu"), seed=7).seed == 7
+
+
+def test_sample_refuses_cpu_logits():
+    from generate.base import sample
+
+    with pytest.raises(RuntimeError):
+        sample(torch.zeros(1, 1, 10), temperature=0.8, top_k=5)
