@@ -47,10 +47,12 @@ class SamplerRNG:
         self.counter = torch.zeros(1, dtype=torch.int64, device=device)
 
 
-def device_sampling(temperature: float, top_k: Optional[int], dtype: torch.dtype) -> bool:
+def device_sampling(temperature: float, top_k: Optional[int], dtype: torch.dtype, vocab: int = 0) -> bool:
     """Whether ``sample`` at this setting runs as the one-launch HIP sampler (ops.sample_topk): temperature > 0 with
-    top_k in [1, 1024] over bf16 logits — the reference's defaults (top_k 200, temperature 0.8) included."""
-    return temperature > 0.0 and top_k is not None and 1 <= top_k <= ops.MAX_TOP_K and dtype == torch.bfloat16
+    top_k in [1, 1024] over bf16 logits of at most 65536 entries — the reference's defaults (top_k 200,
+    temperature 0.8) included."""
+    return (temperature > 0.0 and top_k is not None and 1 <= top_k <= ops.MAX_TOP_K and dtype == torch.bfloat16
+            and vocab <= ops.MAX_SAMPLE_VOCAB)
 
 
 def sample(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] = None,
@@ -63,7 +65,7 @@ def sample(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] 
     if not logits.is_cuda:
         raise RuntimeError("sample: logits must be on the GPU (this build has no CPU path)")
     if temperature > 0.0:
-        if device_sampling(temperature, top_k, logits.dtype):
+        if device_sampling(temperature, top_k, logits.dtype, logits.size(-1)):
             rng = rng if rng is not None else SamplerRNG(logits.device)
             return ops.sample_topk(logits.contiguous(), top_k, temperature, seed=rng.seed, counter=rng.counter)
         if top_k is not None:
@@ -82,7 +84,8 @@ def next_token(model: GPT, input_pos: torch.Tensor, x: torch.Tensor, **kwargs: A
 def graph_sampling(model: GPT, temperature: float, top_k: Optional[int]) -> bool:
     """Whether decode steps at this setting run as captured HIP graphs (lit_gpt/runtime.py DecodeGraph): greedy, or
     the device sampler (``device_sampling``) over the model's bf16 logits."""
-    return temperature == 0.0 or device_sampling(temperature, top_k, model.transformer.wte.weight.dtype)
+    wte = model.transformer.wte.weight
+    return temperature == 0.0 or device_sampling(temperature, top_k, wte.dtype, model.config.padded_vocab_size)
 
 
 DECODE_CHUNK = 8  # greedy decode steps per graph launch (lit_gpt/runtime.py DecodeGraph.steps)

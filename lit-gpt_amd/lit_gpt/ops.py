@@ -533,6 +533,7 @@ def argmax_embed(logits, table, emb_out, out_idx=None, token_out=None, pos_inout
 
 
 MAX_TOP_K = 1024  # lga_sample_topk keeps at most this many logits
+MAX_SAMPLE_VOCAB = 65536  # ... out of at most this many (one workgroup holds them in LDS)
 
 
 def sample_topk(logits, top_k, temperature, *, uniform=None, seed=0, counter=None, out_idx=None, token_out=None,

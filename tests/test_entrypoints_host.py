@@ -118,6 +118,7 @@ def test_sampling_route_and_rng_state():
     assert not device_sampling(0.8, 0, bf)
     assert not device_sampling(0.8, 200, f32)
     assert not device_sampling(0.0, 200, bf)
+    assert device_sampling(0.8, 200, bf, 65536) and not device_sampling(0.8, 200, bf, 65537)
     torch.manual_seed(1234)
     a = SamplerRNG(torch.device("cpu"))
     torch.manual_seed(1234)
