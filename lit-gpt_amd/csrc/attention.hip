@@ -838,8 +838,8 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_
 #ifndef LGA_ATTN_Q2
 #define LGA_ATTN_Q2 4, 4
 #endif
-#ifndef LGA_ATTN_Q4
-#define LGA_ATTN_Q4 2, 4
+#ifndef LGA_ATTN_Q4  // 8 waves (round 4, tools/attn_sweep.py 32 8 128: Mixtral at 16 splits 12.5-12.9 vs 13.7-14.1 us)
+#define LGA_ATTN_Q4 2, 8
 #endif
 #ifndef LGA_ATTN_Q8
 #define LGA_ATTN_Q8 2, 4
