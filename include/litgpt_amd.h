@@ -131,8 +131,9 @@ int lga_gelu(const void* a, void* y, long n, int approximate_tanh, lga_stream_t 
  * q (T, H, hs); caches (G, max_seq, hs); query t attends keys 0..input_pos[t]; y (T, H*hs).
  * n_splits > 1 splits keys 0..input_pos[t] evenly (flash-decoding; the split merge happens in the same launch
  * by the last-arriving workgroup) and needs `workspace` of lga_attention_workspace_bytes(T, H, hs, n_splits) bytes
- * plus `counters` (T * G * 64 uint32 — one per (t, group) at a 256-B stride so the device-scope atomics do not
- * share a line; zeroed once at allocation, re-armed by the kernel).
+ * plus `counters` (T * H * 64 uint32 — one per (t, group, head slice) at a 256-B stride so the device-scope
+ * atomics do not share a line; zeroed once at allocation, re-armed by the kernel; at T = 1 a group's heads may be
+ * dealt to up to H/G workgroups when the groups are few).
  * head_size in {64, 128}; H/G in {1,2,4,8}; 1 <= n_splits <= 256. */
 int lga_attention(const void* q, const void* k_cache, const void* v_cache, const int64_t* input_pos, void* y,
                   float* workspace, unsigned* counters, int T, int n_head, int n_query_groups, int head_size,

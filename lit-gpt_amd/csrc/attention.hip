@@ -56,13 +56,16 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
                                                    uint16_t* __restrict__ y, float* __restrict__ ws,
                                                    unsigned* __restrict__ cnt, int n_head, int max_seq, float scale,
                                                    const int64_t* __restrict__ rope_pos, const float* __restrict__ cos,
-                                                   const float* __restrict__ sin, int rope_rows) {
+                                                   const float* __restrict__ sin, int rope_rows, int hsplit) {
   constexpr int LPR = HS / 8;    // lanes per key row
   constexpr int RGW = 64 / LPR;  // row groups per wave
   constexpr int RG = NW * RGW;   // row groups per workgroup
   constexpr int NT = NW * 64;
-  const int split = blockIdx.x, g = blockIdx.y, t = blockIdx.z;
-  const int n_splits = gridDim.x, G = gridDim.y;
+  // blockIdx.y = (query group, head slice): with hsplit > 1 the group's QPKT heads are dealt to hsplit workgroups of
+  // QPK heads each (few groups per rank: more workgroups per launch, each doing less per key)
+  const int split = blockIdx.x, gy = blockIdx.y, t = blockIdx.z;
+  const int g = gy / hsplit, hsi = gy % hsplit, QPKT = QPK * hsplit;
+  const int n_splits = gridDim.x;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int rg = wave * RGW + lane / LPR;
   const int sub = lane % LPR;
@@ -87,10 +90,10 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
 #pragma unroll
   for (int h = 0; h < QPK; ++h) {
     if (FUSED) {  // qkv row layout per group: [q_0 .. q_{QPK-1}, k, v] x HS (scripts/convert_hf_checkpoint.py:181-187)
-      const uint4 raw = *(const uint4*)(q + ((size_t)g * (QPK + 2) + h) * HS + sub * 8);
+      const uint4 raw = *(const uint4*)(q + ((size_t)g * (QPKT + 2) + hsi * QPK + h) * HS + sub * 8);
       unpack8(rope8(raw, cr, sr, sub), qf[h]);
     } else {
-      unpack8(*(const uint4*)(q + ((size_t)t * n_head + (size_t)g * QPK + h) * HS + sub * 8), qf[h]);
+      unpack8(*(const uint4*)(q + ((size_t)t * n_head + (size_t)g * QPKT + hsi * QPK + h) * HS + sub * 8), qf[h]);
     }
   }
   LGA_TRACE(2);
@@ -169,11 +172,13 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
   }
   LGA_TRACE(3);
   if (FUSED && owns_new && rg == 0) {  // the new key/value: rope k, append both to the cache, score from registers
-    const uint16_t* kvrow = q + ((size_t)g * (QPK + 2) + QPK) * HS + sub * 8;
+    const uint16_t* kvrow = q + ((size_t)g * (QPKT + 2) + QPKT) * HS + sub * 8;
     const uint4 kr = rope8(*(const uint4*)kvrow, cr, sr, sub);
     const uint4 vr = *(const uint4*)(kvrow + HS);
-    *(uint4*)(kc + ((size_t)g * max_seq + p) * HS + sub * 8) = kr;
-    *(uint4*)(vc + ((size_t)g * max_seq + p) * HS + sub * 8) = vr;
+    if (hsi == 0) {  // one head slice appends; the others score the same key from their registers
+      *(uint4*)(kc + ((size_t)g * max_seq + p) * HS + sub * 8) = kr;
+      *(uint4*)(vc + ((size_t)g * max_seq + p) * HS + sub * 8) = vr;
+    }
     float kf[8], vf[8];
     unpack8(kr, kf);
     unpack8(vr, vf);
@@ -222,7 +227,7 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
     }
   }
   __syncthreads();
-  const size_t row0 = (size_t)t * n_head + (size_t)g * QPK;  // first head row of this group
+  const size_t row0 = (size_t)t * n_head + (size_t)g * QPKT + hsi * QPK;  // first head row of this slice
   for (int it = threadIdx.x; it < QPK * HS; it += NT) {
     const int h = it / HS, d = it % HS;
     float mx = -INFINITY;
@@ -251,7 +256,7 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
   // ---- publish, then the last-arriving split of this (t, group) merges all splits ----
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
   __syncthreads();
-  unsigned* ctr = cnt + ((size_t)t * G + g) * kCounterStride;
+  unsigned* ctr = cnt + ((size_t)t * gridDim.y + gy) * kCounterStride;
   if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   LGA_TRACE(5);
@@ -835,6 +840,9 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_
 #ifndef LGA_ATTN_Q1
 #define LGA_ATTN_Q1 4, 4
 #endif
+#ifndef LGA_ATTN_Q1_FEW
+#define LGA_ATTN_Q1_FEW 2, 8
+#endif
 #ifndef LGA_ATTN_Q2
 #define LGA_ATTN_Q2 4, 4
 #endif
@@ -851,22 +859,42 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_
 template <int HS, int QPK, int UNR, int NW, bool FUSED>
 static void launch_one(dim3 grid, hipStream_t stream, const void* q, void* kc, void* vc, const int64_t* pos, void* y,
                        float* ws, unsigned* cnt, int H, int max_seq, float scale, const int64_t* rope_pos,
-                       const float* cos, const float* sin, int rope_rows) {
+                       const float* cos, const float* sin, int rope_rows, int hsplit) {
   attn_kernel<HS, QPK, UNR, NW, FUSED, LGA_ATTN_PIPE != 0><<<grid, NW * 64, 0, stream>>>((const uint16_t*)q, (uint16_t*)kc, (uint16_t*)vc,
                                                                      pos, (uint16_t*)y, ws, cnt, H, max_seq, scale,
-                                                                     rope_pos, cos, sin, rope_rows);
+                                                                     rope_pos, cos, sin, rope_rows, hsplit);
+}
+
+// head slices per query group: split a group's heads over more workgroups while the launch would fill at most half
+// the CUs (tools/attn_sweep.py, p = 2303, 16 splits: Llama-2-70B at TP = 8 — one group of 8 heads per rank — 22.5 ->
+// 7.8 us with 8 slices; 70B TP = 1 23.6 -> 13.4 with 2; Mixtral 12.9 -> 10.3 with 2, Mixtral TP = 2 12.6 -> 8.3
+// with 4; profiles/r04u_attn_head_slices.txt)
+static int attn_hsplit(int T, int G, int qpk, int n_splits) {
+  int h = 1;
+  if (T == 1 && n_splits > 1)
+    while (h < qpk && G * h * n_splits <= 128) h *= 2;
+  if (const char* e = getenv("LGA_ATTN_HSPLIT")) {  // lab A/B
+    const int v = atoi(e);
+    if (v >= 1 && v <= qpk && qpk % v == 0) h = v;
+  }
+  return h;
 }
 
 template <int HS, bool FUSED>
 static int launch_hs(const void* q, void* kc, void* vc, const int64_t* pos, void* y, float* ws, unsigned* cnt, int T,
                      int H, int G, int max_seq, int n_splits, float scale, const int64_t* rope_pos, const float* cos,
                      const float* sin, int rope_rows, hipStream_t stream) {
-  const dim3 grid(n_splits, G, T);
+  const int hsplit = attn_hsplit(T, G, H / G, n_splits);
+  const dim3 grid(n_splits, G * hsplit, T);
 #define LGA_ATTN(QPK, CFG)                                                                                        \
   launch_one<HS, QPK, CFG, FUSED>(grid, stream, q, kc, vc, pos, y, ws, cnt, H, max_seq, scale, rope_pos, cos, sin, \
-                                  rope_rows)
-  switch (H / G) {
-    case 1: LGA_ATTN(1, LGA_ATTN_Q1); break;
+                                  rope_rows, hsplit)
+  switch (H / G / hsplit) {
+    case 1:  // one head per group: 8 waves x 2 keys in flight when the groups are few (TP ranks: G = 4 7.9 vs 8.2 us,
+             // G = 8 8.0 vs 8.7 at 16 splits; profiles/r04u_attn_head_slices.txt), else 4 x 4 (Llama-2-7B, G = 32)
+      if (G * hsplit <= 16) LGA_ATTN(1, LGA_ATTN_Q1_FEW);
+      else LGA_ATTN(1, LGA_ATTN_Q1);
+      break;
     case 2: LGA_ATTN(2, LGA_ATTN_Q2); break;
     case 4: LGA_ATTN(4, LGA_ATTN_Q4); break;
     case 8: LGA_ATTN(8, LGA_ATTN_Q8); break;
@@ -970,7 +998,8 @@ extern "C" int lga_attn_trace_read(unsigned long long* host, int n) {
 }
 #endif
 
-// fp32 partials (T * H * n_splits * (hs + 4)); the counters (T * G * 64 uint32) must be zeroed once at allocation
+// fp32 partials (T * H * n_splits * (hs + 4)); the counters (T * n_head * 64 uint32: one per (row, query group, head
+// slice) at a 256-B stride) must be zeroed once at allocation
 extern "C" size_t lga_attention_workspace_bytes(int T, int n_head, int head_size, int n_splits) {
   return (size_t)T * n_head * (n_splits < 1 ? 1 : n_splits) * (head_size + 4) * sizeof(float);
 }

@@ -18,6 +18,30 @@ __device__ __forceinline__ uint16_t* slot_ptr(unsigned char* mb, int slot, int s
   return (uint16_t*)(mb + kFlagBytes) + ((size_t)slot * kMaxRanks + src) * cap;
 }
 
+// Mailbox payload traffic is system-coherent (sc0 sc1): the pushes write through every cache level, the reads bypass
+// them, so a slot's bytes never depend on which XCD's L2 (or which process's mapping of the IPC buffer) saw them
+// last — on top of the flags' release / acquire. (8 ranks sharing one GPU, 64 back-to-back calls, intermittently
+// summed a stale slot with plain payload accesses: tests/workers/allreduce_worker.py "burst".) 16-B buffer accesses,
+// offsets in voffset; the resource's base is wave-uniform.
+typedef uint32_t mb_u32x4 __attribute__((ext_vector_type(4)));
+constexpr int kSysCoherent = 1 | 16;  // cache-policy aux bits sc0 | sc1 (gfx940+)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t mb_rsrc(const void* base, int bytes) {
+  // the base is wave-uniform by construction; readfirstlane makes that visible to hipCC, which would otherwise keep
+  // the resource in VGPRs and wrap every access in a waterfall loop
+  const uint64_t v = (uint64_t)(uintptr_t)base;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(uintptr_t)(((uint64_t)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ void st_sys16(__amdgpu_buffer_rsrc_t r, int off, uint4 v) {
+  const mb_u32x4 w = {v.x, v.y, v.z, v.w};
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, off, 0, kSysCoherent);
+}
+__device__ __forceinline__ uint4 ld_sys16(__amdgpu_buffer_rsrc_t r, int off) {
+  const mb_u32x4 w = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, kSysCoherent);
+  return make_uint4(w.x, w.y, w.z, w.w);
+}
+
 // The flag protocol follows the memory model (LGA_COMM_FORMAL=1, default): a system-scope release before each flag,
 // an acquire after the wait. Mailboxes are UNCACHED device memory (lga_comm_alloc: hipDeviceMallocUncached), so
 // LGA_COMM_FORMAL=0 builds the form that relies on that instead (drains + barriers, no cache maintenance); on one
@@ -74,12 +98,28 @@ __device__ __forceinline__ void wait_flags(const Peers& peers, int rank, int wor
 
 // y[8 i .. 8 i + 8) = bf16(sum over ranks 0..world-1 of src_r) (+ residual: bf16(bf16(sum) + residual)) — the
 // ordered fp32 sum every rank computes identically
-__device__ __forceinline__ uint4 ordered_sum8(const uint4* const* src, int world, const uint16_t* residual, int i) {
+// rs[r]: rank r's slot in this rank's mailbox (read system-coherent; built by slot_rsrcs), except rank local_rank
+// (-1: none), whose partial is read from `x_local`. The rank loop is unrolled to kMaxRanks so the resources stay in
+// scalar registers (a runtime-indexed array would put them in VGPRs and wrap every load in a waterfall loop).
+__device__ __forceinline__ void slot_rsrcs(const Peers& peers, int rank, int slot, int world, int cap,
+                                           __amdgpu_buffer_rsrc_t (&rs)[kMaxRanks]) {
+#pragma unroll
+  for (int r = 0; r < kMaxRanks; ++r) rs[r] = mb_rsrc(slot_ptr(peers.mb[rank], slot, r < world ? r : 0, cap), cap * 2);
+}
+__device__ __forceinline__ uint4 ordered_sum8(const __amdgpu_buffer_rsrc_t (&rs)[kMaxRanks], const uint4* x_local,
+                                             int local_rank, int world, const uint16_t* residual, int i) {
   float acc[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) acc[e] = 0.0f;
-  for (int r = 0; r < world; ++r) {
-    const uint4 v = src[r][i];
+  // every rank's piece in flight at once (one load round trip), then the sum in rank order
+  uint4 vin[kMaxRanks];
+#pragma unroll
+  for (int r = 0; r < kMaxRanks; ++r)
+    vin[r] = r >= world ? make_uint4(0, 0, 0, 0) : (r == local_rank ? x_local[i] : ld_sys16(rs[r], i * 16));
+#pragma unroll
+  for (int r = 0; r < kMaxRanks; ++r) {
+    if (r >= world) break;
+    const uint4 v = vin[r];
     const uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {

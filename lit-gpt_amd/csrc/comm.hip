@@ -29,14 +29,14 @@ __global__ void __launch_bounds__(kCommThreads) allreduce_kernel(const uint16_t*
                                                                  unsigned* __restrict__ seq_ctr,
                                                                  unsigned* __restrict__ err) {
   const int t = threadIdx.x;
-  const unsigned seq = *seq_ctr + 1u;
+  const unsigned seq = __builtin_amdgcn_readfirstlane(*seq_ctr + 1u);  // uniform: the mailbox resources stay scalar
   const int slot = seq & 1;
   const int n8 = n / 8;
   // 1. push this rank's partial into every peer's mailbox (16-B stores over xGMI)
   for (int r = 0; r < world; ++r) {
     if (r == rank) continue;
-    uint4* dst = (uint4*)slot_ptr(peers.mb[r], slot, rank, cap);
-    for (int i = t; i < n8; i += kCommThreads) dst[i] = ((const uint4*)x)[i];
+    const __amdgpu_buffer_rsrc_t dst = mb_rsrc(slot_ptr(peers.mb[r], slot, rank, cap), n * 2);
+    for (int i = t; i < n8; i += kCommThreads) st_sys16(dst, i * 16, ((const uint4*)x)[i]);
   }
   // 2. release: every storing thread's writes are complete and visible system-wide before any flag (each storing
   //    wave drains its stores, the workgroup barrier orders them before the flag writers: raise_flags in comm.h;
@@ -49,10 +49,10 @@ __global__ void __launch_bounds__(kCommThreads) allreduce_kernel(const uint16_t*
   wait_flags(peers, rank, world, seq, err, t);
   __syncthreads();
   // 4. ordered fp32 sum over ranks 0..W-1, bf16 once, then the residual add in the reference's rounding
-  const uint4* src[kMaxRanks];
-  for (int r = 0; r < world; ++r)
-    src[r] = r == rank ? (const uint4*)x : (const uint4*)slot_ptr(peers.mb[rank], slot, r, cap);
-  for (int i = t; i < n8; i += kCommThreads) ((uint4*)y)[i] = ordered_sum8(src, world, residual, i);
+  __amdgpu_buffer_rsrc_t rs[kMaxRanks];
+  slot_rsrcs(peers, rank, slot, world, cap, rs);
+  for (int i = t; i < n8; i += kCommThreads)
+    ((uint4*)y)[i] = ordered_sum8(rs, (const uint4*)x, rank, world, residual, i);
   __syncthreads();
   if (t == 0) *seq_ctr = seq;
 }

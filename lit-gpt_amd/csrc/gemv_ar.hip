@@ -40,7 +40,8 @@ __global__ void __launch_bounds__(256) gemv_q4_ar_kernel(GemvArgs a, ArArgs c) {
   static_assert(ROWS % 8 == 0, "16-B pieces of whole rows");
   __shared__ unsigned s_last;
   const int t = threadIdx.x;
-  const unsigned seq = *c.seq + 1u;  // read before arriving: only the last arriver advances it
+  // read before arriving (only the last arriver advances it); uniform, so the mailbox resources stay scalar
+  const unsigned seq = __builtin_amdgcn_readfirstlane(*c.seq + 1u);
   const int slot = seq & 1;
   gemv_q4_body<RPR, CPT, FMT, false, false, false, NW, true>(a, blockIdx.x, smem);
   __syncthreads();
@@ -48,7 +49,8 @@ __global__ void __launch_bounds__(256) gemv_q4_ar_kernel(GemvArgs a, ArArgs c) {
   const int row0 = blockIdx.x * ROWS;
   if (t < c.world * CH) {
     const int r = t / CH, ch = t % CH;
-    if (row0 + ch * 8 < a.N) *(uint4*)(slot_ptr(c.peers.mb[r], slot, c.rank, c.cap) + row0 + ch * 8) = rows[ch];
+    if (row0 + ch * 8 < a.N)
+      st_sys16(mb_rsrc(slot_ptr(c.peers.mb[r], slot, c.rank, c.cap), c.cap * 2), (row0 + ch * 8) * 2, rows[ch]);
   }
   // the pushes are complete (uncached mailboxes: acknowledged = visible) before this workgroup arrives
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -86,9 +88,9 @@ __global__ void __launch_bounds__(256) gemv_q4_ar_kernel(GemvArgs a, ArArgs c) {
   raise_flags(c.peers, c.rank, c.world, seq, t);
   wait_flags(c.peers, c.rank, c.world, seq, c.err, t);
   __syncthreads();
-  const uint4* src[kMaxRanks];
-  for (int r = 0; r < c.world; ++r) src[r] = (const uint4*)slot_ptr(c.peers.mb[c.rank], slot, r, c.cap);
-  for (int i = t; i < a.N / 8; i += NW * 64) ((uint4*)c.y)[i] = ordered_sum8(src, c.world, c.residual, i);
+  __amdgpu_buffer_rsrc_t rs[kMaxRanks];
+  slot_rsrcs(c.peers, c.rank, slot, c.world, c.cap, rs);
+  for (int i = t; i < a.N / 8; i += NW * 64) ((uint4*)c.y)[i] = ordered_sum8(rs, nullptr, -1, c.world, c.residual, i);
   __syncthreads();
   if (t == 0) *c.seq = seq;
 }

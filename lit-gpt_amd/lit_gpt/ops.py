@@ -341,7 +341,9 @@ class AttentionWorkspace:
         nbytes = load_library().lga_attention_workspace_bytes(T, n_head, head_size, n_splits)
         self.key = (T, n_head, n_query_groups, head_size, n_splits)
         self.partials = torch.empty(max(nbytes // 4, 1), dtype=torch.float32, device=device)
-        self.counters = torch.zeros(T * n_query_groups * ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
+        # one counter per (row, query group, head slice): at most n_head of them per row (csrc/attention.hip
+        # attn_hsplit deals a group's heads to up to q_per_kv workgroups when the groups are few)
+        self.counters = torch.zeros(T * n_head * ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
 
 
 def attention(q, k_cache, v_cache, input_pos, n_head, n_query_groups, head_size, scale, n_splits=1,

@@ -640,3 +640,31 @@ def test_routed_expert_gemvs_equal_per_expert_gemvs(ops, fmt, group):
                               group, fmt)
     for s, e in enumerate((3, 1)):
         assert torch.equal(out[s], ops.q4_gemv(act[s].contiguous(), qd[e][0], qd[e][1], K, N, group, fmt))
+
+
+@pytest.mark.parametrize("H,G,splits", [(8, 1, 16), (64, 8, 4), (16, 4, 16)])
+def test_attention_decode_head_slices_agree(ops, H, G, splits, monkeypatch):
+    """A query group's heads dealt to 1, 2, ... q_per_kv workgroups (LGA_ATTN_HSPLIT; by default when the groups
+    are few): the same cache appends bit for bit, outputs within fp32 reordering of each other, and the split
+    counters re-armed (two launches per setting on one workspace)."""
+    hs, S, p = 128, 2304, 2303
+    qkv = to_dev_bf16(synth.normal((1, (H + 2 * G) * hs), "hq", 3, 1.0))
+    k0 = to_dev_bf16(synth.normal((G, S, hs), "hk", 3, 1.0))
+    v0 = to_dev_bf16(synth.normal((G, S, hs), "hv", 3, 1.0))
+    cos, sin = om.build_rope_cache(S, hs, 10000)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pos = torch.tensor([p], device=DEV)
+    scale = 1.0 / math.sqrt(hs)
+    ws = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
+    outs, caches = [], []
+    for h in [x for x in (1, 2, 4, 8) if x <= H // G]:
+        monkeypatch.setenv("LGA_ATTN_HSPLIT", str(h))
+        for _ in range(2):
+            kb, vb = k0.clone(), v0.clone()
+            y = ops.attention_decode_fused(qkv, kb, vb, pos, pos, cos, sin, H, G, hs, hs, scale, n_splits=splits,
+                                           workspace=ws).float()
+        outs.append(y)
+        caches.append((kb, vb))
+    for y, (kb, vb) in zip(outs[1:], caches[1:]):
+        assert torch.equal(kb, caches[0][0]) and torch.equal(vb, caches[0][1])
+        assert torch.all((y - outs[0]).abs() <= outs[0].abs() * 2 ** -7 + 2e-3)
