@@ -47,10 +47,10 @@ __global__ void __launch_bounds__(256) gemv_q4_ar_kernel(GemvArgs a, ArArgs c) {
   __syncthreads();
   const uint4* rows = (const uint4*)gemv_out_lds(smem, a.K);
   const int row0 = blockIdx.x * ROWS;
-  if (t < c.world * CH) {
-    const int r = t / CH, ch = t % CH;
-    if (row0 + ch * 8 < a.N)
-      st_sys16(mb_rsrc(slot_ptr(c.peers.mb[r], slot, c.rank, c.cap), c.cap * 2), (row0 + ch * 8) * 2, rows[ch]);
+  // one peer per iteration: the mailbox resource must be wave-uniform (a lane-dependent peer would need a waterfall)
+  for (int r = 0; r < c.world; ++r) {
+    const __amdgpu_buffer_rsrc_t dst = mb_rsrc(slot_ptr(c.peers.mb[r], slot, c.rank, c.cap), c.cap * 2);
+    if (t < CH && row0 + t * 8 < a.N) st_sys16(dst, (row0 + t * 8) * 2, rows[t]);
   }
   // the pushes are complete (uncached mailboxes: acknowledged = visible) before this workgroup arrives
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -34,7 +34,11 @@ def _launch(worker, nproc, args, timeout=540):
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={port}", str(WORKERS / worker), *map(str, args)]
-    env = dict(os.environ, OMP_NUM_THREADS="2")
+    # every rank is a process on the ONE GPU: one hardware queue each keeps up to 8 processes inside the GPU's
+    # hardware queue slots, so the ranks' flag-waiting kernels run together instead of being time-sliced by the
+    # scheduler (a time-sliced peer looks like a lost one: the 5 s bound and stale-looking bursts). One process per
+    # GPU, the deployment the kernels are built for, never shares the queues.
+    env = dict(os.environ, OMP_NUM_THREADS="2", GPU_MAX_HW_QUEUES="1")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     errors = [ln for ln in r.stderr.splitlines() if "Error" in ln and "ChildFailedError" not in ln]
     assert r.returncode == 0, ("\n".join(errors[:8]), r.stdout[-2000:], r.stderr[-3000:])
