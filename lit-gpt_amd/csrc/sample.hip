@@ -38,6 +38,9 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict
   float bv = -INFINITY;
   int bi = 0x7FFFFFFF;
   int done = 0;
+  // the position is read before the logits (in-order vmcnt: its wait never holds the logit loads back), so the
+  // bookkeeping at the end is a store instead of a dependent load round trip
+  const int64_t p0 = (pos_inout && threadIdx.x == 0) ? *pos_inout : 0;
   if (VEC) {
     const int nvec = n / 8;
     const uint4* lv = (const uint4*)logits;
@@ -82,7 +85,7 @@ __global__ void __launch_bounds__(1024) argmax_kernel(const uint16_t* __restrict
     if (bi >= n) bi = 0;
     if (out_idx) *out_idx = bi;
     if (token_out) *token_out = bi;
-    if (pos_inout) *pos_inout += 1;
+    if (pos_inout) *pos_inout = p0 + 1;
     s_tok = bi;
   }
   if (EMB) {

@@ -75,6 +75,9 @@ class XgmiAllReduce:
         self._agree(failure, "mailbox mapping")
         self._mailboxes = (ctypes.c_void_p * self.world)(*ptrs)
         self._self_test()
+        self.fused_ok = True  # lga_q4_gemv_allreduce passed its own self-test (else linear_reduce uses two launches)
+        self.fused_fallback: Optional[str] = None
+        self._self_test_fused()
 
     def _agree(self, failure: Optional[str], what: str) -> None:
         """All ranks learn whether any rank failed (MIN over a flag); on failure every rank raises."""
@@ -101,6 +104,39 @@ class XgmiAllReduce:
         elif not bool((y.float() == want).all()):
             failure = f"rank {self.rank}: self-test sum wrong ({y.float()[:4].tolist()} vs {want})"
         self._agree(failure, "self-test")
+
+    def _self_test_fused(self, n: int = 512, k: int = 1024, calls: int = 4) -> None:
+        """The fused row-parallel GEMV + all-reduce against the two-launch form (GEMV, then ``all_reduce`` with the
+        residual) it must equal bit for bit: ``calls`` back-to-back launches of per-rank weights. Its cross-GPU
+        hand-off (every workgroup's pushes, then the last arriver's flags) is a different protocol from the one-shot
+        kernel's, so it is checked on its own; when it fails on any rank, every rank keeps the xGMI one-shot
+        all-reduce and only the fusion is dropped (``fused_ok``, ``fused_fallback``)."""
+        import types
+
+        g = torch.Generator().manual_seed(1000 + self.rank)
+        w = (torch.randn(n, k, generator=g) * 0.02).to(self.device)
+        x = torch.randn(k, generator=g).bfloat16().to(self.device)
+        res = torch.randn(n, generator=g).bfloat16().to(self.device)
+        failure = None
+        with torch.cuda.device(self.device):
+            qw, sc = ops.quantize(w, ops.FMT_Q4G, 128)
+            lin = types.SimpleNamespace(out_features=n, in_features=k, qweight=qw, scales=sc, bias=None, group=128,
+                                        fmt=ops.FMT_Q4G)
+            want = self.all_reduce(ops.q4_gemv(x, qw, sc, n, k, 128, ops.FMT_Q4G), residual=res)
+            got = [self.gemv_all_reduce(lin, x, residual=res) for _ in range(calls)]
+            torch.cuda.synchronize(self.device)
+        if self.errors():
+            failure = f"rank {self.rank}: fused GEMV all-reduce self-test timed out waiting for a peer"
+        else:
+            bad = [i for i, y in enumerate(got) if not torch.equal(y, want)]
+            if bad:
+                failure = f"rank {self.rank}: fused GEMV all-reduce differs from GEMV + all-reduce at calls {bad}"
+        flag = torch.tensor([0 if failure else 1], dtype=torch.int32,
+                            device=self.device if dist.get_backend(self.group) == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
+        if int(flag.item()) == 0:
+            self.fused_ok = False
+            self.fused_fallback = failure or "fused GEMV all-reduce self-test failed on another rank"
 
     def supports(self, t: torch.Tensor) -> bool:
         return (t.is_cuda and t.dtype == torch.bfloat16 and t.numel() <= self.cap and t.numel() % 8 == 0
@@ -232,7 +268,8 @@ def linear_reduce(hook, lin: torch.nn.Module, x: torch.Tensor, residual: Optiona
     world = hook.args[0]
     if (comm is not None and comm.world == world and isinstance(lin, QuantLinear) and x.numel() == lin.in_features
             and x.dtype == torch.bfloat16 and x.is_cuda and comm.supports_rows(lin.out_features)
-            and (residual is None or residual.numel() == lin.out_features) and fused_gemv_allreduce):
+            and (residual is None or residual.numel() == lin.out_features) and fused_gemv_allreduce
+            and getattr(comm, "fused_ok", True)):
         y = comm.gemv_all_reduce(lin, x.reshape(-1), residual)
         return y.view(*x.shape[:-1], lin.out_features)
     h = compute()

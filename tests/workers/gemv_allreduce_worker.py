@@ -36,7 +36,7 @@ def main():
         return late_peer(c, out, world, rank)
     if "--time" in sys.argv:
         return timing(c, out, world, rank)
-    bad = []
+    bad = [] if c.fused_ok else [f"start-up self-test: {c.fused_fallback}"]
     # (N, K per rank, mode, bias): 7B attn.proj / mlp.proj shards at this world size, 70B-like widths, fp4 / nf4
     cases = [(4096, 4096 // world, "int4-g128", False), (4096, 11008 // world, "int4-g128", False),
              (8192, 8192 // world, "nf4", False), (4096, 2048, "bnb.fp4", True), (1024, 1376, "int4-g32", False)]
