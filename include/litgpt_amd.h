@@ -156,6 +156,12 @@ int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, co
  * softmax(dim=1, dtype=float).to(bf16) (model.py:738). n_expert <= 8. */
 int lga_moe_route(const void* logits, int T, int n_expert, int k, int32_t* expert_ids, void* probs,
                   lga_stream_t stream);
+/* lga_moe_gate_route: one token's router gate (the 4-bit `self.gate(x)` Linear, model.py:736, optional fused
+ * RMSNorm of x as lga_q4_gemv) and its routing (lga_moe_route) in one launch: expert_ids [k] int32, probs [k] bf16,
+ * bit-identical to lga_q4_gemv (n_expert rows) followed by lga_moe_route. n_expert <= 8, K <= 6144. */
+int lga_moe_gate_route(const void* x, const uint8_t* qweight, const void* scales, const void* norm_weight,
+                       float norm_eps, int n_expert, int K, int group, int fmt, int k, int32_t* expert_ids, void* probs,
+                       lga_stream_t stream);
 /* Routed expert GEMVs (the per-expert `expert(x[token_idx])` calls, model.py:741-742, for one token): slot s
  * (0..n_slots-1) uses expert e = expert_ids[s], whose packed weights / scales start at qweight + e * w_stride
  * bytes / scales + e * s_stride bytes (experts stacked with a uniform stride). lga_q4_gemv_experts reads

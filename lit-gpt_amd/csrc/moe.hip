@@ -5,6 +5,7 @@
 // expert ids[s] only, so a decode step reads k of the E experts and never leaves the device (no host-side
 // torch.where as in the reference loop; the step stays inside one HIP graph).
 #include "common.h"
+#include "gemv_body.h"
 
 namespace lga {
 
@@ -70,15 +71,12 @@ __device__ void topk_order(KV* q, int n, int k) {
   insertion(0, k - 1);
 }
 
-// one thread per token row: top-k of E router logits, fp32 softmax over the k values (ATen's lastdim softmax:
-// exp(v - max), sum, multiply by the reciprocal), bf16 probabilities
-__global__ void moe_route_kernel(const uint16_t* __restrict__ logits, int T, int E, int k, int32_t* __restrict__ ids,
-                                 uint16_t* __restrict__ probs) {
-  const int t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T) return;
+// top-k of one row of E router logits, fp32 softmax over the k values (ATen's lastdim softmax: exp(v - max), sum,
+// multiply by the reciprocal), bf16 probabilities; `row` is global memory or LDS (generic pointer)
+__device__ void route_row(const uint16_t* row, int E, int k, int32_t* __restrict__ ids, uint16_t* __restrict__ probs) {
   KV q[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) q[i] = {i < E ? bf2f(logits[(size_t)t * E + i]) : -INFINITY, i};
+  for (int i = 0; i < 8; ++i) q[i] = {i < E ? bf2f(row[i]) : -INFINITY, i};
   topk_order<8>(q, E, k);
   float mx = q[0].v;
   for (int s = 1; s < k; ++s) mx = fmaxf(mx, q[s].v);
@@ -89,9 +87,50 @@ __global__ void moe_route_kernel(const uint16_t* __restrict__ logits, int T, int
   }
   const float r = 1.0f / sum;
   for (int s = 0; s < k; ++s) {
-    ids[(size_t)t * k + s] = q[s].i;
-    probs[(size_t)t * k + s] = f2bf(e[s] * r);
+    ids[s] = q[s].i;
+    probs[s] = f2bf(e[s] * r);
   }
+}
+
+// one thread per token row
+__global__ void moe_route_kernel(const uint16_t* __restrict__ logits, int T, int E, int k, int32_t* __restrict__ ids,
+                                 uint16_t* __restrict__ probs) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= T) return;
+  route_row(logits + (size_t)t * E, E, k, ids + (size_t)t * k, probs + (size_t)t * k);
+}
+
+// Decode (one token): the router gate GEMV and the routing in ONE single-workgroup launch. The E <= 8 gate rows are
+// the decode GEMV body's (lga_q4_gemv's arithmetic, fused RMSNorm included: 4 waves x 4 rows, rows past E repeat
+// row E-1), left in LDS as the bf16 logits lga_q4_gemv would store; thread 0 then routes them exactly as
+// moe_route_kernel does — the pair lga_q4_gemv + lga_moe_route bit for bit, one launch ramp instead of two.
+template <int CPT, int FMT, bool NORM>
+__global__ void __launch_bounds__(256) moe_gate_route_kernel(GemvArgs a, int k, int32_t* __restrict__ ids,
+                                                             uint16_t* __restrict__ probs) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  gemv_q4_body<4, CPT, FMT, false, NORM, false, 4, true>(a, 0, smem);
+  __syncthreads();
+  if (threadIdx.x == 0) route_row(gemv_out_lds(smem, a.K), a.N, k, ids, probs);
+}
+
+template <int CPT, int FMT>
+static void launch_gate_route(const GemvArgs& a, int k, int32_t* ids, uint16_t* probs, hipStream_t stream) {
+  const size_t lds = gemv_lds_bytes(a.K);
+  if (a.norm_w) moe_gate_route_kernel<CPT, FMT, true><<<1, 256, lds, stream>>>(a, k, ids, probs);
+  else moe_gate_route_kernel<CPT, FMT, false><<<1, 256, lds, stream>>>(a, k, ids, probs);
+}
+
+template <int FMT>
+static int dispatch_gate_route(const GemvArgs& a, int k, int32_t* ids, uint16_t* probs, hipStream_t stream) {
+  switch ((a.K / 32 + 63) / 64) {  // chunks per lane: the same template lga_q4_gemv picks for these shapes
+    case 1: launch_gate_route<1, FMT>(a, k, ids, probs, stream); break;
+    case 2: launch_gate_route<2, FMT>(a, k, ids, probs, stream); break;
+    case 3: launch_gate_route<3, FMT>(a, k, ids, probs, stream); break;
+    default:
+      lga_set_error("lga_moe_gate_route: K must be at most 6144");
+      return (int)hipErrorInvalidValue;
+  }
+  return 0;
 }
 
 // y[t] = residual[t] + sum over slots in ascending expert order of bf16(p * E_slot[t]), each add rounded to bf16
@@ -149,6 +188,24 @@ extern "C" int lga_moe_route(const void* logits, int T, int n_expert, int k, int
                 "lga_moe_route: needs 1 <= k <= n_expert <= 8");
   lga::moe_route_kernel<<<(T + 63) / 64, 64, 0, stream>>>((const uint16_t*)logits, T, n_expert, k, expert_ids,
                                                           (uint16_t*)probs);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_moe_gate_route(const void* x, const uint8_t* qweight, const void* scales, const void* norm_weight,
+                                  float norm_eps, int n_expert, int K, int group, int fmt, int k, int32_t* expert_ids,
+                                  void* probs, hipStream_t stream) {
+  LGA_CHECK_ARG(x && qweight && scales && expert_ids && probs, "lga_moe_gate_route: null pointer");
+  LGA_CHECK_ARG(n_expert > 0 && n_expert <= 8 && k > 0 && k <= n_expert,
+                "lga_moe_gate_route: needs 1 <= k <= n_expert <= 8");
+  LGA_CHECK_ARG(K > 0 && K % 32 == 0 && K <= 6144, "lga_moe_gate_route: K must be a multiple of 32, at most 6144");
+  LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_moe_gate_route: bad group");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_moe_gate_route: fmt must be 0 (int4-g), 1 (nf4) or 3 (fp4)");
+  lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, nullptr, nullptr,
+                  (const uint16_t*)norm_weight, nullptr, n_expert, K, group, norm_eps};
+  a.cb = lga::codebook_of(fmt);
+  const int rc = fmt == 0 ? lga::dispatch_gate_route<0>(a, k, expert_ids, (uint16_t*)probs, stream)
+                          : lga::dispatch_gate_route<1>(a, k, expert_ids, (uint16_t*)probs, stream);
+  if (rc) return rc;
   LGA_LAUNCH_RETURN();
 }
 
@@ -231,5 +288,6 @@ extern "C" int lga_moe_group(const int32_t* expert_ids, int T, int k, int n_expe
 
 int lga::preload_moe() {  // the sparse-MoE prefill's routing, grouping and combine kernels
   return lga::preload(lga::moe_route_kernel) + lga::preload(lga::moe_combine_kernel) +
-         lga::preload(lga::moe_group_kernel);
+         lga::preload(lga::moe_group_kernel) + lga::preload(lga::moe_gate_route_kernel<2, 0, true>) +
+         lga::preload(lga::moe_gate_route_kernel<2, 1, true>);
 }

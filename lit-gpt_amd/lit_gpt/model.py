@@ -439,6 +439,11 @@ class LLaMAMLP(nn.Module):
         return out.view(*lead, -1)
 
 
+# decode routing through the fused gate + route launch (lga_moe_gate_route); False keeps lga_q4_gemv + lga_moe_route
+# (tests A/B the two)
+moe_gate_route = True
+
+
 class LLaMAMoE(nn.Module):
     """Sparse MoE (lit_gpt/model.py:719-743): router gate, top-k experts per token, prob-weighted bf16 sum.
 
@@ -493,6 +498,15 @@ class LLaMAMoE(nn.Module):
         return bool(ops.q4f_fits(64, f1.out_features, C, f1.group, f1.fmt)
                     and ops.q4f_fits(64, pj.out_features, pj.in_features, pj.group, pj.fmt))
 
+    def _gate_route_ok(self, C: int) -> bool:
+        """One-token routing through ``lga_moe_gate_route``: a bias-free 4-bit gate without forward hooks (the
+        reference's TP keeps the gate replicated and hook-free, generate/tp.py:58-62) whose shape the kernel takes."""
+        from lit_gpt.quantize import QuantLinear
+
+        g = self.gate
+        return (moe_gate_route and isinstance(g, QuantLinear) and g.bias is None and not g._forward_hooks
+                and g.in_features == C and ops.moe_gate_route_fits(g.out_features, C))
+
     def _expert_hooks(self, x: torch.Tensor, eout: torch.Tensor) -> torch.Tensor:
         hooks = [list(e._forward_hooks.values()) for e in self.experts]
         if any(len(h) != len(hooks[0]) for h in hooks):
@@ -516,8 +530,13 @@ class LLaMAMoE(nn.Module):
             xin = x2 if (norm is None or fuse_norm) else norm(x2)
             nw = norm.weight if fuse_norm else None
             eps = norm.eps if fuse_norm else 1e-5
-            router = _lin(self.gate, xin, norm_weight=nw, norm_eps=eps).view(1, E)
-            ids, probs = ops.moe_route(router, k)
+            if self._gate_route_ok(C):  # gate GEMV + routing in one launch (same bits as the pair below)
+                g = self.gate
+                ids, probs = ops.moe_gate_route(xin.view(-1), g.qweight, g.scales, E, C, g.group, g.fmt, k,
+                                                norm_weight=nw, eps=eps)
+            else:
+                router = _lin(self.gate, xin, norm_weight=nw, norm_eps=eps).view(1, E)
+                ids, probs = ops.moe_route(router, k)
             act = ops.q4_gemv_swiglu_experts(xin.view(-1), q1, s1, q2, s2, ids.view(-1), f1.out_features, C,
                                              f1.group, f1.fmt, norm_weight=nw, eps=eps)
             eout = ops.q4_gemv_experts(act, qp, sp, ids.view(-1), pj.out_features, pj.in_features, pj.group,

@@ -65,6 +65,7 @@ SIGNATURES = {
     "lga_argmax": [_P, _I, _P, _P, _P, _P],
     "lga_argmax_embed": [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P],
     "lga_moe_route": [_P, _I, _I, _I, _P, _P, _P],
+    "lga_moe_gate_route": [_P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P],
     "lga_q4_gemv_experts": [_P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _I, _P, _I, _I, _I, _I,
                             _I, _P],
     "lga_q4_gemv_swiglu_experts": [_P, _P, _P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _F,
@@ -572,6 +573,24 @@ def moe_route(logits, k, ids=None, probs=None):
     probs = probs if probs is not None else torch.empty(T, k, dtype=torch.bfloat16, device=logits.device)
     _check(load_library().lga_moe_route(_dev(logits, "logits", torch.bfloat16), T, E, k, _dev(ids, "ids", torch.int32),
                                         _dev(probs, "probs", torch.bfloat16), _stream()))
+    return ids, probs
+
+
+def moe_gate_route_fits(n_expert: int, K: int) -> bool:
+    """Whether lga_moe_gate_route takes this router gate (E <= 8 rows, K <= 6144, K % 32 == 0)."""
+    return 0 < n_expert <= 8 and K % 32 == 0 and 0 < K <= 6144
+
+
+def moe_gate_route(x, qweight, scales, n_expert, K, group, fmt, k, *, norm_weight=None, eps=1e-5, ids=None,
+                   probs=None):
+    """One token: router logits = gate(x) (4-bit GEMV, optional fused RMSNorm) and their routing in ONE launch ->
+    (ids (1, k) int32, probs (1, k) bf16), bit-identical to q4_gemv + moe_route (lit_gpt/model.py:736-738)."""
+    ids = ids if ids is not None else torch.empty(1, k, dtype=torch.int32, device=x.device)
+    probs = probs if probs is not None else torch.empty(1, k, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_moe_gate_route(_dev(x, "x", torch.bfloat16), _dev(qweight, "qweight", torch.uint8),
+                                             _dev(scales, "scales"), _opt(norm_weight, "norm_weight", torch.bfloat16),
+                                             float(eps), n_expert, K, group, fmt, k, _dev(ids, "ids", torch.int32),
+                                             _dev(probs, "probs", torch.bfloat16), _stream()))
     return ids, probs
 
 

@@ -596,6 +596,39 @@ def test_moe_route_matches_cpu_topk_on_ties(ops):
             assert int(d.max()) <= 1, (E, k)
 
 
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (3, 64), (0, 32)])
+@pytest.mark.parametrize("K", [4096, 1024, 6144, 2080])
+def test_moe_gate_route_matches_gemv_then_route(ops, fmt, group, K):
+    """lga_moe_gate_route (one launch) == lga_q4_gemv of the gate rows + lga_moe_route, bit for bit: with and without
+    the fused RMSNorm, 4 / 6 / 8 experts, k = 1 / 2, and gate rows duplicated so the router logits tie."""
+    if K % group:
+        pytest.skip("K must be a multiple of the group")
+    g = torch.Generator().manual_seed(K + fmt)
+    for E in (8, 6, 4):
+        w = torch.randn(E, K, generator=g) * 0.02
+        if E == 8:
+            w[5] = w[2]  # tied logits: the CPU torch.topk tie order decides
+        qw, sc = ops.quantize(w.to(DEV), fmt, group)
+        for norm in (False, True):
+            x = torch.randn(K, generator=g).bfloat16().to(DEV)
+            nw = (1.0 + 0.1 * torch.randn(K, generator=g)).bfloat16().to(DEV) if norm else None
+            router = ops.q4_gemv(x, qw, sc, E, K, group, fmt, norm_weight=nw, eps=1e-5)
+            for k in (1, 2):
+                ids0, p0 = ops.moe_route(router.view(1, E), k)
+                ids1, p1 = ops.moe_gate_route(x, qw, sc, E, K, group, fmt, k, norm_weight=nw, eps=1e-5)
+                assert torch.equal(ids0, ids1), (E, norm, k, ids0, ids1)
+                assert torch.equal(p0.view(torch.int16), p1.view(torch.int16)), (E, norm, k)
+
+
+def test_moe_gate_route_rejects_bad_shapes(ops):
+    x = torch.zeros(8192, dtype=torch.bfloat16, device=DEV)
+    qw, sc = ops.quantize(torch.zeros(8, 8192, device=DEV), 0, 128)
+    with pytest.raises(RuntimeError, match="6144"):
+        ops.moe_gate_route(x, qw, sc, 8, 8192, 128, 0, 2)
+    with pytest.raises(RuntimeError, match="n_expert"):
+        ops.moe_gate_route(x[:4096], qw, sc, 9, 4096, 128, 0, 2)
+
+
 def test_moe_combine_matches_reference_loop(ops):
     """y[tok] += probs * expert_out in ascending expert order, bf16 arithmetic (model.py:739-742) + residual."""
     T, k, C = 9, 2, 4096

@@ -92,7 +92,8 @@ def _watch_router_margins(ref, choices=None):
 
 
 class _GpuRoutes:
-    """Records the expert sets the product's router kernel (ops.moe_route) picked, per call (eager runs only)."""
+    """Records the expert sets the product's router kernels (ops.moe_route, and ops.moe_gate_route at decode) picked,
+    per call (eager runs only)."""
 
     def __init__(self):
         self.calls = []
@@ -100,18 +101,23 @@ class _GpuRoutes:
     def __enter__(self):
         from lit_gpt import ops
 
-        self._ops, self._orig = ops, ops.moe_route
+        self._ops = ops
+        self._orig = {name: getattr(ops, name) for name in ("moe_route", "moe_gate_route")}
 
-        def wrapped(*a, **kw):
-            ids, probs = self._orig(*a, **kw)
-            self.calls.append(torch.sort(ids.detach().long().cpu(), dim=-1).values)
-            return ids, probs
+        def wrap(fn):
+            def wrapped(*a, **kw):
+                ids, probs = fn(*a, **kw)
+                self.calls.append(torch.sort(ids.detach().long().cpu(), dim=-1).values)
+                return ids, probs
+            return wrapped
 
-        ops.moe_route = wrapped
+        for name, fn in self._orig.items():
+            setattr(ops, name, wrap(fn))
         return self
 
     def __exit__(self, *exc):
-        self._ops.moe_route = self._orig
+        for name, fn in self._orig.items():
+            setattr(self._ops, name, fn)
 
 
 def _routing_ambiguous(margins, tol=2 ** -6):
@@ -250,6 +256,41 @@ def test_kv_cache_matches_no_cache_forward():
         inc.append(model(ids[t:t + 1].view(1, 1), torch.tensor([t], device=DEV))[0].float())
     inc = torch.cat(inc)
     assert (inc - full).abs().max().item() <= 0.03 * full.abs().max().item()
+
+
+@pytest.mark.parametrize("mode", ["int4-g128", "nf4"])
+@torch.inference_mode()
+def test_moe_decode_fused_gate_route_bit_identical(mode, monkeypatch):
+    """The sparse-MoE decode step with the gate GEMV and the routing in one launch (lga_moe_gate_route) produces the
+    same logits, bit for bit, as the two-launch form (lga_q4_gemv + lga_moe_route), and actually takes the fused
+    route."""
+    from lit_gpt import model as lm
+    from lit_gpt import ops
+
+    cfg = _cfg("moe")
+    sd = synth.state_dict(cfg, seed=51)
+    T, N = 12, 6
+    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=51)).to(DEV)
+    stream = torch.from_numpy(synth.token_ids(N, cfg.vocab_size, seed=52)).to(DEV)
+    calls = []
+    orig = ops.moe_gate_route
+
+    def counted(*a, **kw):
+        calls.append(1)
+        return orig(*a, **kw)
+
+    monkeypatch.setattr(ops, "moe_gate_route", counted)
+    outs = {}
+    for fused in (True, False):
+        monkeypatch.setattr(lm, "moe_gate_route", fused)
+        model = build_gpu_model(cfg, sd, mode, T + N)
+        got = [model(prompt.view(1, -1), torch.arange(T, device=DEV))[0, -1]]
+        for i in range(N):
+            got.append(model(stream[i:i + 1].view(1, 1), torch.tensor([T + i], device=DEV))[0, -1])
+        outs[fused] = torch.stack(got).cpu()
+        if fused:
+            assert len(calls) == N * cfg.n_layer, "decode did not take lga_moe_gate_route"
+    assert torch.equal(outs[True].view(torch.int16), outs[False].view(torch.int16))
 
 
 @torch.inference_mode()
