@@ -162,6 +162,13 @@ int lga_moe_route(const void* logits, int T, int n_expert, int k, int32_t* exper
 int lga_moe_gate_route(const void* x, const uint8_t* qweight, const void* scales, const void* norm_weight,
                        float norm_eps, int n_expert, int K, int group, int fmt, int k, int32_t* expert_ids, void* probs,
                        lga_stream_t stream);
+/* lga_q4_gemv_experts_combine: one token, k = 2 — the routed proj GEMVs of both slots (x [2][K], expert_ids [2],
+ * weights stacked as lga_q4_gemv_experts) and lga_moe_combine with the residual in one launch:
+ * y [N] = residual + sum in ascending expert id of bf16(probs[s] * expert_out[s]), bit-identical to
+ * lga_q4_gemv_experts + lga_moe_combine. N < 24000, K <= 16384. */
+int lga_q4_gemv_experts_combine(const void* x, const uint8_t* qweight, const void* scales, const int32_t* expert_ids,
+                                const void* probs, const void* residual, int n_expert, long long w_stride,
+                                long long s_stride, void* y, int N, int K, int group, int fmt, lga_stream_t stream);
 /* Routed expert GEMVs (the per-expert `expert(x[token_idx])` calls, model.py:741-742, for one token): slot s
  * (0..n_slots-1) uses expert e = expert_ids[s], whose packed weights / scales start at qweight + e * w_stride
  * bytes / scales + e * s_stride bytes (experts stacked with a uniform stride). lga_q4_gemv_experts reads

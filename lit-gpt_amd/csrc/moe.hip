@@ -113,6 +113,47 @@ __global__ void __launch_bounds__(256) moe_gate_route_kernel(GemvArgs a, int k, 
   if (threadIdx.x == 0) route_row(gemv_out_lds(smem, a.K), a.N, k, ids, probs);
 }
 
+// Decode (one token, k = 2): the routed proj GEMVs of both experts and lga_moe_combine in ONE launch. A workgroup
+// computes its rows for both experts (each against its own SwiGLU input), so no partial leaves the workgroup before
+// the weighted sum: y = residual + bf16 sum in ascending expert id of bf16(p * expert_out), bit-identical to
+// lga_q4_gemv_experts + lga_moe_combine (the rows / chunks per lane are the ones lga_q4_gemv picks for the shape).
+template <int RPR, int CPT, int FMT>
+__global__ void __launch_bounds__(1024) moe_down_combine_kernel(GemvArgs a, const int32_t* __restrict__ ids) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const long long e0 = min(max(ids[0], 0), a.n_expert - 1), e1 = min(max(ids[1], 0), a.n_expert - 1);
+  a.moe_swap = ids[1] < ids[0];  // lga_moe_combine's stable order by expert id
+  a.qw2 = a.qw + e1 * a.ew;
+  a.sc2 = (const unsigned char*)a.sc + e1 * a.es;
+  a.qw += e0 * a.ew;
+  a.sc = (const unsigned char*)a.sc + e0 * a.es;
+  gemv_q4_body<RPR, CPT, FMT, false, false, true, 16, false, true>(a, blockIdx.x, smem);
+}
+
+template <int RPR, int CPT, int FMT>
+static void launch_down_combine(const GemvArgs& a, const int32_t* ids, hipStream_t stream) {
+  // 16 waves, 8 per expert: 8 * RPR rows per workgroup, one workgroup per CU (both inputs staged in LDS)
+  const int blocks = (a.N + 8 * RPR - 1) / (8 * RPR);
+  moe_down_combine_kernel<RPR, CPT, FMT><<<blocks, 1024, gemv_moe2_lds_bytes(a.K), stream>>>(a, ids);
+}
+
+template <int FMT>
+static int dispatch_down_combine(const GemvArgs& a, const int32_t* ids, hipStream_t stream) {
+  switch ((a.K / 32 + 63) / 64) {  // gemv.hip dispatch's (rows per wave, chunks per lane) for one-expert rows < 24000
+    case 1: launch_down_combine<4, 1, FMT>(a, ids, stream); break;
+    case 2: launch_down_combine<4, 2, FMT>(a, ids, stream); break;
+    case 3: launch_down_combine<4, 3, FMT>(a, ids, stream); break;
+    case 4: launch_down_combine<2, 4, FMT>(a, ids, stream); break;
+    case 5:
+    case 6: launch_down_combine<2, 6, FMT>(a, ids, stream); break;
+    case 7:
+    case 8: launch_down_combine<2, 8, FMT>(a, ids, stream); break;
+    default:
+      lga_set_error("lga_q4_gemv_experts_combine: K must be at most 16384");
+      return (int)hipErrorInvalidValue;
+  }
+  return 0;
+}
+
 template <int CPT, int FMT>
 static void launch_gate_route(const GemvArgs& a, int k, int32_t* ids, uint16_t* probs, hipStream_t stream) {
   const size_t lds = gemv_lds_bytes(a.K);
@@ -209,6 +250,28 @@ extern "C" int lga_moe_gate_route(const void* x, const uint8_t* qweight, const v
   LGA_LAUNCH_RETURN();
 }
 
+extern "C" int lga_q4_gemv_experts_combine(const void* x, const uint8_t* qweight, const void* scales,
+                                           const int32_t* expert_ids, const void* probs, const void* residual,
+                                           int n_expert, long long w_stride, long long s_stride, void* y, int N, int K,
+                                           int group, int fmt, hipStream_t stream) {
+  LGA_CHECK_ARG(x && qweight && scales && expert_ids && probs && residual && y,
+                "lga_q4_gemv_experts_combine: null pointer");
+  LGA_CHECK_ARG(N > 0 && N < 24000 && K > 0 && K % 32 == 0 && K <= 16384,
+                "lga_q4_gemv_experts_combine: needs N < 24000 and K a multiple of 32, at most 16384");
+  LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv_experts_combine: bad group");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_q4_gemv_experts_combine: fmt must be 0, 1 or 3");
+  LGA_CHECK_ARG(n_expert > 0 && w_stride >= (long long)N * K / 2 && s_stride > 0,
+                "lga_q4_gemv_experts_combine: bad expert geometry");
+  lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, nullptr, (const uint16_t*)residual, nullptr,
+                  (uint16_t*)y, N, K, group, 0.0f, nullptr, w_stride, s_stride, K, n_expert, 2};
+  a.cb = lga::codebook_of(fmt);
+  a.probs = (const uint16_t*)probs;
+  const int rc = fmt == 0 ? lga::dispatch_down_combine<0>(a, expert_ids, stream)
+                          : lga::dispatch_down_combine<1>(a, expert_ids, stream);
+  if (rc) return rc;
+  LGA_LAUNCH_RETURN();
+}
+
 extern "C" int lga_moe_combine(const void* expert_out, const void* probs, const int32_t* expert_ids,
                                const void* residual, void* y, int T, int k, int C, hipStream_t stream) {
   LGA_CHECK_ARG(expert_out && probs && expert_ids && y, "lga_moe_combine: null pointer");
@@ -289,5 +352,5 @@ extern "C" int lga_moe_group(const int32_t* expert_ids, int T, int k, int n_expe
 int lga::preload_moe() {  // the sparse-MoE prefill's routing, grouping and combine kernels
   return lga::preload(lga::moe_route_kernel) + lga::preload(lga::moe_combine_kernel) +
          lga::preload(lga::moe_group_kernel) + lga::preload(lga::moe_gate_route_kernel<2, 0, true>) +
-         lga::preload(lga::moe_gate_route_kernel<2, 1, true>);
+         lga::preload(lga::moe_gate_route_kernel<2, 1, true>) + lga::preload(lga::moe_down_combine_kernel<2, 8, 0>);
 }

@@ -442,6 +442,9 @@ class LLaMAMLP(nn.Module):
 # decode routing through the fused gate + route launch (lga_moe_gate_route); False keeps lga_q4_gemv + lga_moe_route
 # (tests A/B the two)
 moe_gate_route = True
+# decode k = 2: routed proj GEMVs + combine in one launch (lga_q4_gemv_experts_combine); False keeps
+# lga_q4_gemv_experts + lga_moe_combine (tests A/B the two)
+moe_fused_combine = True
 
 
 class LLaMAMoE(nn.Module):
@@ -539,6 +542,11 @@ class LLaMAMoE(nn.Module):
                 ids, probs = ops.moe_route(router, k)
             act = ops.q4_gemv_swiglu_experts(xin.view(-1), q1, s1, q2, s2, ids.view(-1), f1.out_features, C,
                                              f1.group, f1.fmt, norm_weight=nw, eps=eps)
+            if (moe_fused_combine and res is not None and not any(e._forward_hooks for e in self.experts)
+                    and ops.q4_gemv_experts_combine_fits(k, pj.out_features, pj.in_features)):
+                # the routed proj GEMVs and the combine (+ residual) in one launch, same bits as the three below
+                return ops.q4_gemv_experts_combine(act, qp, sp, ids.view(-1), probs.view(-1), res.view(-1),
+                                                   pj.out_features, pj.in_features, pj.group, pj.fmt).view(*lead, C)
             eout = ops.q4_gemv_experts(act, qp, sp, ids.view(-1), pj.out_features, pj.in_features, pj.group,
                                        pj.fmt).view(1, k, C)
         else:

@@ -66,6 +66,8 @@ SIGNATURES = {
     "lga_argmax_embed": [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P],
     "lga_moe_route": [_P, _I, _I, _I, _P, _P, _P],
     "lga_moe_gate_route": [_P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P],
+    "lga_q4_gemv_experts_combine": [_P, _P, _P, _P, _P, _P, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _I, _I, _I,
+                                    _I, _P],
     "lga_q4_gemv_experts": [_P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _I, _P, _I, _I, _I, _I,
                             _I, _P],
     "lga_q4_gemv_swiglu_experts": [_P, _P, _P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _F,
@@ -609,6 +611,26 @@ def q4_gemv_experts(x, qweight, scales, ids, N, K, group, fmt, *, out=None, vari
                                               _dev(scales, "scales"), _dev(ids, "ids", torch.int32), k,
                                               qweight.size(0), ws, ss, K, _dev(y, "y", torch.bfloat16), N, K, group,
                                               fmt, variant, _stream()))
+    return y
+
+
+def q4_gemv_experts_combine_fits(k: int, N: int, K: int) -> bool:
+    """Whether lga_q4_gemv_experts_combine takes this routed proj (k = 2 slots, N < 24000, K <= 16384)."""
+    return k == 2 and 0 < N < 24000 and K % 32 == 0 and 0 < K <= 16384
+
+
+def q4_gemv_experts_combine(x, qweight, scales, ids, probs, residual, N, K, group, fmt, *, out=None):
+    """One token, k = 2: y (N,) = residual + the two routed experts' proj outputs weighted by ``probs`` and summed
+    in ascending expert id with the bf16 rounding points of lga_moe_combine — bit-identical to q4_gemv_experts +
+    moe_combine, in one launch. x (2, K): each slot's input; W stacked (E, N, K/2)."""
+    if ids.numel() != 2 or probs.numel() != 2 or x.numel() != 2 * K or residual.numel() != N:
+        raise ValueError("q4_gemv_experts_combine: needs 2 slots (ids, probs, x of 2 x K) and a residual of N")
+    ws, ss = _expert_strides(qweight, scales)
+    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_q4_gemv_experts_combine(
+        _dev(x, "x", torch.bfloat16), _dev(qweight, "qweight", torch.uint8), _dev(scales, "scales"),
+        _dev(ids, "ids", torch.int32), _dev(probs, "probs", torch.bfloat16), _dev(residual, "residual", torch.bfloat16),
+        qweight.size(0), ws, ss, _dev(y, "y", torch.bfloat16), N, K, group, fmt, _stream()))
     return y
 
 

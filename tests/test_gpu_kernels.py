@@ -620,6 +620,33 @@ def test_moe_gate_route_matches_gemv_then_route(ops, fmt, group, K):
                 assert torch.equal(p0.view(torch.int16), p1.view(torch.int16)), (E, norm, k)
 
 
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (3, 64), (0, 32)])
+@pytest.mark.parametrize("N,K", [(4096, 14336), (512, 384), (1000, 2080), (768, 4096), (640, 6144), (512, 11008)])
+def test_experts_combine_matches_gemv_then_combine(ops, fmt, group, N, K):
+    """lga_q4_gemv_experts_combine (one launch) == lga_q4_gemv_experts + lga_moe_combine (+ residual), bit for bit:
+    both slot orders (the lower expert id added first), rows past a 16-row tile, every chunks-per-lane template."""
+    if K % group:
+        pytest.skip("K must be a multiple of the group")
+    g = torch.Generator().manual_seed(N + K + fmt)
+    E = 8
+    qw, sc = [], []
+    for e in range(E):
+        q, s_ = ops.quantize((torch.randn(N, K, generator=g) * 0.02).to(DEV), fmt, group)
+        qw.append(q)
+        sc.append(s_)
+    qw, sc = torch.stack(qw), torch.stack(sc)
+    for pair in ((1, 6), (6, 1), (0, 7)):
+        ids = torch.tensor(pair, dtype=torch.int32, device=DEV)
+        x = torch.randn(2, K, generator=g).bfloat16().to(DEV)
+        probs = torch.softmax(torch.randn(2, generator=g), 0).bfloat16().to(DEV)
+        res = (torch.randn(N, generator=g) * 2).bfloat16().to(DEV)
+        eout = ops.q4_gemv_experts(x, qw, sc, ids, N, K, group, fmt)
+        want = ops.moe_combine(eout.view(1, 2, N).contiguous(), probs.view(1, 2), ids.view(1, 2),
+                               residual=res.view(1, N)).view(-1)
+        got = ops.q4_gemv_experts_combine(x, qw, sc, ids, probs, res, N, K, group, fmt)
+        assert torch.equal(got.view(torch.int16), want.view(torch.int16)), (pair, (got.float() - want.float()).abs().max())
+
+
 def test_moe_gate_route_rejects_bad_shapes(ops):
     x = torch.zeros(8192, dtype=torch.bfloat16, device=DEV)
     qw, sc = ops.quantize(torch.zeros(8, 8192, device=DEV), 0, 128)
