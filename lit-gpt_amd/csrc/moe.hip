@@ -72,32 +72,32 @@ __device__ void topk_order(KV* q, int n, int k) {
 }
 
 // top-k of one row of E router logits, fp32 softmax over the k values (ATen's lastdim softmax: exp(v - max), sum,
-// multiply by the reciprocal), bf16 probabilities; `row` is global memory or LDS (generic pointer)
-__device__ void route_row(const uint16_t* row, int E, int k, int32_t* __restrict__ ids, uint16_t* __restrict__ probs) {
-  KV q[8];
+// multiply by the reciprocal), bf16 probabilities; `row` is global memory or LDS (generic pointer). The selection
+// works on q[8] in LDS: its data-dependent indexing would put a register array in scratch (a memory round trip per
+// access); each exp is evaluated twice (same input, same bits) instead of being kept in such an array.
+__device__ void route_row(const uint16_t* row, int E, int k, int32_t* __restrict__ ids, uint16_t* __restrict__ probs,
+                          KV* q) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) q[i] = {i < E ? bf2f(row[i]) : -INFINITY, i};
   topk_order<8>(q, E, k);
   float mx = q[0].v;
   for (int s = 1; s < k; ++s) mx = fmaxf(mx, q[s].v);
-  float e[8], sum = 0.0f;
-  for (int s = 0; s < k; ++s) {
-    e[s] = expf(q[s].v - mx);
-    sum += e[s];
-  }
+  float sum = 0.0f;
+  for (int s = 0; s < k; ++s) sum += expf(q[s].v - mx);
   const float r = 1.0f / sum;
   for (int s = 0; s < k; ++s) {
     ids[s] = q[s].i;
-    probs[s] = f2bf(e[s] * r);
+    probs[s] = f2bf(expf(q[s].v - mx) * r);
   }
 }
 
 // one thread per token row
-__global__ void moe_route_kernel(const uint16_t* __restrict__ logits, int T, int E, int k, int32_t* __restrict__ ids,
-                                 uint16_t* __restrict__ probs) {
+__global__ void __launch_bounds__(64) moe_route_kernel(const uint16_t* __restrict__ logits, int T, int E, int k,
+                                                       int32_t* __restrict__ ids, uint16_t* __restrict__ probs) {
+  __shared__ KV sq[64][8];
   const int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= T) return;
-  route_row(logits + (size_t)t * E, E, k, ids + (size_t)t * k, probs + (size_t)t * k);
+  route_row(logits + (size_t)t * E, E, k, ids + (size_t)t * k, probs + (size_t)t * k, sq[threadIdx.x]);
 }
 
 // Decode (one token): the router gate GEMV and the routing in ONE single-workgroup launch. The E <= 8 gate rows are
@@ -108,9 +108,10 @@ template <int CPT, int FMT, bool NORM>
 __global__ void __launch_bounds__(256) moe_gate_route_kernel(GemvArgs a, int k, int32_t* __restrict__ ids,
                                                              uint16_t* __restrict__ probs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ KV sq[8];
   gemv_q4_body<4, CPT, FMT, false, NORM, false, 4, true>(a, 0, smem);
   __syncthreads();
-  if (threadIdx.x == 0) route_row(gemv_out_lds(smem, a.K), a.N, k, ids, probs);
+  if (threadIdx.x == 0) route_row(gemv_out_lds(smem, a.K), a.N, k, ids, probs, sq);
 }
 
 // Decode (one token, k = 2): the routed proj GEMVs of both experts and lga_moe_combine in ONE launch. A workgroup
