@@ -4,6 +4,8 @@
 // The expert GEMVs themselves are lga_q4_gemv(_swiglu)_experts (gemv.hip): slot s of a token streams the weights of
 // expert ids[s] only, so a decode step reads k of the E experts and never leaves the device (no host-side
 // torch.where as in the reference loop; the step stays inside one HIP graph).
+#include <cstdlib>
+
 #include "common.h"
 #include "gemv_body.h"
 
@@ -118,8 +120,9 @@ __global__ void __launch_bounds__(256) moe_gate_route_kernel(GemvArgs a, int k, 
 // computes its rows for both experts (each against its own SwiGLU input), so no partial leaves the workgroup before
 // the weighted sum: y = residual + bf16 sum in ascending expert id of bf16(p * expert_out), bit-identical to
 // lga_q4_gemv_experts + lga_moe_combine (the rows / chunks per lane are the ones lga_q4_gemv picks for the shape).
-template <int RPR, int CPT, int FMT>
-__global__ void __launch_bounds__(1024) moe_down_combine_kernel(GemvArgs a, const int32_t* __restrict__ ids) {
+template <int RPR, int CPT, int FMT, int NW = 16>
+__global__ void __launch_bounds__(NW * 64, NW == 8 ? 4 : 1) moe_down_combine_kernel(GemvArgs a,
+                                                                                 const int32_t* __restrict__ ids) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const long long e0 = min(max(ids[0], 0), a.n_expert - 1), e1 = min(max(ids[1], 0), a.n_expert - 1);
   a.moe_swap = ids[1] < ids[0];  // lga_moe_combine's stable order by expert id
@@ -127,12 +130,17 @@ __global__ void __launch_bounds__(1024) moe_down_combine_kernel(GemvArgs a, cons
   a.sc2 = (const unsigned char*)a.sc + e1 * a.es;
   a.qw += e0 * a.ew;
   a.sc = (const unsigned char*)a.sc + e0 * a.es;
-  gemv_q4_body<RPR, CPT, FMT, false, false, true, 16, false, true>(a, blockIdx.x, smem);
+  gemv_q4_body<RPR, CPT, FMT, false, false, true, NW, false, true>(a, blockIdx.x, smem);
 }
 
 template <int RPR, int CPT, int FMT>
 static void launch_down_combine(const GemvArgs& a, const int32_t* ids, hipStream_t stream) {
   // 16 waves, 8 per expert: 8 * RPR rows per workgroup, one workgroup per CU (both inputs staged in LDS)
+  static const int nw = getenv("LGA_MOE_NW") ? atoi(getenv("LGA_MOE_NW")) : 16;  // lab A/B: 8 = two 8-wave workgroups per CU
+  if (nw == 8) {
+    moe_down_combine_kernel<RPR, CPT, FMT, 8><<<(a.N + 4 * RPR - 1) / (4 * RPR), 512, gemv_moe2_lds_bytes(a.K), stream>>>(a, ids);
+    return;
+  }
   const int blocks = (a.N + 8 * RPR - 1) / (8 * RPR);
   moe_down_combine_kernel<RPR, CPT, FMT><<<blocks, 1024, gemv_moe2_lds_bytes(a.K), stream>>>(a, ids);
 }

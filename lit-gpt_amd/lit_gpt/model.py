@@ -444,7 +444,7 @@ class LLaMAMLP(nn.Module):
 moe_gate_route = True
 # decode k = 2: routed proj GEMVs + combine in one launch (lga_q4_gemv_experts_combine); False keeps
 # lga_q4_gemv_experts + lga_moe_combine (tests A/B the two)
-moe_fused_combine = True
+moe_fused_combine = os.environ.get("LGA_MOE_FUSED_COMBINE", "1") != "0"
 
 
 class LLaMAMoE(nn.Module):
