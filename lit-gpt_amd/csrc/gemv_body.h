@@ -49,6 +49,7 @@ struct GemvArgs {
   // probs = the 2 routing probabilities, moe_swap = slot 1's expert id is the lower (it is added first)
   const uint16_t* probs = nullptr;
   int moe_swap = 0;
+  float moe_pa = 0.0f, moe_pb = 0.0f;  // MOE2: the probabilities in addition order (read at kernel start)
 };
 
 // LDS of gemv_q4_body: x pairs (2K B), chunk sums (K/32 floats), norm partials (16), codebook (16), then (LDS_OUT)
@@ -285,10 +286,9 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
     if (slot == 0) {
       const float e0 = bf2f(ex[lr]), e1 = bf2f(ex[(NW / 2) * RPR + lr]);
       const float ea = a.moe_swap ? e1 : e0, eb = a.moe_swap ? e0 : e1;
-      const float pa = bf2f(a.probs[a.moe_swap ? 1 : 0]), pb = bf2f(a.probs[a.moe_swap ? 0 : 1]);
       float acc = 0.0f;
-      acc = round_bf(acc + round_bf(pa * ea));
-      acc = round_bf(acc + round_bf(pb * eb));
+      acc = round_bf(acc + round_bf(a.moe_pa * ea));
+      acc = round_bf(acc + round_bf(a.moe_pb * eb));
       acc = __uint_as_float(((uint32_t)__shfl(res, vi)) << 16) + acc;
       if ((lane & (GROUP - 1)) == 0 && row < a.N) a.y[row] = f2bf(acc);
     }

@@ -126,6 +126,9 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 4 : 1) moe_down_combine_ker
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const long long e0 = min(max(ids[0], 0), a.n_expert - 1), e1 = min(max(ids[1], 0), a.n_expert - 1);
   a.moe_swap = ids[1] < ids[0];  // lga_moe_combine's stable order by expert id
+  // the probabilities are read here, with the ids (scalar loads), not after the GEMV (a dependent round trip there)
+  a.moe_pa = bf2f(a.probs[a.moe_swap ? 1 : 0]);
+  a.moe_pb = bf2f(a.probs[a.moe_swap ? 0 : 1]);
   a.qw2 = a.qw + e1 * a.ew;
   a.sc2 = (const unsigned char*)a.sc + e1 * a.es;
   a.qw += e0 * a.ew;
