@@ -442,9 +442,9 @@ class LLaMAMLP(nn.Module):
 # decode routing through the fused gate + route launch (lga_moe_gate_route); False keeps lga_q4_gemv + lga_moe_route
 # (tests A/B the two)
 moe_gate_route = True
-# decode k = 2: routed proj GEMVs + combine in one launch (lga_q4_gemv_experts_combine); False keeps
-# lga_q4_gemv_experts + lga_moe_combine (tests A/B the two)
-moe_fused_combine = os.environ.get("LGA_MOE_FUSED_COMBINE", "1") != "0"
+# decode k = 2: routed proj GEMVs + combine in one launch (lga_q4_gemv_experts_combine) — off by default: bit-identical
+# but slower on MI355X (Mixtral bench 443.6 vs 452.6-454.0 tok/s A/B on one box); tests A/B the two
+moe_fused_combine = os.environ.get("LGA_MOE_FUSED_COMBINE", "0") == "1"
 
 
 class LLaMAMoE(nn.Module):
