@@ -70,7 +70,9 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
   const int rg = wave * RGW + lane / LPR;
   const int sub = lane % LPR;
   LGA_TRACE(0);
+  // both positions in one scalar round trip (hipcc otherwise waits for input_pos before issuing rope_pos)
   const long p = input_pos[t];
+  const long rp_raw = FUSED ? rope_pos[t] : 0;
   const int L = (int)min(p + 1, (long)max_seq);  // keys 0..p (never past the cache)
   const int chunk = (L + n_splits - 1) / n_splits;
   const int k_lo = split * chunk;
@@ -81,32 +83,63 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
   const float* cr = nullptr;
   const float* sr = nullptr;
   if (FUSED) {
-    const long rp = min(max(rope_pos[t], 0L), (long)rope_rows - 1);
+    const long rp = min(max(rp_raw, 0L), (long)rope_rows - 1);
     cr = cos + (size_t)rp * HS + sub * 8;
     sr = sin + (size_t)rp * HS + sub * 8;
   }
+  const uint16_t* kbase = kc + (size_t)g * max_seq * HS + sub * 8;
+  const uint16_t* vbase = vc + (size_t)g * max_seq * HS + sub * 8;
+  // clamped duplicate rows (past k_end) are masked in consume() and hit in cache
+  auto fetch = [&](uint4 (&kv)[UNR], uint4 (&vv)[UNR], int j0) {
+#pragma unroll
+    for (int u = 0; u < UNR; ++u) {
+      const int j = max(min(j0 + u * RG, k_end - 1), 0);
+      kv[u] = ld_kv(kbase + (size_t)j * HS);
+      vv[u] = ld_kv(vbase + (size_t)j * HS);
+    }
+  };
+  const int j_first = k_lo + rg;
 
+  // the q rows are loaded first and the first K/V batch right behind them (vmcnt retires in order: the RoPE below
+  // waits for q only, with the K/V loads in flight); an empty split's batch re-reads row 0 and is never consumed
+  uint4 qraw[QPK];
+#pragma unroll
+  for (int h = 0; h < QPK; ++h) {
+    if (FUSED)  // qkv row layout per group: [q_0 .. q_{QPK-1}, k, v] x HS (scripts/convert_hf_checkpoint.py:181-187)
+      qraw[h] = *(const uint4*)(q + ((size_t)g * (QPKT + 2) + hsi * QPK + h) * HS + sub * 8);
+    else
+      qraw[h] = *(const uint4*)(q + ((size_t)t * n_head + (size_t)g * QPKT + hsi * QPK + h) * HS + sub * 8);
+  }
+  float cs[FUSED ? 8 : 1], sn[FUSED ? 8 : 1];
+  if (FUSED) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      cs[i] = cr[i];
+      sn[i] = sr[i];
+    }
+  }
+  uint4 ka[UNR], va[UNR], kb[UNR], vb[UNR];
+  if (PIPE) fetch(ka, va, j_first);
+  __builtin_amdgcn_sched_barrier(0);  // keep the K/V batch above the RoPE's wait for q
   float qf[QPK][8];
 #pragma unroll
   for (int h = 0; h < QPK; ++h) {
-    if (FUSED) {  // qkv row layout per group: [q_0 .. q_{QPK-1}, k, v] x HS (scripts/convert_hf_checkpoint.py:181-187)
-      const uint4 raw = *(const uint4*)(q + ((size_t)g * (QPKT + 2) + hsi * QPK + h) * HS + sub * 8);
-      unpack8(rope8(raw, cr, sr, sub), qf[h]);
-    } else {
-      unpack8(*(const uint4*)(q + ((size_t)t * n_head + (size_t)g * QPKT + hsi * QPK + h) * HS + sub * 8), qf[h]);
-    }
+    if (FUSED) unpack8(rope8(qraw[h], cs, sn, sub), qf[h]);
+    else unpack8(qraw[h], qf[h]);
   }
   LGA_TRACE(2);
+  // m starts at a finite floor, not -inf: every row group runs the split's step count, so one whose keys are all
+  // past k_end sees only masked (-inf) scores, and exp(floor - floor) = 1 keeps its (l, o) = 0 instead of NaN; a
+  // real first score s gives exp(kMFloor - s) = 0 exactly as exp(-inf) did
+  constexpr float kMFloor = -1e30f;
   float m[QPK], l[QPK], o[QPK][8];
 #pragma unroll
   for (int h = 0; h < QPK; ++h) {
-    m[h] = -INFINITY;
+    m[h] = kMFloor;
     l[h] = 0.0f;
 #pragma unroll
     for (int i = 0; i < 8; ++i) o[h][i] = 0.0f;
   }
-  const uint16_t* kbase = kc + (size_t)g * max_seq * HS + sub * 8;
-  const uint16_t* vbase = vc + (size_t)g * max_seq * HS + sub * 8;
   // one step = UNR keys per row group: scores, online-softmax rescale, P.V (masked keys score -inf)
   auto consume = [&](const uint4 (&kv)[UNR], const uint4 (&vv)[UNR], int j0) {
 #pragma unroll
@@ -140,40 +173,30 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
       m[h] = mx;
     }
   };
-  // clamped duplicate rows (past k_end) are masked in consume() and hit in cache
-  auto fetch = [&](uint4 (&kv)[UNR], uint4 (&vv)[UNR], int j0) {
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int j = max(min(j0 + u * RG, k_end - 1), 0);
-      kv[u] = ld_kv(kbase + (size_t)j * HS);
-      vv[u] = ld_kv(vbase + (size_t)j * HS);
+  if (PIPE) {
+    // software pipeline: step i + 1's 2*UNR loads are issued before step i's math, so every row group keeps 2-4
+    // steps of K/V in flight and a split costs one load round trip plus its streaming time (the first batch was
+    // issued above, next to q)
+    const int stp = RG * UNR;
+    const int nst = k_end > k_lo ? (k_end - k_lo + stp - 1) / stp : 0;
+    int i = 0;
+    for (; i + 1 < nst; i += 2) {
+      fetch(kb, vb, j_first + (i + 1) * stp);
+      consume(ka, va, j_first + i * stp);
+      if (i + 2 < nst) fetch(ka, va, j_first + (i + 2) * stp);
+      consume(kb, vb, j_first + (i + 1) * stp);
     }
-  };
-  const int j_first = k_lo + rg;
-  if (PIPE && k_lo < k_end) {
-    // software pipeline: the next step's 2*UNR loads are issued before this step's math, so every row group
-    // keeps 2-4 steps of K/V in flight and a split costs one load round trip plus its streaming time
-    uint4 ka[UNR], va[UNR], kb[UNR], vb[UNR];
-    fetch(ka, va, j_first);
-    int j0 = j_first;
-    for (; j0 + RG * UNR < k_end; j0 += 2 * RG * UNR) {
-      fetch(kb, vb, j0 + RG * UNR);
-      consume(ka, va, j0);
-      if (j0 + 2 * RG * UNR < k_end) fetch(ka, va, j0 + 2 * RG * UNR);
-      consume(kb, vb, j0 + RG * UNR);
-    }
-    if (j0 < k_end) consume(ka, va, j0);
+    if (i < nst) consume(ka, va, j_first + i * stp);
   } else {
     for (int j0 = j_first; j0 < k_end; j0 += RG * UNR) {
-      uint4 kv[UNR], vv[UNR];
-      fetch(kv, vv, j0);
-      consume(kv, vv, j0);
+      fetch(ka, va, j0);
+      consume(ka, va, j0);
     }
   }
   LGA_TRACE(3);
   if (FUSED && owns_new && rg == 0) {  // the new key/value: rope k, append both to the cache, score from registers
     const uint16_t* kvrow = q + ((size_t)g * (QPKT + 2) + QPKT) * HS + sub * 8;
-    const uint4 kr = rope8(*(const uint4*)kvrow, cr, sr, sub);
+    const uint4 kr = rope8(*(const uint4*)kvrow, cs, sn, sub);
     const uint4 vr = *(const uint4*)(kvrow + HS);
     if (hsi == 0) {  // one head slice appends; the others score the same key from their registers
       *(uint4*)(kc + ((size_t)g * max_seq + p) * HS + sub * 8) = kr;
@@ -204,8 +227,8 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
     for (int h = 0; h < QPK; ++h) {
       const float mo = __shfl_xor(m[h], off), lo = __shfl_xor(l[h], off);
       const float mn = fmaxf(m[h], mo);
-      const float ca = mn == -INFINITY ? 0.0f : expf(m[h] - mn);
-      const float cb = mn == -INFINITY ? 0.0f : expf(mo - mn);
+      const float ca = expf(m[h] - mn);  // m >= kMFloor: finite, never exp(-inf - -inf)
+      const float cb = expf(mo - mn);
       l[h] = l[h] * ca + lo * cb;
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[h][i] = o[h][i] * ca + __shfl_xor(o[h][i], off) * cb;
@@ -213,8 +236,8 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
     }
   }
   __shared__ float sm[NW][QPK], sl[NW][QPK];
-  __shared__ float so[NW][QPK][HS];
-  __shared__ unsigned s_last;
+  __shared__ __attribute__((aligned(16))) float so[NW][QPK][HS];
+  __shared__ unsigned s_ticket;
   if (lane < LPR) {
 #pragma unroll
     for (int h = 0; h < QPK; ++h) {
@@ -222,82 +245,99 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
         sm[wave][h] = m[h];
         sl[wave][h] = l[h];
       }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) so[wave][h][sub * 8 + i] = o[h][i];
+      *(float4*)&so[wave][h][sub * 8] = make_float4(o[h][0], o[h][1], o[h][2], o[h][3]);
+      *(float4*)&so[wave][h][sub * 8 + 4] = make_float4(o[h][4], o[h][5], o[h][6], o[h][7]);
     }
   }
   __syncthreads();
-  const size_t row0 = (size_t)t * n_head + (size_t)g * QPKT + hsi * QPK;  // first head row of this slice
-  for (int it = threadIdx.x; it < QPK * HS; it += NT) {
-    const int h = it / HS, d = it % HS;
-    float mx = -INFINITY;
+  // block merge: a thread owns 4 consecutive output columns (h, 4 dq .. 4 dq + 3) of one head of the slice
+  constexpr int NQ = QPK * HS / 4;
+  static_assert(NQ <= NT, "one 4-column item per thread");
+  const bool has_item = threadIdx.x < NQ;
+  const int hq = threadIdx.x / (HS / 4), dq = threadIdx.x % (HS / 4);
+  float bm = -INFINITY, bl = 0.0f, bo[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (has_item) {
 #pragma unroll
-    for (int w = 0; w < NW; ++w) mx = fmaxf(mx, sm[w][h]);
-    float lt = 0.0f, ot = 0.0f;
+    for (int w = 0; w < NW; ++w) bm = fmaxf(bm, sm[w][hq]);
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      const float c = mx == -INFINITY ? 0.0f : expf(sm[w][h] - mx);
-      lt += sl[w][h] * c;
-      ot += so[w][h][d] * c;
-    }
-    if (n_splits == 1) {
-      y[(row0 + h) * HS + d] = f2bf(ot / lt);
-    } else {
-      float* wsr = ws + ((row0 + h) * n_splits + split) * (HS + 4);
-      st_sc1(wsr + 4 + d, ot);
-      if (d == 0) {
-        st_sc1(wsr, mx);
-        st_sc1(wsr + 1, lt);
-      }
+      const float c = expf(sm[w][hq] - bm);
+      bl += sl[w][hq] * c;
+      const float4 ov = *(const float4*)&so[w][hq][dq * 4];
+      bo[0] += ov.x * c;
+      bo[1] += ov.y * c;
+      bo[2] += ov.z * c;
+      bo[3] += ov.w * c;
     }
   }
+  const size_t row0 = (size_t)t * n_head + (size_t)g * QPKT + hsi * QPK;  // first head row of this slice
+  if (n_splits == 1) {
+    if (has_item) {
+      uint16_t* yr = y + (row0 + hq) * HS + dq * 4;
+      *(uint2*)yr = make_uint2(pack2(bo[0] / bl, bo[1] / bl), pack2(bo[2] / bl, bo[3] / bl));
+    }
+    return;
+  }
   LGA_TRACE(4);
-  if (n_splits == 1) return;
-  // ---- publish, then the last-arriving split of this (t, group) merges all splits ----
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  // ---- publish (m, l, o), then the last-arriving split of this (t, group) merges all splits (MI355X_MICROARCH.md
+  // "Valid forms" row 1: 16-B sc1 stores, every storing wave drains, a workgroup barrier, one lane's agent-scope
+  // add; the last arriver's loads are sc1 too). Per (head row, split): {m, l, 0, 0, o[HS]} fp32 ----
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(ws + row0 * n_splits * (HS + 4)), (short)0, QPK * n_splits * (HS + 4) * 4, 0x00020000);
+  if (has_item) {
+    const unsigned off = (unsigned)((hq * n_splits + split) * (HS + 4)) * 4;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, make_float4(bo[0], bo[1], bo[2], bo[3])), wrs,
+                                           off + 16 + dq * 16, 0, 16);
+    if (dq == 0)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, make_float4(bm, bl, 0.0f, 0.0f)), wrs, off,
+                                             0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   unsigned* ctr = cnt + ((size_t)t * gridDim.y + gy) * kCounterStride;
-  if (threadIdx.x == 0) s_last = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   LGA_TRACE(5);
-  if (s_last != (unsigned)(n_splits - 1)) return;
-  // combine, one output column per thread, 8 splits per round with every (m, l, o) load of the round in flight
-  // at once (one load round trip for the usual <= 8 splits) and an online rescale across rounds. Split 0 always
-  // holds key 0, so the running max is finite after round 0; empty splits carry m = -inf, l = 0, o = 0 and
-  // clamped out-of-range slots are forced to m = -inf: both get weight exp(-inf) = 0.
-  for (int it = threadIdx.x; it < QPK * HS; it += NT) {
-    const int h = it / HS, d = it % HS;
-    const float* base = ws + (row0 + h) * n_splits * (HS + 4);
-    float mx = -INFINITY, lt = 0.0f, ot = 0.0f;
+  if (s_ticket != (unsigned)(n_splits - 1)) return;
+  // one output column quad per thread, 8 splits per round with every load of the round in flight at once and an
+  // online rescale across rounds. Split 0 always holds key 0, so the running max is finite after round 0; empty
+  // splits carry m = kMFloor, l = 0, o = 0 and clamped out-of-range slots are forced to m = -inf: both weigh 0.
+  if (has_item) {
+    const unsigned hoff = (unsigned)(hq * n_splits * (HS + 4)) * 4;
+    float mx = -INFINITY, lt = 0.0f, ot[4] = {0.0f, 0.0f, 0.0f, 0.0f};
     for (int s0 = 0; s0 < n_splits; s0 += 8) {
-      float mv[8], lv[8], ov[8];
+      float4 ml[8], o4[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const float* r = base + min(s0 + u, n_splits - 1) * (HS + 4);
-        mv[u] = ld_sc1(r);
-        lv[u] = ld_sc1(r + 1);
-        ov[u] = ld_sc1(r + 4 + d);
+        const unsigned off = hoff + (unsigned)(min(s0 + u, n_splits - 1) * (HS + 4)) * 4;
+        ml[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off, 0, 16));
+        o4[u] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(wrs, off + 16 + dq * 16, 0, 16));
       }
       float nm = mx;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        if (s0 + u >= n_splits) mv[u] = -INFINITY;
-        nm = fmaxf(nm, mv[u]);
+        if (s0 + u >= n_splits) ml[u].x = -INFINITY;
+        nm = fmaxf(nm, ml[u].x);
       }
       const float c = expf(mx - nm);  // round 0: exp(-inf) = 0
       lt *= c;
-      ot *= c;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ot[i] *= c;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const float e = expf(mv[u] - nm);
-        lt = fmaf(lv[u], e, lt);
-        ot = fmaf(ov[u], e, ot);
+        const float e = expf(ml[u].x - nm);
+        lt = fmaf(ml[u].y, e, lt);
+        ot[0] = fmaf(o4[u].x, e, ot[0]);
+        ot[1] = fmaf(o4[u].y, e, ot[1]);
+        ot[2] = fmaf(o4[u].z, e, ot[2]);
+        ot[3] = fmaf(o4[u].w, e, ot[3]);
       }
       mx = nm;
     }
-    y[(row0 + h) * HS + d] = f2bf(ot / lt);
+    uint16_t* yr = y + (row0 + hq) * HS + dq * 4;
+    *(uint2*)yr = make_uint2(pack2(ot[0] / lt, ot[1] / lt), pack2(ot[2] / lt, ot[3] / lt));
   }
-  if (threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
   LGA_TRACE(6);
 }
 

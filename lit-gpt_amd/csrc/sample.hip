@@ -209,7 +209,7 @@ __global__ void __launch_bounds__(1024) topk_sample_kernel(
     } else {
       const unsigned long long cn = *counter;
       *counter = cn + 1;
-      u0 = ((float)(mix64(seed ^ (cn * 0xD1B54A32D192ED03ull)) >> 40) + 0.5f) * 0x1.0p-24f;  // in (0, 1)
+      u0 = ((float)(mix64(seed ^ (cn * 0xD1B54A32D192ED03ull)) >> 41) + 0.5f) * 0x1.0p-23f;  // exact, in (0, 1)
     }
   }
   // stage the logits (pairs of bf16 per load when the row is 4-B aligned), -inf past n; clear the first histogram

@@ -90,19 +90,24 @@ class XgmiAllReduce:
 
     def _self_test(self) -> None:
         """One reduction of known values (rank r contributes r + 1 at every element, + a residual of 0.5): checks
-        that the peers' pushes and flags are visible through the mapped memory before any real call trusts it."""
+        that the peers' pushes and flags are visible through the mapped memory before any real call trusts it. A
+        launch error on one rank is caught and agreed like a wrong sum, so no peer is left waiting in the
+        collective."""
         n = 1024
-        x = torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device=self.device)
-        res = torch.full((n,), 0.5, dtype=torch.bfloat16, device=self.device)
-        with torch.cuda.device(self.device):
-            y = self.all_reduce(x, residual=res)
-            torch.cuda.synchronize(self.device)
         want = float(self.world * (self.world + 1) // 2) + 0.5
         failure = None
-        if self.errors():
-            failure = f"rank {self.rank}: self-test timed out waiting for a peer"
-        elif not bool((y.float() == want).all()):
-            failure = f"rank {self.rank}: self-test sum wrong ({y.float()[:4].tolist()} vs {want})"
+        try:
+            x = torch.full((n,), float(self.rank + 1), dtype=torch.bfloat16, device=self.device)
+            res = torch.full((n,), 0.5, dtype=torch.bfloat16, device=self.device)
+            with torch.cuda.device(self.device):
+                y = self.all_reduce(x, residual=res)
+                torch.cuda.synchronize(self.device)
+            if self.errors():
+                failure = f"rank {self.rank}: self-test timed out waiting for a peer"
+            elif not bool((y.float() == want).all()):
+                failure = f"rank {self.rank}: self-test sum wrong ({y.float()[:4].tolist()} vs {want})"
+        except Exception as e:  # noqa: BLE001 - any launch / runtime error is this rank's failure, agreed below
+            failure = f"rank {self.rank}: self-test raised {type(e).__name__}: {e}"
         self._agree(failure, "self-test")
 
     def _self_test_fused(self, n: int = 512, k: int = 1024, calls: int = 4) -> None:
@@ -110,31 +115,43 @@ class XgmiAllReduce:
         residual) it must equal bit for bit: ``calls`` back-to-back launches of per-rank weights. Its cross-GPU
         hand-off (every workgroup's pushes, then the last arriver's flags) is a different protocol from the one-shot
         kernel's, so it is checked on its own; when it fails on any rank, every rank keeps the xGMI one-shot
-        all-reduce and only the fusion is dropped (``fused_ok``, ``fused_fallback``)."""
+        all-reduce and only the fusion is dropped (``fused_ok``, ``fused_fallback``). A timeout or a launch error on
+        any rank instead raises ``XgmiUnavailable`` on every rank (RCCL for all decode all-reduces)."""
         import types
 
         g = torch.Generator().manual_seed(1000 + self.rank)
-        w = (torch.randn(n, k, generator=g) * 0.02).to(self.device)
-        x = torch.randn(k, generator=g).bfloat16().to(self.device)
-        res = torch.randn(n, generator=g).bfloat16().to(self.device)
         failure = None
-        with torch.cuda.device(self.device):
-            qw, sc = ops.quantize(w, ops.FMT_Q4G, 128)
-            lin = types.SimpleNamespace(out_features=n, in_features=k, qweight=qw, scales=sc, bias=None, group=128,
-                                        fmt=ops.FMT_Q4G)
-            want = self.all_reduce(ops.q4_gemv(x, qw, sc, n, k, 128, ops.FMT_Q4G), residual=res)
-            got = [self.gemv_all_reduce(lin, x, residual=res) for _ in range(calls)]
-            torch.cuda.synchronize(self.device)
-        if self.errors():
-            failure = f"rank {self.rank}: fused GEMV all-reduce self-test timed out waiting for a peer"
-        else:
-            bad = [i for i, y in enumerate(got) if not torch.equal(y, want)]
-            if bad:
-                failure = f"rank {self.rank}: fused GEMV all-reduce differs from GEMV + all-reduce at calls {bad}"
-        flag = torch.tensor([0 if failure else 1], dtype=torch.int32,
+        code = 0  # 0 ok; 1 results differ (drop the fusion only); 2 a peer timed out or a launch raised
+        try:
+            w = (torch.randn(n, k, generator=g) * 0.02).to(self.device)
+            x = torch.randn(k, generator=g).bfloat16().to(self.device)
+            res = torch.randn(n, generator=g).bfloat16().to(self.device)
+            with torch.cuda.device(self.device):
+                qw, sc = ops.quantize(w, ops.FMT_Q4G, 128)
+                lin = types.SimpleNamespace(out_features=n, in_features=k, qweight=qw, scales=sc, bias=None,
+                                            group=128, fmt=ops.FMT_Q4G)
+                want = self.all_reduce(ops.q4_gemv(x, qw, sc, n, k, 128, ops.FMT_Q4G), residual=res)
+                got = [self.gemv_all_reduce(lin, x, residual=res) for _ in range(calls)]
+                torch.cuda.synchronize(self.device)
+            if self.errors():
+                code, failure = 2, f"rank {self.rank}: fused GEMV all-reduce self-test timed out waiting for a peer"
+            else:
+                bad = [i for i, y in enumerate(got) if not torch.equal(y, want)]
+                if bad:
+                    code = 1
+                    failure = f"rank {self.rank}: fused GEMV all-reduce differs from GEMV + all-reduce at calls {bad}"
+        except Exception as e:  # noqa: BLE001 - agreed below so that no peer waits in the collective
+            code, failure = 2, f"rank {self.rank}: fused GEMV all-reduce self-test raised {type(e).__name__}: {e}"
+        flag = torch.tensor([code], dtype=torch.int32,
                             device=self.device if dist.get_backend(self.group) == "nccl" else "cpu")
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=self.group)
-        if int(flag.item()) == 0:
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        agreed = int(flag.item())
+        if agreed == 2:
+            # a timeout leaves the mailboxes' sequence flags out of step between the ranks, and the one-shot kernel
+            # uses the same mailboxes, flags and counter: every rank leaves xGMI for RCCL
+            self.close()
+            raise XgmiUnavailable(failure or "fused GEMV all-reduce self-test timed out or raised on another rank")
+        if agreed == 1:
             self.fused_ok = False
             self.fused_fallback = failure or "fused GEMV all-reduce self-test failed on another rank"
 

@@ -2,7 +2,7 @@
 
 usage: ATTN_LIBS=tools/_lab/trace_4_4.so,... python tools/attn_trace.py
 Per block (thread 0): 0 start, 1 position known, 2 q ready (+ first KV batch landed), 3 key loop done,
-4 block merge done, 5 arrival counter returned, 6 combine done (last block). Times in us from the
+4 block merge done, 5 partial published + arrival counter returned, 6 combine done (last block). Times in us from the
 earliest block start (s_memrealtime, 100 MHz).
 """
 
@@ -32,9 +32,9 @@ def run(lib_path, H=32, G=32, hs=128, S=4096, layers=16):
     cos = torch.randn(S, hs, device=dev)
     sin = torch.randn(S, hs, device=dev)
     scale = 1.0 / math.sqrt(hs)
-    for p in (128, 2048):
+    for p in [int(v) for v in os.environ.get("ATTN_POS", "2048,2302").split(",")]:
         pos = torch.tensor([p], device=dev)
-        for splits in (8, 16):
+        for splits in [int(v) for v in os.environ.get("ATTN_SPLITS", "8").split(",")]:
             ws = ops.AttentionWorkspace(1, H, G, hs, splits, dev)
             for i in range(layers):
                 kc, vc = caches[i]
@@ -52,9 +52,11 @@ def run(lib_path, H=32, G=32, hs=128, S=4096, layers=16):
             rel = (tr - t0) / 100.0  # us
             last = tr[:, 6] > 0
             print(f"{Path(lib_path).name} p={p} splits={splits}")
-            for k, name in enumerate(["start", "pos", "q+kv0", "loop", "merge", "atomic"]):
+            for k, name in enumerate(["start", "pos", "q+kv0", "loop", "merge"]):
                 col = rel[:, k]
                 print(f"   {name:7s} min {col.min():6.2f}  med {np.median(col):6.2f}  max {col.max():6.2f}")
+            col = rel[:, 5]
+            print(f"   {'atomic':7s} min {col.min():6.2f}  med {np.median(col):6.2f}  max {col.max():6.2f}")
             col = rel[last, 6]
             print(f"   {'combine':7s} min {col.min():6.2f}  med {np.median(col):6.2f}  max {col.max():6.2f}"
                   f"  (n={last.sum()})", flush=True)

@@ -61,6 +61,9 @@ def main():
         lib.lga_gemv_trace_read(buf.ctypes.data, nw_max * 8)
         tr = buf.reshape(nw_max, 8).astype(np.int64)
         tr = tr[tr[:, 0] > 0]
+        if len(tr) == 0:  # the streaming form (gemv_stream.h) carries no stamps
+            print(f"== {name} N={N} K={K}: no stamps (streaming form)", flush=True)
+            continue
         t0 = tr[:, 0].min()
         rel = (tr - t0) / 100.0
         print(f"== {name} N={N} K={K} waves={len(tr)}", flush=True)
