@@ -149,6 +149,21 @@ int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, co
                                const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, void* y,
                                float* workspace, unsigned* counters, int n_head, int n_query_groups, int head_size,
                                int rope_n_elem, int max_seq, int n_splits, float scale, lga_stream_t stream);
+/* lga_attention_decode_proj: lga_attention_decode_fused followed, in the SAME launch, by the out-projection
+ * `self.proj(y)` (lit_gpt/model.py:656; the 4-bit Linear bnb's gemv_4bit serves at reference generate/base.py:128-136)
+ * and the Block residual add `x + h` (model.py:591): out (N) = bf16(proj(y) [+ bias]) + residual, bit-identical to
+ * lga_q4_gemv(y, ..., residual). y (n_head*hs bf16) still receives the attention row. sync: 128 zeroed uint32 per
+ * workspace (hand-off counter + base; never re-zeroed). Covers the geometries lga_attention_decode_proj_supported
+ * reports (hs 128, n_splits >= 2, K = n_head*hs = 4096, q_per_kv slice 1 or 2, grid <= CUs); TP's row-parallel
+ * projection keeps its own launch. */
+int lga_attention_decode_proj_supported(int n_head, int n_query_groups, int head_size, int n_splits, int N, int K,
+                                        int group, int fmt);
+int lga_attention_decode_proj(const void* qkv, void* k_cache, void* v_cache, const int64_t* cache_pos,
+                              const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, void* y,
+                              float* workspace, unsigned* counters, unsigned* sync, int n_head, int n_query_groups,
+                              int head_size, int rope_n_elem, int max_seq, int n_splits, float scale,
+                              const uint8_t* proj_qweight, const void* proj_scales, const void* proj_bias,
+                              const void* residual, void* out, int N, int group, int fmt, lga_stream_t stream);
 
 /* -- sparse MoE (LLaMAMoE.forward, lit_gpt/model.py:727-743; Mixtral) ------------------------------------------
  * lga_moe_route: per token row of router logits [T][n_expert] bf16 -> expert_ids [T][k] int32 and probs [T][k]
@@ -223,6 +238,11 @@ int lga_comm_close(void* ptr);
 int lga_comm_free(void* ptr);
 int lga_allreduce_bf16(const void* x, const void* residual, void* y, int n, void* const* mailboxes, int rank,
                        int world, int cap, unsigned* seq_counter, unsigned* err, lga_stream_t stream);
+/* lga_comm_trace: diagnostics of the all-reduce protocol. Every later lga_allreduce_bf16 / lga_q4_gemv_allreduce
+ * launch of this process records its call into buf (n_records x 16 uint64 on the device, indexed by the call's
+ * sequence number): sequence, rank, entry / flags-raised / wait-done times (s_memrealtime, 100 MHz), timeout, and
+ * the peers' flag words seen when the wait ended. buf = NULL switches it off. Not part of the reference interface. */
+int lga_comm_trace(void* buf, int n_records);
 /* The row-parallel decode Linear and its all-reduce in ONE launch (generate/tp.py:53,57,70 hook the reduction on
  * attn.proj / mlp.proj; lit_gpt/model.py:591-592 adds the residual): y (N) = lga_allreduce_bf16 of
  * lga_q4_gemv(x, W, bias) over the ranks (+ residual), bit for bit — each workgroup pushes its partial rows into
@@ -243,6 +263,16 @@ int lga_argmax(const void* logits, int n, int64_t* out_idx, int32_t* token_out, 
  * bit-identical to lga_embedding of the token — one launch per step fewer. */
 int lga_argmax_embed(const void* logits, int n, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
                      const void* table, int n_embd, int vocab, void* emb_out, lga_stream_t stream);
+/* lga_q4_gemv_argmax_embed: the greedy decode step's head in ONE launch — optional fused RMSNorm (ln_f), the 4-bit
+ * lm_head GEMV (model.py:519; logits (N) bf16 still written), argmax (generate/base.py:30-41 at temperature 0,
+ * torch.argmax order: NaN first, ties to the lowest index) and lga_argmax_embed's bookkeeping (token_out, out_idx,
+ * *pos_inout += 1, the token's row of table into emb_out). Bit-identical to lga_q4_gemv + lga_argmax_embed.
+ * work: lga_q4_gemv_argmax_work_bytes(N, K) bytes, zeroed once (its counters re-arm). K <= 4096. */
+size_t lga_q4_gemv_argmax_work_bytes(int N, int K);
+int lga_q4_gemv_argmax_embed(const void* x, const uint8_t* qweight, const void* scales, const void* norm_weight,
+                             float norm_eps, void* logits, int N, int K, int group, int fmt, void* work,
+                             int64_t* out_idx, int32_t* token_out, int64_t* pos_inout, const void* table, int C, int V,
+                             void* emb_out, lga_stream_t stream);
 
 /* -- temperature sampling (generate/base.py:30-41 with top_k and temperature > 0: torch.topk, scatter into -inf,
  *    softmax(logits / temperature) in the logits' dtype, torch.multinomial(probs, 1)) in ONE launch --------------

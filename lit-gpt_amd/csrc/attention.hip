@@ -18,8 +18,13 @@
 #include <cstdlib>
 
 #include "decode_ops.h"
+#include "gemv_body.h"
 
 namespace lga {
+
+#ifndef LGA_ATTN_PIPE
+#define LGA_ATTN_PIPE 1
+#endif
 
 #ifdef LGA_ATTN_TRACE  // lab builds only (tools/attn_trace.py): per-block phase timestamps, 100 MHz clock
 __device__ unsigned long long g_attn_trace[8192 * 8];
@@ -50,13 +55,22 @@ __device__ __forceinline__ uint4 ld_kv(const uint16_t* p) {
 // q heads itself, and the workgroup whose split owns the new position p ropes k, appends k and v to the cache
 // at p (KVCache.forward, lit_gpt/model.py:788-795) and scores that key from registers — replacing the separate
 // lga_rope_kv_append launch of the decode step.
-template <int HS, int QPK, int UNR, int NW, bool FUSED, bool PIPE>
-__global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
-                                                   uint16_t* __restrict__ vc, const int64_t* __restrict__ input_pos,
-                                                   uint16_t* __restrict__ y, float* __restrict__ ws,
-                                                   unsigned* __restrict__ cnt, int n_head, int max_seq, float scale,
-                                                   const int64_t* __restrict__ rope_pos, const float* __restrict__ cos,
-                                                   const float* __restrict__ sin, int rope_rows, int hsplit) {
+// PROJ (decode, fused, tensor parallelism off): the attention output row y is handed to the out-projection GEMV that
+// every workgroup of the SAME launch runs afterwards (attn_proj_kernel). The combining splits store y write-through
+// (sc1), drain, and add 1 to sync[kHeads]; the projection's workgroups issue their weight loads first and wait until
+// sync[kHeads] reaches base + C (C = combining workgroups per launch, base = sync[kBase] read at kernel start). The
+// combiner whose add completes the launch moves sync[kBase] to base + C — every workgroup has read the base by then:
+// each one holds an arrival ticket of some combined head, and a head combines only after all its splits arrived.
+constexpr int kHeads = 0, kBase = 64;  // sync words, 256 B apart
+
+template <int HS, int QPK, int UNR, int NW, bool FUSED, bool PIPE, bool PROJ>
+__device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
+                                          uint16_t* __restrict__ vc, const int64_t* __restrict__ input_pos,
+                                          uint16_t* __restrict__ y, float* __restrict__ ws,
+                                          unsigned* __restrict__ cnt, int n_head, int max_seq, float scale,
+                                          const int64_t* __restrict__ rope_pos, const float* __restrict__ cos,
+                                          const float* __restrict__ sin, int rope_rows, int hsplit,
+                                          unsigned* __restrict__ sync, unsigned base) {
   constexpr int LPR = HS / 8;    // lanes per key row
   constexpr int RGW = 64 / LPR;  // row groups per wave
   constexpr int RG = NW * RGW;   // row groups per workgroup
@@ -335,10 +349,72 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
       mx = nm;
     }
     uint16_t* yr = y + (row0 + hq) * HS + dq * 4;
-    *(uint2*)yr = make_uint2(pack2(ot[0] / lt, ot[1] / lt), pack2(ot[2] / lt, ot[3] / lt));
+    const uint2 yv = make_uint2(pack2(ot[0] / lt, ot[1] / lt), pack2(ot[2] / lt, ot[3] / lt));
+    if (PROJ)  // handed to other workgroups of this launch: write-through
+      __hip_atomic_store((unsigned long long*)yr, ((unsigned long long)yv.y << 32) | yv.x, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    else
+      *(uint2*)yr = yv;
   }
   if (threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+  if (PROJ) {  // y of this (t, group slice) is out: every storing wave drains, a barrier, one lane counts it
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned C = gridDim.y * gridDim.z;
+      const unsigned prev = __hip_atomic_fetch_add(sync + kHeads, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == base + C - 1u) __hip_atomic_store(sync + kBase, base + C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   LGA_TRACE(6);
+}
+
+template <int HS, int QPK, int UNR, int NW, bool FUSED, bool PIPE>
+__global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
+                                                   uint16_t* __restrict__ vc, const int64_t* __restrict__ input_pos,
+                                                   uint16_t* __restrict__ y, float* __restrict__ ws,
+                                                   unsigned* __restrict__ cnt, int n_head, int max_seq, float scale,
+                                                   const int64_t* __restrict__ rope_pos, const float* __restrict__ cos,
+                                                   const float* __restrict__ sin, int rope_rows, int hsplit) {
+  attn_body<HS, QPK, UNR, NW, FUSED, PIPE, false>(q, kc, vc, input_pos, y, ws, cnt, n_head, max_seq, scale, rope_pos,
+                                                  cos, sin, rope_rows, hsplit, nullptr, 0u);
+}
+
+// The out-projection (CausalSelfAttention.proj, lit_gpt/model.py:656) + the Block residual add (:591) of a decode
+// token inside the attention launch: after its attention role (publish, or combine) every workgroup computes the
+// GEMV rows blk = its flat index with gemv_q4_body's exact arithmetic (bit-identical to lga_q4_gemv with a
+// residual), its weight loads issued before it waits for y. Replaces the separate proj launch: its ramp, and the
+// boundary in front of it, overlap the attention's tail.
+struct ProjArgs {
+  const uint8_t* qw;
+  const void* sc;
+  const uint16_t* bias;
+  const uint16_t* residual;
+  uint16_t* out;
+  unsigned* sync;
+  int N, K, group, cb;
+};
+
+template <int HS, int QPK, int UNR, int NW, int RPR, int CPT, int FMT>
+__global__ void __launch_bounds__(NW * 64) attn_proj_kernel(const uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
+                                                        uint16_t* __restrict__ vc, const int64_t* __restrict__ input_pos,
+                                                        uint16_t* __restrict__ y, float* __restrict__ ws,
+                                                        unsigned* __restrict__ cnt, int n_head, int max_seq,
+                                                        float scale, const int64_t* __restrict__ rope_pos,
+                                                        const float* __restrict__ cos, const float* __restrict__ sin,
+                                                        int rope_rows, int hsplit, ProjArgs pa) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const unsigned base = pa.sync[kBase];  // written only by the previous launch's last combiner (kernel boundary)
+  attn_body<HS, QPK, UNR, NW, true, LGA_ATTN_PIPE != 0, true>(q, kc, vc, input_pos, y, ws, cnt, n_head, max_seq,
+                                                              scale, rope_pos, cos, sin, rope_rows, hsplit, pa.sync,
+                                                              base);
+  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
+  if (blk * NW * RPR >= pa.N) return;
+  GemvArgs a{y, pa.qw, pa.sc, nullptr, nullptr, pa.bias, pa.residual, nullptr, pa.out, pa.N, pa.K, pa.group, 0.0f};
+  a.cb = pa.cb;
+  a.xwait = pa.sync + kHeads;
+  a.xwait_target = base + gridDim.y * gridDim.z;
+  gemv_q4_body<RPR, CPT, FMT, false, false, true, NW, false, false, true>(a, blk, smem);
 }
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -892,9 +968,6 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_pair_kernel(const uint16_
 #ifndef LGA_ATTN_Q8
 #define LGA_ATTN_Q8 2, 4
 #endif
-#ifndef LGA_ATTN_PIPE
-#define LGA_ATTN_PIPE 1
-#endif
 
 template <int HS, int QPK, int UNR, int NW, bool FUSED>
 static void launch_one(dim3 grid, hipStream_t stream, const void* q, void* kc, void* vc, const int64_t* pos, void* y,
@@ -942,6 +1015,24 @@ static int launch_hs(const void* q, void* kc, void* vc, const int64_t* pos, void
   }
 #undef LGA_ATTN
   return 0;
+}
+
+// attn_proj_kernel geometry: the decode-attention config a q_per_kv slice runs (as launch_hs picks it) x the proj
+// GEMV's row tile (gemv.hip dispatch: K = 4096 -> 4 rows x 2 chunks per lane). Returns 0 when not covered.
+static int proj_shape(int H, int G, int hs, int n_splits, int N, int K, int group, int fmt, int* hsplit_out) {
+  if (hs != 128 || n_splits < 2 || H % G || K != H * hs || K != 4096 || N % 16 || group < 32 || group % 32 ||
+      K % group || (fmt != 0 && fmt != 1 && fmt != 3))
+    return 0;
+  const int hsplit = attn_hsplit(1, G, H / G, n_splits);
+  const int qpk = H / G / hsplit;
+  if (qpk != 1 && qpk != 2) return 0;
+  if (qpk == 1 && G * hsplit <= 16) return 0;  // the 8-wave few-groups config: not instantiated
+  const long wgs = (long)n_splits * G * hsplit;
+  // every workgroup holds one 16-row block of the projection and the whole grid must be resident at once (the
+  // projection's workgroups wait for heads combined by others of the same launch)
+  if (wgs * 16 < N || wgs > num_cu()) return 0;
+  if (hsplit_out) *hsplit_out = hsplit;
+  return qpk;
 }
 
 }  // namespace lga
@@ -1024,6 +1115,49 @@ extern "C" int lga_attention_decode_fused(const void* qkv, void* k_cache, void* 
                                            n_query_groups, max_seq, n_splits, scale, rope_pos, cos, sin, rope_rows,
                                            stream);
   if (rc) return rc;
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_attention_decode_proj_supported(int n_head, int n_query_groups, int head_size, int n_splits, int N,
+                                                   int K, int group, int fmt) {
+  if (n_head <= 0 || n_query_groups <= 0) return 0;
+  return lga::proj_shape(n_head, n_query_groups, head_size, n_splits, N, K, group, fmt, nullptr) ? 1 : 0;
+}
+
+extern "C" int lga_attention_decode_proj(const void* qkv, void* k_cache, void* v_cache, const int64_t* cache_pos,
+                                         const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows,
+                                         void* y, float* workspace, unsigned* counters, unsigned* sync, int n_head,
+                                         int n_query_groups, int head_size, int rope_n_elem, int max_seq, int n_splits,
+                                         float scale, const uint8_t* proj_qweight, const void* proj_scales,
+                                         const void* proj_bias, const void* residual, void* out, int N, int group,
+                                         int fmt, hipStream_t stream) {
+  LGA_CHECK_ARG(qkv && k_cache && v_cache && cache_pos && rope_pos && cos && sin && y && workspace && counters && sync &&
+                    proj_qweight && proj_scales && residual && out,
+                "lga_attention_decode_proj: null pointer");
+  LGA_CHECK_ARG(n_query_groups > 0 && n_head % n_query_groups == 0, "lga_attention_decode_proj: bad head geometry");
+  LGA_CHECK_ARG(head_size == 128 && rope_n_elem == 128, "lga_attention_decode_proj: needs head_size == rope_n_elem == 128");
+  LGA_CHECK_ARG(rope_rows > 0 && max_seq > 0, "lga_attention_decode_proj: empty rope cache or kv cache");
+  const int K = n_head * head_size;
+  int hsplit = 1;
+  const int qpk = lga::proj_shape(n_head, n_query_groups, head_size, n_splits, N, K, group, fmt, &hsplit);
+  LGA_CHECK_ARG(qpk != 0, "lga_attention_decode_proj: geometry not covered (lga_attention_decode_proj_supported)");
+  const dim3 grid(n_splits, n_query_groups * hsplit, 1);
+  const size_t lds = lga::gemv_lds_bytes(K);
+  lga::ProjArgs pa{proj_qweight, proj_scales, (const uint16_t*)proj_bias, (const uint16_t*)residual, (uint16_t*)out,
+                   sync, N, K, group, lga::codebook_of(fmt)};
+#define LGA_AP(QPK, FMT)                                                                                              \
+  lga::attn_proj_kernel<128, QPK, 4, 4, 4, 2, FMT><<<grid, 256, lds, stream>>>(                                      \
+      (const uint16_t*)qkv, (uint16_t*)k_cache, (uint16_t*)v_cache, cache_pos, (uint16_t*)y, workspace, counters,    \
+      n_head, max_seq, scale, rope_pos, cos, sin, rope_rows, hsplit, pa)
+  const int kf = lga::kernel_fmt(fmt);
+  if (qpk == 1) {
+    if (kf == 0) LGA_AP(1, 0);
+    else LGA_AP(1, 1);
+  } else {
+    if (kf == 0) LGA_AP(2, 0);
+    else LGA_AP(2, 1);
+  }
+#undef LGA_AP
   LGA_LAUNCH_RETURN();
 }
 

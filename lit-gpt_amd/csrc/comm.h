@@ -12,7 +12,19 @@ constexpr size_t kFlagBytes = kMaxRanks * kFlagStride * 4;
 
 struct Peers {
   unsigned char* mb[kMaxRanks];
+  // diagnostics (lga_comm_trace; null = off): one record of kTraceWords uint64 per call, indexed by the call's sequence
+  // number: [0] seq | rank << 32 | kind << 40 (1 one-shot, 2 fused GEMV), [1] entry (one-shot) / last arrival (fused)
+  // time, [2] flags raised, [3] wait done, [4] timed out, [5] the sequence word read at entry, [6 + r] the flag of
+  // rank r in this rank's mailbox when the wait ended; times from s_memrealtime (100 MHz, one clock per device)
+  unsigned long long* trace;
+  int trace_n;
 };
+constexpr int kTraceWords = 16;
+__device__ __forceinline__ unsigned long long* trace_rec(const Peers& p, unsigned seq) {
+  return p.trace ? p.trace + (size_t)((seq - 1u) % (unsigned)p.trace_n) * kTraceWords : nullptr;
+}
+// host side: the record buffer lga_comm_trace installed (comm.hip)
+void comm_trace_get(unsigned long long** buf, int* n);
 
 __device__ __forceinline__ uint16_t* slot_ptr(unsigned char* mb, int slot, int src, int cap) {
   return (uint16_t*)(mb + kFlagBytes) + ((size_t)slot * kMaxRanks + src) * cap;
@@ -54,6 +66,9 @@ __device__ __forceinline__ uint4 ld_sys16(__amdgpu_buffer_rsrc_t r, int off) {
 // data stores are complete: each storing wave drained (asm vmcnt(0)) and the workgroup barrier ordered them before
 // the flag writers, which drain again and store the flag (system scope).
 __device__ __forceinline__ void raise_flags(const Peers& peers, int rank, int world, unsigned seq, int t) {
+  if (unsigned long long* rec = trace_rec(peers, seq)) {
+    if (t == 0) rec[2] = __builtin_amdgcn_s_memrealtime();
+  }
   if (t < world && t != rank) {
     unsigned* f = (unsigned*)peers.mb[t] + rank * kFlagStride;
 #if LGA_COMM_FORMAL
@@ -76,14 +91,24 @@ __device__ __forceinline__ void wait_flags(const Peers& peers, int rank, int wor
     const bool mine = t < world && t != rank;
     const unsigned* f = (const unsigned*)peers.mb[rank] + (mine ? t : 0) * kFlagStride;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned v = seq;
+    bool timed_out = false;
     while (true) {
-      const unsigned v = mine ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : seq;
+      v = mine ? __hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : seq;
       if (__all((int)(v - seq) >= 0)) break;
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > 500000000ull) {
         if (t == 0) __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        timed_out = true;
         break;
       }
+    }
+    if (unsigned long long* rec = trace_rec(peers, seq)) {
+      if (t == 0) {
+        rec[3] = __builtin_amdgcn_s_memrealtime();
+        rec[4] = timed_out ? 1ull : 0ull;
+      }
+      if (t < world) rec[6 + t] = mine ? v : seq;
     }
 #if LGA_COMM_FORMAL
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");

@@ -22,6 +22,13 @@ namespace lga {
 
 constexpr int kCommThreads = 512;
 
+static unsigned long long* g_trace = nullptr;
+static int g_trace_n = 0;
+void comm_trace_get(unsigned long long** buf, int* n) {
+  *buf = g_trace;
+  *n = g_trace_n;
+}
+
 __global__ void __launch_bounds__(kCommThreads) allreduce_kernel(const uint16_t* __restrict__ x,
                                                                  const uint16_t* __restrict__ residual,
                                                                  uint16_t* __restrict__ y, int n, Peers peers,
@@ -29,8 +36,16 @@ __global__ void __launch_bounds__(kCommThreads) allreduce_kernel(const uint16_t*
                                                                  unsigned* __restrict__ seq_ctr,
                                                                  unsigned* __restrict__ err) {
   const int t = threadIdx.x;
-  const unsigned seq = __builtin_amdgcn_readfirstlane(*seq_ctr + 1u);  // uniform: the mailbox resources stay scalar
+  const unsigned raw = *seq_ctr;
+  const unsigned seq = __builtin_amdgcn_readfirstlane(raw + 1u);  // uniform: the mailbox resources stay scalar
   const int slot = seq & 1;
+  if (unsigned long long* rec = trace_rec(peers, seq)) {
+    if (t == 0) {
+      rec[0] = seq | ((unsigned long long)rank << 32) | (1ull << 40);
+      rec[1] = __builtin_amdgcn_s_memrealtime();
+      rec[5] = raw;
+    }
+  }
   const int n8 = n / 8;
   // 1. push this rank's partial into every peer's mailbox (16-B stores over xGMI)
   for (int r = 0; r < world; ++r) {
@@ -113,7 +128,18 @@ extern "C" int lga_allreduce_bf16(const void* x, const void* residual, void* y, 
     LGA_CHECK_ARG(mailboxes[r] != nullptr, "lga_allreduce_bf16: null mailbox");
     p.mb[r] = (unsigned char*)mailboxes[r];
   }
+  lga::comm_trace_get(&p.trace, &p.trace_n);
   lga::allreduce_kernel<<<1, lga::kCommThreads, 0, stream>>>((const uint16_t*)x, (const uint16_t*)residual,
                                                              (uint16_t*)y, n, p, rank, world, cap, seq_counter, err);
   LGA_LAUNCH_RETURN();
+}
+
+// Diagnostics: every later all-reduce launch of this process (one-shot and fused GEMV, captured ones included — the
+// pointer is baked into a graph at capture) records its call in buf (n_records x 16 uint64, indexed by sequence
+// number; layout in comm.h Peers). buf = null switches it off.
+extern "C" int lga_comm_trace(void* buf, int n_records) {
+  LGA_CHECK_ARG(!buf || n_records > 0, "lga_comm_trace: n_records must be positive");
+  lga::g_trace = (unsigned long long*)buf;
+  lga::g_trace_n = buf ? n_records : 0;
+  return 0;
 }

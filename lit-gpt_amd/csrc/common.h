@@ -83,6 +83,17 @@ inline int preload(F* f) {
   hipFuncAttributes a;
   return hipFuncGetAttributes(&a, (const void*)f) == hipSuccess ? 0 : 1;
 }
+// compute units of the current device (cached; 256 if the query fails)
+inline int num_cu() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
 int preload_gemm_q4f();
 int preload_attention();
 int preload_norm_rope();

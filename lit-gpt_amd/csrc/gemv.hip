@@ -68,15 +68,16 @@ __global__ void __launch_bounds__(256) gemv_q4s_kernel(GemvArgs a) {
   gemv_q4_stream<RT, CPT, FMT, DUAL, NORM, RES>(a, smem);
 }
 
-static int num_cu() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
+// greedy decode head: RMSNorm + lm_head GEMV (streaming form) + argmax + next-token embedding in one launch
+template <int RT, int CPT, int FMT, bool NORM>
+__global__ void __launch_bounds__(256) gemv_q4s_amax_kernel(GemvArgs a, AmaxArgs am) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  gemv_q4_stream<RT, CPT, FMT, false, NORM, false, true>(a, smem, am);
+}
+
+static int amax_grid(int N, int K) {  // the streaming form's grid for a plain GEMV (launch_stream, 3 per CU)
+  const int tiles = (N + 1) / 2;
+  return max(1, min(num_cu() * 3, (tiles + 3) / 4));
 }
 
 // streaming form (variant bit 2): RT rows per tile, `wpc` workgroups per CU (variant bits 4..7, default 2)
@@ -248,3 +249,43 @@ extern "C" int lga_gemv_trace_read(unsigned long long* host, int n) {
   return (int)e;
 }
 #endif
+
+extern "C" size_t lga_q4_gemv_argmax_work_bytes(int N, int K) {
+  return (size_t)lga::amax_grid(N, K) * 8 + 9 * 256;
+}
+
+extern "C" int lga_q4_gemv_argmax_embed(const void* x, const uint8_t* qweight, const void* scales,
+                                        const void* norm_weight, float norm_eps, void* logits, int N, int K, int group,
+                                        int fmt, void* work, int64_t* out_idx, int32_t* token_out, int64_t* pos_inout,
+                                        const void* table, int C, int V, void* emb_out, hipStream_t stream) {
+  LGA_CHECK_ARG(x && qweight && scales && logits && work, "lga_q4_gemv_argmax_embed: null pointer");
+  LGA_CHECK_ARG(N > 0 && K > 0 && K % 32 == 0 && K <= 4096, "lga_q4_gemv_argmax_embed: K must be a multiple of 32, <= 4096");
+  LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv_argmax_embed: bad group");
+  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_q4_gemv_argmax_embed: fmt must be 0, 1 or 3");
+  LGA_CHECK_ARG(!table || (emb_out && C > 0 && C % 8 == 0 && V > 0 && ((uintptr_t)table % 16) == 0 &&
+                           ((uintptr_t)emb_out % 16) == 0),
+                "lga_q4_gemv_argmax_embed: table and emb_out must be 16-B aligned rows of C % 8 == 0");
+  lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, nullptr, nullptr,
+                  (const uint16_t*)norm_weight, (uint16_t*)logits, N, K, group, norm_eps};
+  a.cb = lga::codebook_of(fmt);
+  const int blocks = lga::amax_grid(N, K);
+  lga::AmaxArgs am{(unsigned long long*)work, (unsigned*)((char*)work + (size_t)blocks * 8), out_idx, token_out,
+                   pos_inout, (const uint16_t*)table, (uint16_t*)emb_out, C, V};
+  const size_t lds = (size_t)K * 2 + (K / 32) * 4 + 16 * 4 + 16 * 4;
+  const int cpt = (K / 32 + 63) / 64, kf = lga::kernel_fmt(fmt);
+  const bool norm = norm_weight != nullptr;
+#define LGA_AM(CPT, FMT)                                                                                  \
+  do {                                                                                                    \
+    if (norm) lga::gemv_q4s_amax_kernel<2, CPT, FMT, true><<<blocks, 256, lds, stream>>>(a, am);          \
+    else lga::gemv_q4s_amax_kernel<2, CPT, FMT, false><<<blocks, 256, lds, stream>>>(a, am);              \
+  } while (0)
+  if (cpt == 1) {
+    if (kf == 0) LGA_AM(1, 0);
+    else LGA_AM(1, 1);
+  } else {
+    if (kf == 0) LGA_AM(2, 0);
+    else LGA_AM(2, 1);
+  }
+#undef LGA_AM
+  LGA_LAUNCH_RETURN();
+}

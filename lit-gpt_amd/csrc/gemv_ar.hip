@@ -85,6 +85,13 @@ __global__ void __launch_bounds__(256) gemv_q4_ar_kernel(GemvArgs a, ArArgs c) {
   __syncthreads();
   if (!s_last) return;
   // ---- the last arriver: every row of this rank is in every mailbox ----
+  if (unsigned long long* rec = trace_rec(c.peers, seq)) {
+    if (t == 0) {
+      rec[0] = seq | ((unsigned long long)c.rank << 32) | (2ull << 40);
+      rec[1] = __builtin_amdgcn_s_memrealtime();
+      rec[5] = seq - 1u;
+    }
+  }
   raise_flags(c.peers, c.rank, c.world, seq, t);
   wait_flags(c.peers, c.rank, c.world, seq, c.err, t);
   __syncthreads();
@@ -146,6 +153,7 @@ extern "C" int lga_q4_gemv_allreduce(const void* x, const uint8_t* qweight, cons
     LGA_CHECK_ARG(mailboxes[r] != nullptr, "lga_q4_gemv_allreduce: null mailbox");
     c.peers.mb[r] = (unsigned char*)mailboxes[r];
   }
+  lga::comm_trace_get(&c.peers.trace, &c.peers.trace_n);
   c.rank = rank;
   c.world = world;
   c.cap = cap;

@@ -50,6 +50,11 @@ struct GemvArgs {
   const uint16_t* probs = nullptr;
   int moe_swap = 0;
   float moe_pa = 0.0f, moe_pb = 0.0f;  // MOE2: the probabilities in addition order (read at kernel start)
+  // XWAIT (the out-projection inside the decode-attention launch): x is produced by other workgroups of the same
+  // launch; the body issues its weight / scale / residual loads first, then waits until *xwait reaches
+  // xwait_target (wrap-safe) and reads x with sc1 loads
+  const unsigned* xwait = nullptr;
+  unsigned xwait_target = 0;
 };
 
 // LDS of gemv_q4_body: x pairs (2K B), chunk sums (K/32 floats), norm partials (16), codebook (16), then (LDS_OUT)
@@ -68,9 +73,10 @@ __device__ __forceinline__ uint16_t* gemv_out_lds(unsigned char* smem, int K) { 
 // as the single-expert GEMV computes it — then the rows' two results meet in LDS and are summed as lga_moe_combine
 // does (ascending expert id, bf16 rounding points, + residual): the routed proj GEMV and the combine in one launch.
 template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, int NW = 4, bool LDS_OUT = false,
-          bool MOE2 = false>
+          bool MOE2 = false, bool XWAIT = false>
 __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char* smem) {
   static_assert(!MOE2 || (!DUAL && RES && !NORM && !LDS_OUT), "MOE2 runs as RES, without dual / norm / LDS output");
+  static_assert(!XWAIT || (!MOE2 && !NORM && !DUAL), "XWAIT: a plain (residual) projection");
   if (a.eidx) {  // wave-uniform: one scalar load of the routed expert id, then plain pointer offsets
     const long long e = min(max(a.eidx[blockIdx.y], 0), a.n_expert - 1);
     a.qw += e * a.ew;
@@ -106,7 +112,7 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
   // 1. activation (and norm weight) share of this thread: uint4 t, t+NT, ... (clamped, branch-free)
   uint4 xr[XI], nr[XI], xr2[MOE2 ? XI : 1];
 #pragma unroll
-  for (int i = 0; i < XI; ++i) {
+  for (int i = 0; i < (XWAIT ? 0 : XI); ++i) {
     const int u = min(t + NT * i, n8 - 1);
     if (MOE2) xr2[MOE2 ? i : 0] = ((const uint4*)(a.x + a.xs))[u];
 #ifdef LGA_LAB_NOX  // lab builds only: cost of the activation fetch
@@ -149,6 +155,26 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
   if (RES) res = a.residual[min(row0 + (lane & (RPR - 1)), a.N - 1)];
   __builtin_amdgcn_sched_barrier(0);  // nothing that waits on x may move above the weight loads
   LGA_GTRACE_NOWAIT(1);
+  if (XWAIT) {
+    // x comes from other workgroups of this launch (MI355X_MICROARCH.md "Valid forms" row 1): one lane polls the
+    // producers' agent-scope counter with sc1 loads, a workgroup barrier, then every x load is an sc1 load. The
+    // weights above stay in flight meanwhile. Bounded (1 s at 100 MHz) so a broken hand-off cannot hang the GPU.
+    if (t == 0) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while ((int)(__hip_atomic_load(a.xwait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.xwait_target) < 0 &&
+             __builtin_amdgcn_s_memrealtime() - t0 < 100000000ull)
+        __builtin_amdgcn_s_sleep(1);
+    }
+    __syncthreads();
+    const __amdgpu_buffer_rsrc_t xrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.K * 2, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < XI; ++i) {
+      const int u = min(t + NT * i, n8 - 1);
+      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(xrs, u * 16, 0, 16);  // sc1
+      xr[i] = make_uint4(v.x, v.y, v.z, v.w);
+    }
+  }
 
   // 3. stage x into LDS (RMS-normalised when NORM) while the weights stream
   float rs = 1.0f;

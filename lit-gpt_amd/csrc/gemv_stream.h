@@ -17,8 +17,36 @@ struct GemvTile {
   uint32_t res;
 };
 
-template <int RT, int CPT, int FMT, bool DUAL, bool NORM, bool RES>
-__device__ __forceinline__ void gemv_q4_stream(GemvArgs a, unsigned char* smem) {
+// AMAX (greedy decode: lm_head + argmax in one launch): every row's bf16 logit is also offered to a running
+// (value, index) arg-max with torch.argmax's order (NaN first, then larger, ties to the lower index — a strict total
+// order, so the reduction order never changes the winner); each workgroup publishes its winner, and the workgroup
+// that arrives last reduces them, writes the token / advances input_pos as lga_argmax does and gathers the token's
+// embedding row for the next step (lga_argmax_embed).
+struct AmaxArgs {
+  unsigned long long* cand;  // [gridDim.x] {value bits, index} written sc1
+  unsigned* cnt;             // 9 counters, 256 B apart: 8 per-(blockIdx % 8) classes + the top one (re-armed)
+  int64_t* out_idx;
+  int32_t* token_out;
+  int64_t* pos_inout;
+  const uint16_t* table;  // [V][C] bf16 or null
+  uint16_t* emb_out;
+  int C, V;
+};
+
+__device__ __forceinline__ bool amax_better(float v, int i, float bv, int bi) {  // = sample.hip better()
+  const bool vn = v != v, bn = bv != bv;
+  if (vn || bn) return vn && (!bn || i < bi);
+  return (v > bv) || (v == bv && i < bi);
+}
+__device__ __forceinline__ void amax_take(float v, int i, float& bv, int& bi) {
+  const bool t = amax_better(v, i, bv, bi);
+  bv = t ? v : bv;
+  bi = t ? i : bi;
+}
+
+template <int RT, int CPT, int FMT, bool DUAL, bool NORM, bool RES, bool AMAX = false>
+__device__ __forceinline__ void gemv_q4_stream(GemvArgs a, unsigned char* smem, AmaxArgs am = AmaxArgs{}) {
+  static_assert(!AMAX || (!DUAL && !RES), "AMAX: a plain (lm_head) GEMV");
   constexpr int NW = 4, NT = NW * 64;
   constexpr int XI = (CPT * 4 + NW - 1) / NW;
   using Tile = GemvTile<RT, CPT, FMT, DUAL>;
@@ -32,6 +60,8 @@ __device__ __forceinline__ void gemv_q4_stream(GemvArgs a, unsigned char* smem) 
   const int gw = blockIdx.x * NW + wave, W = gridDim.x * NW;
   const int T = (a.N + RT - 1) / RT;
   if (FMT == 1 && t < 16) nf4[t] = kCode4[a.cb][t];
+  // AMAX: the position is read up front (only the last workgroup uses it), so its update is a store, not a load
+  const int64_t am_p0 = (AMAX && am.pos_inout && t == 0) ? *am.pos_inout : 0;
 
   // 1. activation (and norm weight) share of this thread, first in the vmcnt order
   uint4 xr[XI], nr[XI];
@@ -113,6 +143,8 @@ __device__ __forceinline__ void gemv_q4_stream(GemvArgs a, unsigned char* smem) 
 
   // 4. tile loop: dot + butterfly + epilogue of tile k, then issue tile k + 2 into the freed buffer
   const uint32_t nmask = nibble_mask(), nmagic = f16_magic(), nmask_hi = nibble_mask_hi();
+  float abv = -INFINITY;  // AMAX: this lane's best (value, row)
+  int abi = 0x7FFFFFFF;
   auto consume = [&](const Tile& b, int tile) {
     float part[R];
 #pragma unroll
@@ -157,7 +189,11 @@ __device__ __forceinline__ void gemv_q4_stream(GemvArgs a, unsigned char* smem) 
       } else if (a.bias) {
         o += bf2f(a.bias[min(row, a.N - 1)]);
       }
-      if ((lane & (GROUP - 1)) == 0 && tile < T && row < a.N) a.y[row] = f2bf(o);
+      const uint16_t ob = f2bf(o);
+      if ((lane & (GROUP - 1)) == 0 && tile < T && row < a.N) {
+        a.y[row] = ob;
+        if (AMAX) amax_take(bf2f(ob), row, abv, abi);
+      }
     }
   };
   for (int tile = gw; tile < T; tile += 2 * W) {  // wave-uniform trip count
@@ -166,6 +202,70 @@ __device__ __forceinline__ void gemv_q4_stream(GemvArgs a, unsigned char* smem) 
     if (tile + W >= T) break;
     consume(B, tile + W);
     issue(B, tile + 3 * W);
+  }
+  if constexpr (AMAX) {
+    // workgroup winner: the wave's lanes, then the 4 waves through LDS (the x staging is no longer read)
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) amax_take(__shfl_xor(abv, off), __shfl_xor(abi, off), abv, abi);
+    __shared__ float s_v[NW];
+    __shared__ int s_i[NW];
+    __shared__ unsigned s_last;
+    if (lane == 0) {
+      s_v[wave] = abv;
+      s_i[wave] = abi;
+    }
+    __syncthreads();
+    if (t == 0) {
+      for (int w = 1; w < NW; ++w) amax_take(s_v[w], s_i[w], abv, abi);
+      // publish (MI355X_MICROARCH.md "Valid forms" row 1: an sc1 store, drained, then the agent-scope adds), then
+      // arrive on this workgroup's class counter; the last of a class arrives on the top counter
+      __hip_atomic_store(am.cand + blockIdx.x, ((unsigned long long)(unsigned)abi << 32) | __float_as_uint(abv),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned cls = blockIdx.x & 7, classes = min(gridDim.x, 8u);
+      const unsigned in_cls = (gridDim.x - cls + 7) / 8;
+      unsigned last = 0;
+      unsigned* cc = am.cnt + cls * 64;
+      if (__hip_atomic_fetch_add(cc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_cls - 1) {
+        __hip_atomic_store(cc, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm: the class is complete
+        unsigned* top = am.cnt + 8 * 64;
+        last = __hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == classes - 1;
+        if (last) __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // the last workgroup: every winner is published (each arrival followed its own drained sc1 store; the counter
+    // chain carries them here); reduce them with sc1 loads
+    float bv = -INFINITY;
+    int bi = 0x7FFFFFFF;
+    for (int i = t; i < (int)gridDim.x; i += NT) {
+      const unsigned long long c = __hip_atomic_load(am.cand + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      amax_take(__uint_as_float((unsigned)c), (int)(c >> 32), bv, bi);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) amax_take(__shfl_xor(bv, off), __shfl_xor(bi, off), bv, bi);
+    __shared__ int s_tok;
+    if (lane == 0) {
+      s_v[wave] = bv;
+      s_i[wave] = bi;
+    }
+    __syncthreads();
+    if (t == 0) {
+      for (int w = 1; w < NW; ++w) amax_take(s_v[w], s_i[w], bv, bi);
+      if (bi >= a.N) bi = 0;
+      if (am.out_idx) *am.out_idx = bi;
+      if (am.token_out) *am.token_out = bi;
+      if (am.pos_inout) *am.pos_inout = am_p0 + 1;
+      s_tok = bi;
+    }
+    if (am.table) {
+      __syncthreads();
+      const long id = min(max(s_tok, 0), am.V - 1);  // as lga_embedding: the gather stays in bounds
+      const uint4* src = (const uint4*)(am.table + (size_t)id * am.C);
+      for (int i = t; i < am.C / 8; i += NT) ((uint4*)am.emb_out)[i] = src[i];
+    }
   }
 }
 

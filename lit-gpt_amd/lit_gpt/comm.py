@@ -197,6 +197,18 @@ class XgmiAllReduce:
             self.cap, self.seq.data_ptr(), self.arrive.data_ptr(), self.err.data_ptr(), ops._stream()))
         return y
 
+    def enable_trace(self, n_records: int = 256) -> None:
+        """Diagnostics (lga_comm_trace): every later all-reduce launch of this process records its call — entry,
+        flags-raised and wait-done times, timeout, the peers' flag words seen — in a device buffer (``traces()``).
+        Process-wide; install it before capturing graphs that should record."""
+        self._trace = torch.zeros(n_records, 16, dtype=torch.int64, device=self.device)
+        ops._check(ops.load_library().lga_comm_trace(self._trace.data_ptr(), n_records))
+
+    def traces(self):
+        """The recorded calls as a (n, 16) int64 numpy array (rows of calls not made are zero); syncs."""
+        torch.cuda.synchronize(self.device)
+        return self._trace.cpu().numpy()
+
     def supports_rows(self, n: int) -> bool:
         return 0 < n <= self.cap and n % 8 == 0
 
@@ -209,6 +221,9 @@ class XgmiAllReduce:
     def close(self) -> None:
         lib = ops.load_library()
         torch.cuda.synchronize(self.device)
+        if getattr(self, "_trace", None) is not None:
+            lib.lga_comm_trace(None, 0)
+            self._trace = None
         self._mailboxes = None
         for p in self._opened:
             lib.lga_comm_close(p)

@@ -170,11 +170,13 @@ class GPT(nn.Module):
         return self.cos, self.sin
 
     def forward(self, idx: torch.Tensor, input_pos: Optional[torch.Tensor] = None, *,
-                last_token_only: bool = False, embedded: Optional[torch.Tensor] = None) -> torch.Tensor:
+                last_token_only: bool = False, embedded: Optional[torch.Tensor] = None,
+                hidden_only: bool = False) -> torch.Tensor:
         """(B=1, T) ids -> (1, T, padded_vocab) logits; ``last_token_only`` computes only the last row (1, 1, V)
         — all that ``generate`` samples from (generate/base.py:31). ``embedded`` (T * n_embd bf16) is
         ``transformer.wte(idx)`` already gathered — by the previous decode step's ``ops.argmax_embed`` in
-        ``DecodeGraph`` — and replaces the embedding launch."""
+        ``DecodeGraph`` — and replaces the embedding launch. ``hidden_only`` stops before ln_f / lm_head and returns
+        the last block's output (DecodeGraph runs the head fused with the greedy argmax)."""
         B, T = idx.shape
         if self.max_seq_length < T:
             raise ValueError(f"Cannot forward sequence of length {T}, max seq length is only {self.max_seq_length}.")
@@ -197,6 +199,8 @@ class GPT(nn.Module):
             x = block(x, cos, sin, None, input_pos)
         if last_token_only:
             x = x[:, -1:].contiguous()
+        if hidden_only:
+            return x
         ln = self.transformer.ln_f
         if isinstance(ln, RMSNorm):
             return _lin(self.lm_head, x, norm_weight=ln.weight, norm_eps=ln.eps)
@@ -296,6 +300,9 @@ class CausalSelfAttention(nn.Module):
     # decode tokens (T = 1) with full 128-dim rotary use lga_attention_decode_fused; False keeps the two-launch
     # rope_kv_append + attention path (bit-identical; tests compare the two)
     fuse_decode = True
+    # ... and the decode out-projection + residual inside that launch (lga_attention_decode_proj) where it covers the
+    # geometry; False keeps the separate proj GEMV launch (bit-identical; tests compare the two)
+    fuse_proj = True
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
                 input_pos: Optional[torch.Tensor] = None, *, norm: Optional["RMSNorm"] = None,
@@ -337,6 +344,13 @@ class CausalSelfAttention(nn.Module):
             if ws is None or ws.key != (1, H, G, hs, n_splits) or ws.counters.device != dev:
                 ws = self._attn_ws = ops.AttentionWorkspace(1, H, G, hs, n_splits, dev)
         if T == 1 and self.fuse_decode and ops.decode_fusable(hs, c.rope_n_elem) and qkv.dtype == torch.bfloat16:
+            if (self.fuse_proj and reduce is None and residual is not None and not self.proj._forward_hooks
+                    and ops.decode_proj_supported(H, G, hs, n_splits, self.proj)):
+                # decode token: RoPE + KV-append + attention + out-projection + residual in a single launch
+                out, _ = ops.attention_decode_proj(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem,
+                                                   1.0 / math.sqrt(hs), n_splits, ws, self.proj,
+                                                   residual.reshape(1, -1).contiguous())
+                return out.view(B, T, -1)
             # decode token: RoPE + KV-append + attention in a single launch
             y = ops.attention_decode_fused(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem,
                                            1.0 / math.sqrt(hs), n_splits, workspace=ws)

@@ -62,7 +62,12 @@ SIGNATURES = {
     "lga_attention": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_attention_workspace_bytes": [_I, _I, _I, _I],
     "lga_attention_decode_fused": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
+    "lga_attention_decode_proj_supported": [_I, _I, _I, _I, _I, _I, _I, _I],
+    "lga_attention_decode_proj": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P,
+                                  _P, _P, _P, _I, _I, _I, _P],
     "lga_argmax": [_P, _I, _P, _P, _P, _P],
+    "lga_q4_gemv_argmax_work_bytes": [_I, _I],
+    "lga_q4_gemv_argmax_embed": [_P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P],
     "lga_argmax_embed": [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P],
     "lga_moe_route": [_P, _I, _I, _I, _P, _P, _P],
     "lga_moe_gate_route": [_P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P],
@@ -84,6 +89,7 @@ SIGNATURES = {
     "lga_comm_open": [_P, ctypes.POINTER(_P)],
     "lga_comm_close": [_P],
     "lga_comm_free": [_P],
+    "lga_comm_trace": [_P, _I],
     "lga_allreduce_bf16": [_P, _P, _P, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P, _P],
     "lga_f32_linear": [_P, _P, _P, _P, _P, _I, _I, _I, _P],
     "lga_f32_layernorm": [_P, _P, _P, _P, _I, _I, _F, _P],
@@ -97,7 +103,7 @@ SIGNATURES = {
                               _P],
 }
 _RESTYPES = {"lga_q4f_workspace_bytes": ctypes.c_size_t, "lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
-             "lga_comm_mailbox_bytes": ctypes.c_size_t}
+             "lga_comm_mailbox_bytes": ctypes.c_size_t, "lga_q4_gemv_argmax_work_bytes": ctypes.c_size_t}
 
 _lib: Optional[ctypes.CDLL] = None
 
@@ -347,6 +353,8 @@ class AttentionWorkspace:
         # one counter per (row, query group, head slice): at most n_head of them per row (csrc/attention.hip
         # attn_hsplit deals a group's heads to up to q_per_kv workgroups when the groups are few)
         self.counters = torch.zeros(T * n_head * ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
+        # lga_attention_decode_proj's hand-off words (a monotonic counter and its per-launch base; never re-zeroed)
+        self.sync = torch.zeros(128, dtype=torch.int32, device=device)
 
 
 def attention(q, k_cache, v_cache, input_pos, n_head, n_query_groups, head_size, scale, n_splits=1,
@@ -397,6 +405,78 @@ def attention_decode_fused(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin,
         cos.shape[0], _dev(y, "y", torch.bfloat16), ws, cnt, n_head, n_query_groups, head_size, rope_n_elem, max_seq,
         n_splits, float(scale), _stream()))
     return y
+
+
+def decode_proj_supported(n_head, n_query_groups, head_size, n_splits, lin) -> bool:
+    """Whether lga_attention_decode_proj covers this decode step: a 4-bit ``QuantLinear`` out-projection of the
+    geometries the fused launch is built for (csrc/attention.hip proj_shape)."""
+    from lit_gpt.quantize import QuantLinear
+
+    if not isinstance(lin, QuantLinear) or lin.qweight.dtype != torch.uint8:
+        return False
+    return bool(load_library().lga_attention_decode_proj_supported(
+        n_head, n_query_groups, head_size, n_splits, lin.out_features, lin.in_features, lin.group, lin.fmt))
+
+
+def attention_decode_proj(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin, n_head, n_query_groups, head_size,
+                          rope_n_elem, scale, n_splits, workspace: AttentionWorkspace, lin, residual, out=None,
+                          y=None):
+    """One decode token: RoPE + KV-append + attention + the 4-bit out-projection + residual in ONE launch (reference
+    model.py:656 and :591). Returns (out (1, N), y (1, H*hs)); out is bit-identical to
+    ``q4_gemv(y, ..., residual=residual)``."""
+    if qkv.shape[0] != 1:
+        raise ValueError("attention_decode_proj handles exactly one token (T = 1)")
+    if workspace is None or workspace.key != (1, n_head, n_query_groups, head_size, n_splits):
+        raise ValueError("attention_decode_proj needs the layer's AttentionWorkspace")
+    max_seq = k_cache.shape[-2]
+    N = lin.out_features
+    y = y if y is not None else torch.empty(1, n_head * head_size, dtype=torch.bfloat16, device=qkv.device)
+    out = out if out is not None else torch.empty(1, N, dtype=torch.bfloat16, device=qkv.device)
+    _check(load_library().lga_attention_decode_proj(
+        _dev(qkv, "qkv", torch.bfloat16), _dev(k_cache, "k_cache", torch.bfloat16),
+        _dev(v_cache, "v_cache", torch.bfloat16), _dev(cache_pos, "cache_pos", torch.int64),
+        _dev(rope_pos, "rope_pos", torch.int64), _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32),
+        cos.shape[0], _dev(y, "y", torch.bfloat16), _dev(workspace.partials, "workspace", torch.float32),
+        _dev(workspace.counters, "counters", torch.int32), _dev(workspace.sync, "sync", torch.int32), n_head,
+        n_query_groups, head_size, rope_n_elem, max_seq, n_splits, float(scale),
+        _dev(lin.qweight, "qweight", torch.uint8), _dev(lin.scales, "scales"), _opt(lin.bias, "bias", torch.bfloat16),
+        _dev(residual, "residual", torch.bfloat16), _dev(out, "out", torch.bfloat16), N, lin.group, lin.fmt,
+        _stream()))
+    return out, y
+
+
+class HeadWorkspace:
+    """Scratch of the fused greedy head (lga_q4_gemv_argmax_embed): per-workgroup winners + arrival counters,
+    zeroed once; the kernel re-arms its counters, so it is reusable across launches and graph replays."""
+
+    def __init__(self, N: int, K: int, device) -> None:
+        nbytes = load_library().lga_q4_gemv_argmax_work_bytes(N, K)
+        self.key = (N, K)
+        self.buf = torch.zeros((nbytes + 7) // 8, dtype=torch.int64, device=device)
+
+
+def head_argmax_supported(lin) -> bool:
+    """Whether lga_q4_gemv_argmax_embed covers this lm_head: a 4-bit QuantLinear with K <= 4096, no bias."""
+    from lit_gpt.quantize import QuantLinear
+
+    return (isinstance(lin, QuantLinear) and lin.bias is None and lin.in_features <= 4096
+            and lin.in_features % 32 == 0 and lin.qweight.is_cuda)
+
+
+def q4_gemv_argmax_embed(x, lin, work: HeadWorkspace, *, norm_weight=None, eps=1e-5, table=None, emb_out=None,
+                         logits=None, out_idx=None, token_out=None, pos_inout=None):
+    """Greedy decode head in one launch: logits = lm_head(RMSNorm(x)), token = argmax(logits) (torch.argmax order),
+    the lga_argmax_embed bookkeeping (token_out, out_idx, pos_inout += 1, table row -> emb_out). Returns logits."""
+    N, K = lin.out_features, lin.in_features
+    logits = logits if logits is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
+    V, C = (table.shape if table is not None else (0, 0))
+    _check(load_library().lga_q4_gemv_argmax_embed(
+        _dev(x.reshape(-1), "x", torch.bfloat16), _dev(lin.qweight, "qweight", torch.uint8), _dev(lin.scales, "scales"),
+        _opt(norm_weight, "norm_weight", torch.bfloat16), float(eps), _dev(logits, "logits", torch.bfloat16), N, K,
+        lin.group, lin.fmt, _dev(work.buf, "work"), _opt(out_idx, "out_idx", torch.int64),
+        _opt(token_out, "token_out", torch.int32), _opt(pos_inout, "pos_inout", torch.int64),
+        _opt(table, "table", torch.bfloat16), C, V, _opt(emb_out, "emb_out", torch.bfloat16), _stream()))
+    return logits
 
 
 def preload_kernels() -> None:

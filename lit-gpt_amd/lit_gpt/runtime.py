@@ -57,11 +57,28 @@ class DecodeGraph:
                     self._step_body(self.history[i:i + 1])
             self.chunk_graph = gc
 
+    # greedy steps run ln_f + lm_head + argmax + the next embedding row as ONE launch (ops.q4_gemv_argmax_embed)
+    # where the head is a 4-bit Linear it covers; False keeps lm_head GEMV + argmax_embed (bit-identical)
+    fuse_head = True
+
     def _step_body(self, idx_out: Optional[torch.Tensor] = None, embedded: bool = True) -> None:
         fuse = self.fuse_embedding
-        logits = self.model(self.token, self.pos, last_token_only=True,
-                            embedded=self.x_emb if (fuse and embedded) else None).reshape(-1)
-        table = self.model.transformer.wte.weight if fuse else None
+        model = self.model
+        ln = model.transformer.ln_f
+        if (self.temperature == 0.0 and fuse and self.fuse_head and ops.head_argmax_supported(model.lm_head)
+                and type(ln).__name__ == "RMSNorm" and not model.lm_head._forward_hooks):
+            h = model(self.token, self.pos, last_token_only=True, embedded=self.x_emb if embedded else None,
+                      hidden_only=True).reshape(-1)
+            if getattr(self, "_head_ws", None) is None:
+                self._head_ws = ops.HeadWorkspace(model.lm_head.out_features, model.lm_head.in_features, h.device)
+                self.logits = torch.empty(model.lm_head.out_features, dtype=torch.bfloat16, device=h.device)
+            ops.q4_gemv_argmax_embed(h, model.lm_head, self._head_ws, norm_weight=ln.weight, eps=ln.eps,
+                                     table=model.transformer.wte.weight, emb_out=self.x_emb, logits=self.logits,
+                                     out_idx=idx_out, token_out=self.token.view(-1), pos_inout=self.pos)
+            return
+        logits = model(self.token, self.pos, last_token_only=True,
+                       embedded=self.x_emb if (fuse and embedded) else None).reshape(-1)
+        table = model.transformer.wte.weight if fuse else None
         if self.temperature > 0.0:
             ops.sample_topk(logits, self.top_k, self.temperature, seed=self.rng.seed, counter=self.rng.counter,
                             out_idx=idx_out, token_out=self.token.view(-1), pos_inout=self.pos, table=table,

@@ -252,6 +252,38 @@ class OracleGPT:
         return self._lin("lm_head", x)
 
 
+def one_block_rows(og: OracleGPT, idx: torch.Tensor, rows: List[int]) -> torch.Tensor:
+    """Rows ``rows`` of GPT.forward's logits (model.py:499-519, no cache) for a ONE-block model over idx (T,),
+    without the T x T work of a full forward: the qkv Linear and RoPE run over every position (the keys and values
+    every query sees), the query, attention, projection, MLP and head only for the requested rows. Row t of the
+    causal forward attends keys 0..t (SDPA is_causal, model.py:658-665) — exactly one query row over the prefix —
+    and is also what a decode step at input_pos t computes from a cache filled by the prefix (model.py:509, 788-795).
+    Long-prompt prefill parity (32k tokens) at a cost linear in T."""
+    c = og.cfg
+    if c.n_layer != 1 or c.parallel_residual:
+        raise NotImplementedError("one_block_rows: one sequential-residual block")
+    T = idx.numel()
+    G, hs, H = c.n_query_groups, c.head_size, c.n_head
+    qpk, n = H // G, c.rope_n_elem
+    cos, sin = build_rope_cache(T, n, c.rope_base, c.rope_condense_ratio, og.rope_pos_dtype)
+    x = og.p["transformer.wte.weight"][idx.long()]
+    qkv = og._lin("transformer.h.0.attn.attn", og._norm("transformer.h.0.norm_1", x)).view(T, G, qpk + 2, hs)
+    k = qkv[:, :, qpk].transpose(0, 1)  # (G, T, hs)
+    v = qkv[:, :, qpk + 1].transpose(0, 1)
+    k = torch.cat((apply_rope(k[..., :n], cos, sin), k[..., n:]), dim=-1)
+    out = []
+    for t in rows:
+        q = qkv[t, :, :qpk].reshape(H, 1, hs)
+        q = torch.cat((apply_rope(q[..., :n], cos[t:t + 1], sin[t:t + 1]), q[..., n:]), dim=-1)
+        y = F.scaled_dot_product_attention(q[None], k[None, :, : t + 1], v[None, :, : t + 1],
+                                           scale=1.0 / math.sqrt(hs), enable_gqa=G != H)
+        h = og._lin("transformer.h.0.attn.proj", y[0].transpose(0, 1).reshape(1, H * hs))
+        xr = h + x[t:t + 1]
+        xr = og._mlp(0, og._norm("transformer.h.0.norm_2", xr)) + xr
+        out.append(og._lin("lm_head", og._norm("transformer.ln_f", xr)))
+    return torch.cat(out)
+
+
 def sample(logits: torch.Tensor, temperature: float = 1.0, top_k: Optional[int] = None,
            multinomial: Optional[Callable[[torch.Tensor], torch.Tensor]] = None) -> torch.Tensor:
     """generate/base.py:30-41 on the last row of (T, V) logits; returns (1,) int64."""

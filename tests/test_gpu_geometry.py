@@ -129,3 +129,105 @@ def test_decode_attention_32k_context_mixtral_tp2_rank_shape():
         err = (y.double() - ref).abs()
         # bf16 output (2^-9 relative) + fp32 accumulation over 32k keys
         assert torch.all(err <= ref.abs() * 2 ** -7 + 2e-3), float(err.max())
+
+
+@pytest.mark.parametrize("name,mode", [("Llama-2-7b-hf", "int4-g128"), ("Mixtral-8x7B-v0.1", "nf4")])
+@torch.inference_mode()
+def test_decode_out_projection_inside_attention_launch_bit_identical(name, mode):
+    """The decode step's out-projection + residual inside the attention launch (CausalSelfAttention.fuse_proj,
+    lga_attention_decode_proj) gives bit-identical logits to the separate proj GEMV launch, at full width (7B's
+    32 groups; Mixtral's GQA, whose q_per_kv 4 runs as 2 head slices of 2)."""
+    from generate.base import build_model
+    from lit_gpt import Config
+    from lit_gpt.model import CausalSelfAttention
+
+    from lit_gpt import ops
+
+    cfg = Config.from_name(name, n_layer=1)
+    T, N = 300, 5  # a cache of >= 256 rows: the production split count (8 / 16), so the fused launch covers it
+    model = build_model(cfg, quantize=mode, device=DEV, seed=3, max_seq_length=T + N + 1)
+    attn = model.transformer.h[0].attn
+    H, G, hs = cfg.n_head, cfg.n_query_groups, cfg.head_size
+    assert ops.decode_proj_supported(H, G, hs, ops.decode_splits(G, H // G, hs, T + N + 1), attn.proj)
+    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=3)).to(DEV)
+    outs = {}
+    try:
+        for fused in (False, True):
+            CausalSelfAttention.fuse_proj = fused
+            for b in model.transformer.h:
+                b.attn.kv_cache.reset_parameters()
+            lg = model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1]
+            tok, seq = int(torch.argmax(lg)), []
+            for i in range(N):
+                lg = model(torch.tensor([[tok]], device=DEV), torch.tensor([T + i], device=DEV),
+                           last_token_only=True)[0, -1]
+                seq.append(lg.clone())
+                tok = int(torch.argmax(lg))
+            outs[fused] = torch.stack(seq)
+    finally:
+        CausalSelfAttention.fuse_proj = True
+    assert torch.equal(outs[False], outs[True])
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("T", [8192, 32000])
+@torch.inference_mode()
+def test_mixtral_tp2_rank_geometry_long_prompt_prefill(T):
+    """BASELINE config 5's long prompt (Mixtral block_size 32768, reference config.py:1294; generate/base.py:83-85
+    prefills the whole prompt in one forward): one full-width block at the TP=2 rank geometry (16 query heads, 4 KV
+    groups, experts of intermediate 7168), int4-g128, prefill of T tokens (MFMA GEMMs, grouped expert GEMMs over
+    2T routed rows, flash attention over T keys), then one decode step over the T-row cache. The last prefill row's
+    logits and the decode step's logits against the oracle (oracle.one_block_rows: the keys of every position, the
+    queries / MLP / head of those rows) in bf16 and float64 (tests/parity.py bounds)."""
+    from generate.base import build_model
+    from lit_gpt import Config
+
+    cfg = Config.from_name("Mixtral-8x7B-v0.1", n_layer=1, n_head=16, n_query_groups=4, intermediate_size=7168)
+    model = build_model(cfg, quantize="int4-g128", device=DEV, seed=11, max_seq_length=T + 2)
+    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=11)).to(DEV)
+    lg0 = model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1].float()
+    tok = int(torch.argmax(lg0))
+    lg1 = model(torch.tensor([[tok]], device=DEV), torch.tensor([T], device=DEV), last_token_only=True)[0, -1].float()
+    got = [lg0.cpu(), lg1.cpu()]
+    assert all(torch.isfinite(g).all() for g in got)
+
+    sd = oracle_state_from_model(model)
+    del model
+    torch.cuda.empty_cache()
+    idx = torch.cat([prompt.cpu().long(), torch.tensor([tok])])
+    refs = {}
+    for dt in (torch.bfloat16, torch.float64):
+        og = om.OracleGPT(cfg, sd, dtype=dt, rope_pos_dtype=torch.bfloat16)
+        refs[dt] = om.one_block_rows(og, idx, [T - 1, T])
+        del og
+    worst = max(check_step(got[i], refs[torch.bfloat16][i], refs[torch.float64][i], f"T={T} row {i}")
+                for i in range(2))
+    print(f"\nMixtral TP=2 rank, T={T}: worst max|d logit| / max|logit| = {worst:.4%}")
+
+
+@pytest.mark.timeout(600)
+@torch.inference_mode()
+def test_prefill_flash_attention_32k_sampled_rows_vs_fp64():
+    """The MFMA flash attention over a 32,000-token prompt at the Mixtral TP=2 rank geometry (16 heads, 4 groups):
+    a sample of query rows (first, middle, last tiles, and around the 128-row block edges) against an fp64 softmax of
+    the same bf16 q / K / V."""
+    from lit_gpt import ops
+
+    H, G, hs, T = 16, 4, 128, 32000
+    g = torch.Generator().manual_seed(21)
+    q = torch.randn(T, H, hs, generator=g).bfloat16()
+    k = torch.randn(G, T, hs, generator=g).bfloat16()
+    v = torch.randn(G, T, hs, generator=g).bfloat16()
+    pos = torch.arange(T)
+    y = ops.attention(q.to(DEV), k.to(DEV), v.to(DEV), pos.to(DEV), H, G, hs, 1.0 / math.sqrt(hs)).float().cpu()
+    y = y.view(T, H, hs)
+    rows = [0, 1, 127, 128, 4095, 16000, 16127, 16128, 31871, 31872, 31998, 31999]
+    qpk = H // G
+    for t in rows:
+        for h in (0, 5, 15):
+            kk, vv = k[h // qpk, : t + 1].double(), v[h // qpk, : t + 1].double()
+            s = kk @ q[t, h].double() / math.sqrt(hs)
+            ref = torch.softmax(s, 0) @ vv
+            err = (y[t, h].double() - ref).abs()
+            # bf16 P entering P.V (as SDPA's bf16 math) + bf16 output; fp32 accumulation over up to 32k keys
+            assert torch.all(err <= ref.abs() * 2 ** -6 + 5e-3), (t, h, float(err.max()))

@@ -728,3 +728,122 @@ def test_attention_decode_head_slices_agree(ops, H, G, splits, monkeypatch):
     for y, (kb, vb) in zip(outs[1:], caches[1:]):
         assert torch.equal(kb, caches[0][0]) and torch.equal(vb, caches[0][1])
         assert torch.all((y - outs[0]).abs() <= outs[0].abs() * 2 ** -7 + 2e-3)
+
+
+@pytest.mark.parametrize("H,G", [(32, 32), (32, 8)])
+@pytest.mark.parametrize("mode,bias", [("int4-g128", False), ("nf4", False), ("int4-g128", True), ("bnb.fp4", False)])
+def test_attention_decode_proj_bit_identical_to_two_launches(ops, H, G, mode, bias):
+    """RoPE + KV append + attention + out-projection + residual in ONE launch (lga_attention_decode_proj) ==
+    lga_attention_decode_fused then lga_q4_gemv(residual): caches, the attention row and the projected row all
+    bit-identical, over positions that include a repeat (the hand-off words advance per launch) and p = 0."""
+    from lit_gpt.quantize import QuantLinear
+
+    hs, S = 128, 2304
+    C = H * hs
+    qkv = to_dev_bf16(synth.normal((1, (H + 2 * G) * hs), "pq", 9, 1.0))
+    k0 = to_dev_bf16(synth.normal((G, S, hs), "pk", 9, 1.0))
+    v0 = to_dev_bf16(synth.normal((G, S, hs), "pv", 9, 1.0))
+    cos, sin = om.build_rope_cache(S, hs, 10000)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    w = torch.from_numpy(synth.normal((C, C), "pw", 9, 0.02)).float()
+    b = torch.from_numpy(synth.normal((C,), "pb", 9, 0.5)).float() if bias else None
+    lin = QuantLinear.from_float(w, b, mode, torch.device(DEV))
+    res = to_dev_bf16(synth.normal((1, C), "pr", 9, 1.0))
+    splits = ops.decode_splits(G, H // G, hs, S)
+    assert ops.decode_proj_supported(H, G, hs, splits, lin)
+    ws_a = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
+    ws_b = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
+    ka, va, kb, vb = k0.clone(), v0.clone(), k0.clone(), v0.clone()
+    scale = 1.0 / math.sqrt(hs)
+    for p in (2047, 0, 1, 37, 2303, 2047, 1000):
+        pos = torch.tensor([p], device=DEV)
+        ya = ops.attention_decode_fused(qkv, ka, va, pos, pos, cos, sin, H, G, hs, hs, scale, splits, workspace=ws_a)
+        oa = ops.q4_gemv(ya.view(-1), lin.qweight, lin.scales, C, C, lin.group, lin.fmt, bias=lin.bias,
+                         residual=res.view(-1))
+        ob, yb = ops.attention_decode_proj(qkv, kb, vb, pos, pos, cos, sin, H, G, hs, hs, scale, splits, ws_b, lin,
+                                           res)
+        assert torch.equal(ka, kb) and torch.equal(va, vb), p
+        assert torch.equal(ya, yb), p
+        assert torch.equal(oa.view(-1), ob.view(-1)), p
+    assert int(ws_b.counters.abs().sum()) == 0
+
+
+@torch.inference_mode()
+def test_attention_decode_proj_graph_replay(ops):
+    """The fused attention + projection captured in a HIP graph and replayed at advancing positions (the position
+    updated on the device between replays, as DecodeGraph does) equals the eager two-launch path step by step."""
+    from lit_gpt.quantize import QuantLinear
+
+    H = G = 32
+    hs, S = 128, 2304
+    C = H * hs
+    qkv = to_dev_bf16(synth.normal((1, (H + 2 * G) * hs), "gq", 9, 1.0))
+    k0 = to_dev_bf16(synth.normal((G, S, hs), "gk", 9, 1.0))
+    v0 = to_dev_bf16(synth.normal((G, S, hs), "gv", 9, 1.0))
+    cos, sin = om.build_rope_cache(S, hs, 10000)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    lin = QuantLinear.from_float(torch.from_numpy(synth.normal((C, C), "gw", 9, 0.02)).float(), None, "int4-g128",
+                                 torch.device(DEV))
+    res = to_dev_bf16(synth.normal((1, C), "gr", 9, 1.0))
+    splits = ops.decode_splits(G, H // G, hs, S)
+    ws_a = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
+    ws_b = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
+    ka, va, kb, vb = k0.clone(), v0.clone(), k0.clone(), v0.clone()
+    scale = 1.0 / math.sqrt(hs)
+    pos_g = torch.tensor([2040], device=DEV)
+    ob, yb = ops.attention_decode_proj(qkv, kb, vb, pos_g, pos_g, cos, sin, H, G, hs, hs, scale, splits, ws_b, lin,
+                                       res)  # warm-up launch (outside the graph)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        ops.attention_decode_proj(qkv, kb, vb, pos_g, pos_g, cos, sin, H, G, hs, hs, scale, splits, ws_b, lin, res,
+                                  out=ob, y=yb)
+        pos_g.add_(1)
+    pos_a = torch.tensor([2040], device=DEV)
+    ya = ops.attention_decode_fused(qkv, ka, va, pos_a, pos_a, cos, sin, H, G, hs, hs, scale, splits, workspace=ws_a)
+    pos_g.fill_(2041)
+    for step in range(6):
+        pos_a.fill_(2041 + step)
+        ya = ops.attention_decode_fused(qkv, ka, va, pos_a, pos_a, cos, sin, H, G, hs, hs, scale, splits,
+                                        workspace=ws_a)
+        oa = ops.q4_gemv(ya.view(-1), lin.qweight, lin.scales, C, C, lin.group, lin.fmt, residual=res.view(-1))
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(pos_g.item()) == 2042 + step
+        assert torch.equal(ya, yb) and torch.equal(oa.view(-1), ob.view(-1)), step
+    assert torch.equal(ka, kb) and torch.equal(va, vb)
+
+
+@pytest.mark.parametrize("mode,N,K", [("int4-g128", 32000, 4096), ("nf4", 32000, 4096), ("int4-g128", 50304, 2048),
+                                      ("bnb.fp4", 1000, 256)])
+@pytest.mark.parametrize("tie", [False, True])
+def test_fused_greedy_head_bit_identical(ops, mode, N, K, tie):
+    """lga_q4_gemv_argmax_embed (RMSNorm + lm_head GEMV + argmax + the next token's embedding row, one launch) ==
+    lga_q4_gemv(norm) then lga_argmax_embed: logits, token, index, position and embedding row bit-identical; with
+    ``tie`` the winning row is duplicated further down, so the lowest index must win (torch.argmax order). Several
+    launches on one workspace (its arrival counters re-arm)."""
+    from lit_gpt.quantize import QuantLinear
+
+    g = torch.Generator().manual_seed(N + K)
+    w = torch.randn(N, K, generator=g) * 0.02
+    if tie:
+        w[N // 3] = w[7] = torch.randn(K, generator=g) * 0.2  # two identical rows: equal logits
+    lin = QuantLinear.from_float(w, None, mode, torch.device(DEV))
+    nw = (1.0 + torch.randn(K, generator=g) * 0.1).bfloat16().to(DEV)
+    table = torch.randn(N, 64, generator=g).bfloat16().to(DEV)
+    work = ops.HeadWorkspace(N, K, DEV)
+    for it in range(3):
+        x = (torch.randn(K, generator=g) * 2).bfloat16().to(DEV)
+        la = ops.q4_gemv(x, lin.qweight, lin.scales, N, K, lin.group, lin.fmt, norm_weight=nw)
+        ia, ta, pa = (torch.zeros(1, dtype=torch.int64, device=DEV), torch.zeros(1, dtype=torch.int32, device=DEV),
+                      torch.tensor([100 + it], device=DEV))
+        ea = torch.empty(64, dtype=torch.bfloat16, device=DEV)
+        ops.argmax_embed(la, table, ea, out_idx=ia, token_out=ta, pos_inout=pa)
+        ib, tb, pb = torch.zeros_like(ia), torch.zeros_like(ta), torch.tensor([100 + it], device=DEV)
+        eb = torch.empty_like(ea)
+        lb = ops.q4_gemv_argmax_embed(x, lin, work, norm_weight=nw, table=table, emb_out=eb, out_idx=ib,
+                                      token_out=tb, pos_inout=pb)
+        assert torch.equal(la, lb) and int(ia) == int(ib) and int(ta) == int(tb) and int(pa) == int(pb) == 101 + it
+        assert torch.equal(ea, eb)
+        if tie and it == 0:
+            assert int(ib) == 7 or float(la[int(ib)]) > float(la[7])
+    assert int(work.buf[-(9 * 256) // 8:].abs().sum()) == 0  # counters re-armed

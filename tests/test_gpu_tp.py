@@ -39,6 +39,8 @@ def _launch(worker, nproc, args, timeout=540):
     # scheduler (a time-sliced peer looks like a lost one: the 5 s bound and stale-looking bursts). One process per
     # GPU, the deployment the kernels are built for, never shares the queues.
     env = dict(os.environ, OMP_NUM_THREADS="2", GPU_MAX_HW_QUEUES="1")
+    if os.environ.get("LGA_TP_TEST_HW_QUEUES"):  # diagnostics: the queue count under which the bursts once timed out
+        env["GPU_MAX_HW_QUEUES"] = os.environ["LGA_TP_TEST_HW_QUEUES"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
     errors = [ln for ln in r.stderr.splitlines() if "Error" in ln and "ChildFailedError" not in ln]
     assert r.returncode == 0, ("\n".join(errors[:8]), r.stdout[-2000:], r.stderr[-3000:])
@@ -61,6 +63,7 @@ def test_xgmi_allreduce_bit_exact_vs_ordered_sum(nproc, tmp_path):
     8-slot mailboxes and flags all in use), each bit-exact vs the ordered fp32 sum over ranks."""
     out = tmp_path / "status.txt"
     _launch("allreduce_worker.py", nproc, [out], timeout=280)
+    print(Path(str(out) + ".trace.txt").read_text())  # per-call protocol timeline (shown with pytest -s / failures)
     assert out.read_text() == "ok", out.read_text()
 
 
@@ -81,6 +84,7 @@ def test_fused_gemv_allreduce_bit_exact_vs_two_launches(nproc, tmp_path):
     residual, graph-captured (mixed with plain all-reduce calls in one sequence) and back-to-back eager calls."""
     out = tmp_path / "status.txt"
     _launch("gemv_allreduce_worker.py", nproc, [out], timeout=280)
+    print(Path(str(out) + ".trace.txt").read_text())
     assert out.read_text() == "ok", out.read_text()
 
 

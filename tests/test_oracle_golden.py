@@ -236,3 +236,26 @@ def test_reference_tp_logits_equal_unsharded_oracle(fam, world, golden):
     got_q = torch.stack(got_q).float().numpy()
     # reference side ran in bf16: bf16 activation rounding vs the fp32 oracle
     assert np.abs(got_q - ref_q).max() <= 0.03 * np.abs(ref_q).max()
+
+
+@pytest.mark.parametrize("name,kw", [("Llama-2-7b-hf", dict(n_embd=128, n_head=8, n_query_groups=2,
+                                                             intermediate_size=256)),
+                                     ("Mixtral-8x7B-v0.1", dict(n_embd=128, n_head=8, n_query_groups=2,
+                                                                intermediate_size=96))])
+def test_one_block_rows_equal_full_forward(name, kw):
+    """oracle.one_block_rows (linear-cost rows of a one-block forward, used for the 32k-prompt prefill parity) ==
+    OracleGPT.forward's rows, exactly, in float64 — the full causal forward is the reference restatement."""
+    import sys
+    from pathlib import Path
+
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "lit-gpt_amd"))
+    from lit_gpt import Config
+
+    cfg = Config.from_name(name, n_layer=1, vocab_size=256, padded_vocab_size=256, **kw)
+    og = om.OracleGPT(cfg, synth.state_dict(cfg, seed=4), dtype=torch.float64)
+    T = 70
+    idx = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=4))
+    full = og.forward(idx)
+    rows = [0, 1, 33, T - 2, T - 1]
+    got = om.one_block_rows(og, idx, rows)
+    assert torch.allclose(got, full[rows], rtol=1e-12, atol=1e-12)

@@ -40,6 +40,7 @@ def main():
     c = comm.XgmiAllReduce(device=DEV)
     if "--late-peer" in sys.argv:
         return late_peer(c, out, world, rank)
+    c.enable_trace(512)  # every call's protocol record (entry / flags raised / wait done / flags seen), per rank
     bad = []
     it = 0
     for n in (4096, 8192, 32768, 8):
@@ -86,11 +87,59 @@ def main():
             bad.append(f"burst call {k}")
             break
     err = c.errors()
+    report = trace_report(c, world, rank, bad, err)
     dist.barrier()
     c.close()
     if rank == 0:
-        Path(out).write_text("ok" if not bad and err == 0 else f"FAIL err={err} {bad[:5]}")
+        Path(out + ".trace.txt").write_text(report)
+        Path(out).write_text("ok" if not bad and err == 0 else f"FAIL err={err} {bad[:5]}\n{report[-6000:]}")
     dist.destroy_process_group()
+
+
+def trace_report(c, world, rank, bad, err):
+    """Every rank's protocol records, gathered on rank 0: per call (sequence number) and rank the entry, flags-raised
+    and wait-done times (us from the earliest entry of that call on any rank; one clock per device), whether the wait
+    timed out, the sequence word read at entry and the flag words seen. Failing or slow calls are listed in full."""
+    import numpy as np
+
+    mine = {"rank": rank, "trace": c.traces(), "seq": int(c.seq.item()), "err": int(err), "bad": bad}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    if rank != 0:
+        return ""
+    lines = [f"ranks {world}; per rank: seq counter " + " ".join(str(d["seq"]) for d in allr)
+             + "; err " + " ".join(str(d["err"]) for d in allr)]
+    seqs = sorted({int(r[0]) & 0xFFFFFFFF for d in allr for r in d["trace"] if r[0]})
+    worst = []
+    for s in seqs:
+        recs = []
+        for d in allr:
+            r = [x for x in d["trace"] if x[0] and (int(x[0]) & 0xFFFFFFFF) == s]
+            recs.append(r[0] if r else None)
+        if any(x is None for x in recs):
+            worst.append((1e9, s, recs))
+            continue
+        t0 = min(int(x[1]) for x in recs)
+        span = (max(int(x[3]) for x in recs) - t0) / 100.0
+        worst.append((span + (1e8 if any(int(x[4]) for x in recs) else 0), s, recs))
+    worst.sort(key=lambda w: -w[0])
+    spans = sorted(w[0] for w in worst if w[0] < 1e8)
+    if spans:
+        lines.append(f"calls {len(seqs)}; entry->last wait done us: median {np.median(spans):.1f} "
+                     f"p90 {np.percentile(spans, 90):.1f} max {spans[-1]:.1f}")
+    for score, s, recs in worst[:6]:
+        lines.append(f"seq {s}:" + (" TIMED OUT" if score >= 1e8 else "") + ("" if score < 1e9 else " (missing)"))
+        ok = [x for x in recs if x is not None]
+        t0 = min(int(x[1]) for x in ok) if ok else 0
+        for r, x in enumerate(recs):
+            if x is None:
+                lines.append(f"   rank {r}: no record")
+                continue
+            kind = {1: "oneshot", 2: "gemv"}.get(int(x[0]) >> 40, "?")
+            lines.append(f"   rank {r} {kind}: entry {(int(x[1]) - t0) / 100:9.2f} raised {(int(x[2]) - t0) / 100:9.2f} "
+                         f"done {(int(x[3]) - t0) / 100:9.2f} timeout {int(x[4])} seqword {int(x[5])} "
+                         f"flags {[int(v) for v in x[6:6 + world]]}")
+    return "\n".join(lines) + "\n"
 
 
 def late_peer(c, out, world, rank):

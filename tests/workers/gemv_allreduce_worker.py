@@ -13,7 +13,7 @@ import torch
 import torch.distributed as dist
 
 REPO = Path(__file__).resolve().parents[2]
-sys.path[:0] = [str(REPO / "lit-gpt_amd"), str(REPO)]
+sys.path[:0] = [str(REPO / "lit-gpt_amd"), str(REPO), str(Path(__file__).resolve().parent)]
 
 from lit_gpt import comm  # noqa: E402
 from lit_gpt.quantize import QuantLinear  # noqa: E402
@@ -37,6 +37,7 @@ def main():
     if "--time" in sys.argv:
         return timing(c, out, world, rank)
     bad = [] if c.fused_ok else [f"start-up self-test: {c.fused_fallback}"]
+    c.enable_trace(512)  # every call's protocol record, per rank (allreduce_worker.trace_report)
     # (N, K per rank, mode, bias): 7B attn.proj / mlp.proj shards at this world size, 70B-like widths, fp4 / nf4
     cases = [(4096, 4096 // world, "int4-g128", False), (4096, 11008 // world, "int4-g128", False),
              (8192, 8192 // world, "nf4", False), (4096, 2048, "bnb.fp4", True), (1024, 1376, "int4-g32", False)]
@@ -93,10 +94,14 @@ def main():
             bad.append(f"burst call {k}")
             break
     err = c.errors()
+    from allreduce_worker import trace_report
+
+    report = trace_report(c, world, rank, bad, err)
     dist.barrier()
     c.close()
     if rank == 0:
-        Path(out).write_text("ok" if not bad and err == 0 else f"FAIL err={err} {bad[:5]}")
+        Path(out + ".trace.txt").write_text(report)
+        Path(out).write_text("ok" if not bad and err == 0 else f"FAIL err={err} {bad[:5]}\n{report[-6000:]}")
     dist.destroy_process_group()
 
 
