@@ -152,7 +152,7 @@ int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, co
 /* lga_attention_decode_proj: lga_attention_decode_fused followed, in the SAME launch, by the out-projection
  * `self.proj(y)` (lit_gpt/model.py:656; the 4-bit Linear bnb's gemv_4bit serves at reference generate/base.py:128-136)
  * and the Block residual add `x + h` (model.py:591): out (N) = bf16(proj(y) [+ bias]) + residual, bit-identical to
- * lga_q4_gemv(y, ..., residual). y (n_head*hs bf16) still receives the attention row. sync: 128 zeroed uint32 per
+ * lga_q4_gemv(y, ..., residual). y (n_head*hs bf16) still receives the attention row. sync: 1024 zeroed uint32 per
  * workspace (hand-off counter + base; never re-zeroed). Covers the geometries lga_attention_decode_proj_supported
  * reports (hs 128, n_splits >= 2, K = n_head*hs = 4096, q_per_kv slice 1 or 2, grid <= CUs); TP's row-parallel
  * projection keeps its own launch. */

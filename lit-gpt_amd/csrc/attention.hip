@@ -56,12 +56,14 @@ __device__ __forceinline__ uint4 ld_kv(const uint16_t* p) {
 // at p (KVCache.forward, lit_gpt/model.py:788-795) and scores that key from registers — replacing the separate
 // lga_rope_kv_append launch of the decode step.
 // PROJ (decode, fused, tensor parallelism off): the attention output row y is handed to the out-projection GEMV that
-// every workgroup of the SAME launch runs afterwards (attn_proj_kernel). The combining splits store y write-through
-// (sc1), drain, and add 1 to sync[kHeads]; the projection's workgroups issue their weight loads first and wait until
-// sync[kHeads] reaches base + C (C = combining workgroups per launch, base = sync[kBase] read at kernel start). The
-// combiner whose add completes the launch moves sync[kBase] to base + C — every workgroup has read the base by then:
-// each one holds an arrival ticket of some combined head, and a head combines only after all its splits arrived.
-constexpr int kHeads = 0, kBase = 64;  // sync words, 256 B apart
+// the publishing (non-combining) workgroups of the SAME launch run afterwards (attn_proj_kernel). The combining splits
+// store y write-through (sc1), drain, and add 1 to each of kReplicas replicas of a counter (one wave instruction, one
+// lane per replica: MI355X_MICROARCH.md "Valid forms" row 2); a projection workgroup issues its weight loads first,
+// then polls ONE replica until it reaches base + C (C = combining workgroups per launch, base = sync[kBase] read at
+// kernel start) — eight polled lines instead of one. The combiner whose add completes the launch moves sync[kBase] to
+// base + C: every workgroup has read the base by then (each holds an arrival ticket of some combined head, and a head
+// combines only after all its splits arrived).
+constexpr int kReplicas = 8, kBase = kReplicas * 64;  // sync words: replica r at r * 64 (256 B apart), then the base
 
 template <int HS, int QPK, int UNR, int NW, bool FUSED, bool PIPE, bool PROJ>
 __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
@@ -70,7 +72,7 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
                                           unsigned* __restrict__ cnt, int n_head, int max_seq, float scale,
                                           const int64_t* __restrict__ rope_pos, const float* __restrict__ cos,
                                           const float* __restrict__ sin, int rope_rows, int hsplit,
-                                          unsigned* __restrict__ sync, unsigned base) {
+                                          unsigned* __restrict__ sync, unsigned base, int* role = nullptr) {
   constexpr int LPR = HS / 8;    // lanes per key row
   constexpr int RGW = 64 / LPR;  // row groups per wave
   constexpr int RG = NW * RGW;   // row groups per workgroup
@@ -312,7 +314,11 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
   if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   LGA_TRACE(5);
-  if (s_ticket != (unsigned)(n_splits - 1)) return;
+  if (s_ticket != (unsigned)(n_splits - 1)) {
+    if (PROJ) *role = (int)s_ticket;  // a publisher: its arrival ticket (uniform, from LDS)
+    return;
+  }
+  if (PROJ) *role = -1;  // the combiner of this (t, group slice)
   // one output column quad per thread, 8 splits per round with every load of the round in flight at once and an
   // online rescale across rounds. Split 0 always holds key 0, so the running max is finite after round 0; empty
   // splits carry m = kMFloor, l = 0, o = 0 and clamped out-of-range slots are forced to m = -inf: both weigh 0.
@@ -357,13 +363,15 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
       *(uint2*)yr = yv;
   }
   if (threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-  if (PROJ) {  // y of this (t, group slice) is out: every storing wave drains, a barrier, one lane counts it
+  if (PROJ) {  // y of this (t, group slice) is out: every storing wave drains, a barrier, one instruction counts it
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < kReplicas) {
       const unsigned C = gridDim.y * gridDim.z;
-      const unsigned prev = __hip_atomic_fetch_add(sync + kHeads, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (prev == base + C - 1u) __hip_atomic_store(sync + kBase, base + C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned prev =
+          __hip_atomic_fetch_add(sync + threadIdx.x * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x == 0 && prev == base + C - 1u)
+        __hip_atomic_store(sync + kBase, base + C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   LGA_TRACE(6);
@@ -395,6 +403,9 @@ struct ProjArgs {
   int N, K, group, cb;
 };
 
+// Row blocks of NW * RPR rows: publisher `slot` (its head slice gy * (n_splits - 1) + its arrival ticket) takes two
+// adjacent blocks while slot < n2 (one GEMV of 2 RPR rows per wave), one block after: n2 = blocks - publishers, so
+// every row is covered and the combiners — the last splits to finish — compute none.
 template <int HS, int QPK, int UNR, int NW, int RPR, int CPT, int FMT>
 __global__ void __launch_bounds__(NW * 64) attn_proj_kernel(const uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
                                                         uint16_t* __restrict__ vc, const int64_t* __restrict__ input_pos,
@@ -405,16 +416,19 @@ __global__ void __launch_bounds__(NW * 64) attn_proj_kernel(const uint16_t* __re
                                                         int rope_rows, int hsplit, ProjArgs pa) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const unsigned base = pa.sync[kBase];  // written only by the previous launch's last combiner (kernel boundary)
+  int role = -1;
   attn_body<HS, QPK, UNR, NW, true, LGA_ATTN_PIPE != 0, true>(q, kc, vc, input_pos, y, ws, cnt, n_head, max_seq,
                                                               scale, rope_pos, cos, sin, rope_rows, hsplit, pa.sync,
-                                                              base);
-  const int blk = blockIdx.y * gridDim.x + blockIdx.x;
-  if (blk * NW * RPR >= pa.N) return;
+                                                              base, &role);
+  if (role < 0) return;  // combiners compute no projection rows
+  const int slot = blockIdx.y * (gridDim.x - 1) + role;
+  const int publishers = gridDim.y * (gridDim.x - 1), blocks = pa.N / (NW * RPR), n2 = blocks - publishers;
   GemvArgs a{y, pa.qw, pa.sc, nullptr, nullptr, pa.bias, pa.residual, nullptr, pa.out, pa.N, pa.K, pa.group, 0.0f};
   a.cb = pa.cb;
-  a.xwait = pa.sync + kHeads;
+  a.xwait = pa.sync + ((blockIdx.x + blockIdx.y) % kReplicas) * 64;
   a.xwait_target = base + gridDim.y * gridDim.z;
-  gemv_q4_body<RPR, CPT, FMT, false, false, true, NW, false, false, true>(a, blk, smem);
+  if (slot < n2) gemv_q4_body<2 * RPR, CPT, FMT, false, false, true, NW, false, false, true>(a, slot, smem);
+  else gemv_q4_body<RPR, CPT, FMT, false, false, true, NW, false, false, true>(a, 2 * n2 + (slot - n2), smem);
 }
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -1027,10 +1041,10 @@ static int proj_shape(int H, int G, int hs, int n_splits, int N, int K, int grou
   const int qpk = H / G / hsplit;
   if (qpk != 1 && qpk != 2) return 0;
   if (qpk == 1 && G * hsplit <= 16) return 0;  // the 8-wave few-groups config: not instantiated
-  const long wgs = (long)n_splits * G * hsplit;
-  // every workgroup holds one 16-row block of the projection and the whole grid must be resident at once (the
-  // projection's workgroups wait for heads combined by others of the same launch)
-  if (wgs * 16 < N || wgs > num_cu()) return 0;
+  const long wgs = (long)n_splits * G * hsplit, publishers = (long)(n_splits - 1) * G * hsplit, blocks = N / 16;
+  // the publishers hold one or two 16-row blocks of the projection each, and the whole grid must be resident at once
+  // (the projection's workgroups wait for heads combined by others of the same launch)
+  if (blocks < publishers || blocks > 2 * publishers || wgs > num_cu()) return 0;
   if (hsplit_out) *hsplit_out = hsplit;
   return qpk;
 }

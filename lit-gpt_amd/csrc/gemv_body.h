@@ -163,7 +163,7 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       while ((int)(__hip_atomic_load(a.xwait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.xwait_target) < 0 &&
              __builtin_amdgcn_s_memrealtime() - t0 < 100000000ull)
-        __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_s_sleep(2);
     }
     __syncthreads();
     const __amdgpu_buffer_rsrc_t xrs =

@@ -302,7 +302,7 @@ class CausalSelfAttention(nn.Module):
     fuse_decode = True
     # ... and the decode out-projection + residual inside that launch (lga_attention_decode_proj) where it covers the
     # geometry; False keeps the separate proj GEMV launch (bit-identical; tests compare the two)
-    fuse_proj = True
+    fuse_proj = os.environ.get("LGA_FUSE_PROJ", "1") != "0"
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
                 input_pos: Optional[torch.Tensor] = None, *, norm: Optional["RMSNorm"] = None,

@@ -112,8 +112,9 @@ class NativeLibraryError(RuntimeError):
     pass
 
 
-def load_library(path: Optional[Path] = None) -> ctypes.CDLL:
-    """Load (once) and return the HIP library. Raises loudly when it is missing: there is no fallback."""
+def load_library(path: Optional[Path] = None, strict: bool = True) -> ctypes.CDLL:
+    """Load (once) and return the HIP library. Raises loudly when it is missing: there is no fallback.
+    ``strict=False`` (lab A/B of older builds only) skips the symbols a library does not export."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -124,6 +125,8 @@ def load_library(path: Optional[Path] = None) -> ctypes.CDLL:
             "or `make -C lit-gpt_amd/csrc` (hipcc --offload-arch=gfx950). There is no CPU fallback.")
     lib = ctypes.CDLL(str(p))
     for name, argtypes in SIGNATURES.items():
+        if not strict and not hasattr(lib, name):
+            continue
         fn = getattr(lib, name)
         fn.argtypes = argtypes
         fn.restype = _RESTYPES.get(name, ctypes.c_int)
@@ -354,7 +357,7 @@ class AttentionWorkspace:
         # attn_hsplit deals a group's heads to up to q_per_kv workgroups when the groups are few)
         self.counters = torch.zeros(T * n_head * ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
         # lga_attention_decode_proj's hand-off words (a monotonic counter and its per-launch base; never re-zeroed)
-        self.sync = torch.zeros(128, dtype=torch.int32, device=device)
+        self.sync = torch.zeros(1024, dtype=torch.int32, device=device)
 
 
 def attention(q, k_cache, v_cache, input_pos, n_head, n_query_groups, head_size, scale, n_splits=1,

@@ -12,6 +12,7 @@ embedding row for the next step (so the step has no embedding launch) — so a d
 
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -59,7 +60,7 @@ class DecodeGraph:
 
     # greedy steps run ln_f + lm_head + argmax + the next embedding row as ONE launch (ops.q4_gemv_argmax_embed)
     # where the head is a 4-bit Linear it covers; False keeps lm_head GEMV + argmax_embed (bit-identical)
-    fuse_head = True
+    fuse_head = os.environ.get("LGA_FUSE_HEAD", "1") != "0"
 
     def _step_body(self, idx_out: Optional[torch.Tensor] = None, embedded: bool = True) -> None:
         fuse = self.fuse_embedding
