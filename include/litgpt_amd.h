@@ -149,6 +149,22 @@ int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, co
                                const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, void* y,
                                float* workspace, unsigned* counters, int n_head, int n_query_groups, int head_size,
                                int rope_n_elem, int max_seq, int n_splits, float scale, lga_stream_t stream);
+/* lga_qkv_attention_decode: the decode step's attention half in ONE launch — RMSNorm(norm_1) of x, the fused 4-bit
+ * qkv Linear (`self.attn(x)`, lit_gpt/model.py:619; rows [G][q, k, v][hs] bit-identical to lga_q4_gemv with the
+ * norm fused), RoPE of q and k, KVCache.forward's append at cache_pos[0] and the attention over keys 0..p
+ * (lga_attention_decode_fused's math; y within fp32 summation order of it). The K/V rows before p are issued at
+ * kernel start, beside the qkv weights. qkv_scratch: [n_query_groups * 3 * hs] bf16 (written, the rows handed between
+ * workgroups); workspace / counters as lga_attention_decode_fused; group_sync: 2 * n_query_groups * 64 zeroed
+ * uint32 (never re-zeroed). Geometry: lga_qkv_attention_supported (Llama-2-7B at TP = 1: C 4096, MHA, hs 128, 8
+ * splits); caller checks it. */
+int lga_qkv_attention_supported(int n_embd, int n_head, int n_query_groups, int head_size, int n_splits, int group,
+                                int fmt);
+int lga_qkv_attention_decode(const void* x, const void* norm_weight, float norm_eps, const uint8_t* qweight,
+                             const void* scales, const void* bias, int group, int fmt, void* qkv_scratch, void* k_cache,
+                             void* v_cache, const int64_t* cache_pos, const int64_t* rope_pos, const float* cos,
+                             const float* sin, int rope_rows, void* y, float* workspace, unsigned* counters,
+                             unsigned* group_sync, int n_head, int n_query_groups, int head_size, int max_seq,
+                             int n_splits, float scale, lga_stream_t stream);
 /* lga_attention_decode_proj: lga_attention_decode_fused followed, in the SAME launch, by the out-projection
  * `self.proj(y)` (lit_gpt/model.py:656; the 4-bit Linear bnb's gemv_4bit serves at reference generate/base.py:128-136)
  * and the Block residual add `x + h` (model.py:591): out (N) = bf16(proj(y) [+ bias]) + residual, bit-identical to

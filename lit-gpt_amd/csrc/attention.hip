@@ -116,8 +116,8 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
   };
   const int j_first = k_lo + rg;
 
-  // the q rows are loaded first and the first K/V batch right behind them (vmcnt retires in order: the RoPE below
-  // waits for q only, with the K/V loads in flight); an empty split's batch re-reads row 0 and is never consumed
+  // the q rows and the RoPE tables, then the first K/V batch (an empty split's batch re-reads row 0 and is never
+  // consumed)
   uint4 qraw[QPK];
 #pragma unroll
   for (int h = 0; h < QPK; ++h) {
@@ -134,15 +134,17 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
       sn[i] = sr[i];
     }
   }
-  uint4 ka[UNR], va[UNR], kb[UNR], vb[UNR];
-  if (PIPE) fetch(ka, va, j_first);
-  __builtin_amdgcn_sched_barrier(0);  // keep the K/V batch above the RoPE's wait for q
   float qf[QPK][8];
 #pragma unroll
   for (int h = 0; h < QPK; ++h) {
     if (FUSED) unpack8(rope8(qraw[h], cs, sn, sub), qf[h]);
     else unpack8(qraw[h], qf[h]);
   }
+  // the first K/V batch AFTER the RoPE: issued beside q (ahead of the RoPE's wait) every split's first loads leave
+  // in one burst at kernel start, measured 0.25-0.3 us slower per launch (tools/attn_ab.py, round 5)
+  __builtin_amdgcn_sched_barrier(0);
+  uint4 ka[UNR], va[UNR], kb[UNR], vb[UNR];
+  if (PIPE) fetch(ka, va, j_first);
   LGA_TRACE(2);
   // m starts at a finite floor, not -inf: every row group runs the split's step count, so one whose keys are all
   // past k_end sees only masked (-inf) scores, and exp(floor - floor) = 1 keeps its (l, o) = 0 instead of NaN; a

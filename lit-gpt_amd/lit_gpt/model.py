@@ -301,8 +301,9 @@ class CausalSelfAttention(nn.Module):
     # rope_kv_append + attention path (bit-identical; tests compare the two)
     fuse_decode = True
     # ... and the decode out-projection + residual inside that launch (lga_attention_decode_proj) where it covers the
-    # geometry; False keeps the separate proj GEMV launch (bit-identical; tests compare the two)
-    fuse_proj = os.environ.get("LGA_FUSE_PROJ", "1") != "0"
+    # geometry: bit-identical to the separate proj GEMV launch, but measured slower (16.5 vs 15.6 us per block,
+    # DESIGN.md §8b), so it is opt-in (LGA_FUSE_PROJ=1); tests compare the two
+    fuse_proj = os.environ.get("LGA_FUSE_PROJ", "0") == "1"
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
                 input_pos: Optional[torch.Tensor] = None, *, norm: Optional["RMSNorm"] = None,
@@ -313,6 +314,10 @@ class CausalSelfAttention(nn.Module):
         B, T, C = x.size()
         c = self.config
         H, G, hs = c.n_head, c.n_query_groups, c.head_size
+        if T == 1 and input_pos is not None and norm is not None and self.fuse_qkv:
+            y = self._qkv_attention_decode(x, cos, sin, input_pos, norm)
+            if y is not None:
+                return _lin(self.proj, y.view(1, T, H * hs), residual=residual, reduce=reduce).view(B, T, -1)
         qkv = _lin(self.attn, x, norm_weight=None if norm is None else norm.weight,
                    norm_eps=c.norm_eps if norm is None else norm.eps).view(T, -1)
         dev = x.device
@@ -359,6 +364,38 @@ class CausalSelfAttention(nn.Module):
             y = ops.attention(q, kc, vc, pos, H, G, hs, 1.0 / math.sqrt(hs), n_splits, workspace=ws)
         out = _lin(self.proj, y.view(1, T, H * hs), residual=residual, reduce=reduce)
         return out.view(B, T, -1)
+
+    # opt-in (LGA_FUSE_QKV=1): decode tokens of the geometry csrc/qkv_attention.hip covers (Llama-2-7B at TP = 1)
+    # run RMSNorm + qkv GEMV + RoPE + KV append + attention as ONE launch (ops.qkv_attention_decode); q, k, v are
+    # bit-identical, y within fp32 order. Off by default: measured 28 us per block against 19.3 us for the qkv GEMV
+    # launch + lga_attention_decode_fused (tools/qkv_attn_ab.py, round 5; csrc/qkv_attention.hip STATUS)
+    fuse_qkv = os.environ.get("LGA_FUSE_QKV", "0") == "1"
+
+    def _qkv_attention_decode(self, x, cos, sin, input_pos, norm) -> Optional[torch.Tensor]:
+        """The fused decode launch when it covers this step, else None (the caller runs the two launches)."""
+        c = self.config
+        H, G, hs = c.n_head, c.n_query_groups, c.head_size
+        kv = self.kv_cache
+        if (not isinstance(kv, KVCache) or self.attn._forward_hooks or not self.fuse_decode
+                or not ops.decode_fusable(hs, c.rope_n_elem) or x.dtype != torch.bfloat16 or not x.is_cuda
+                or kv.k.dtype != torch.bfloat16 or cos.size(0) == 1):
+            return None
+        S = kv.k.size(-2)
+        n_splits = ops.decode_splits(G, H // G, hs, S)
+        if not ops.qkv_attention_supported(c.n_embd, H, G, hs, n_splits, self.attn):
+            return None
+        dev = x.device
+        ws = getattr(self, "_attn_ws", None)
+        if ws is None or ws.key != (1, H, G, hs, n_splits) or ws.counters.device != dev:
+            ws = self._attn_ws = ops.AttentionWorkspace(1, H, G, hs, n_splits, dev)
+        scratch = getattr(self, "_qkv_scratch", None)
+        if scratch is None or scratch.device != dev:
+            scratch = self._qkv_scratch = torch.empty((H + 2 * G) * hs, dtype=torch.bfloat16, device=dev)
+        pos = input_pos.to(device=dev, dtype=torch.int64)
+        return ops.qkv_attention_decode(x, norm.weight, norm.eps, self.attn, kv.k, kv.v, pos, pos,
+                                        cos.to(device=dev, dtype=torch.float32).contiguous(),
+                                        sin.to(device=dev, dtype=torch.float32).contiguous(), H, G, hs,
+                                        1.0 / math.sqrt(hs), n_splits, ws, scratch)
 
     def scaled_dot_product_attention(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
                                      mask: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -62,6 +62,9 @@ SIGNATURES = {
     "lga_attention": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_attention_workspace_bytes": [_I, _I, _I, _I],
     "lga_attention_decode_fused": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
+    "lga_qkv_attention_supported": [_I, _I, _I, _I, _I, _I, _I],
+    "lga_qkv_attention_decode": [_P, _P, _F, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I,
+                                 _I, _I, _I, _I, _F, _P],
     "lga_attention_decode_proj_supported": [_I, _I, _I, _I, _I, _I, _I, _I],
     "lga_attention_decode_proj": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P,
                                   _P, _P, _P, _I, _I, _I, _P],
@@ -358,6 +361,8 @@ class AttentionWorkspace:
         self.counters = torch.zeros(T * n_head * ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
         # lga_attention_decode_proj's hand-off words (a monotonic counter and its per-launch base; never re-zeroed)
         self.sync = torch.zeros(1024, dtype=torch.int32, device=device)
+        # lga_qkv_attention_decode's per-group row counters and their bases (monotonic; never re-zeroed)
+        self.group_sync = torch.zeros(2 * n_query_groups * ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
 
 
 def attention(q, k_cache, v_cache, input_pos, n_head, n_query_groups, head_size, scale, n_splits=1,
@@ -407,6 +412,38 @@ def attention_decode_fused(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin,
         _dev(rope_pos, "rope_pos", torch.int64), _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32),
         cos.shape[0], _dev(y, "y", torch.bfloat16), ws, cnt, n_head, n_query_groups, head_size, rope_n_elem, max_seq,
         n_splits, float(scale), _stream()))
+    return y
+
+
+def qkv_attention_supported(n_embd, n_head, n_query_groups, head_size, n_splits, lin) -> bool:
+    """Whether lga_qkv_attention_decode covers this decode step (the qkv Linear a 4-bit QuantLinear of the geometry
+    csrc/qkv_attention.hip is built for: Llama-2-7B at TP = 1)."""
+    from lit_gpt.quantize import QuantLinear
+
+    return (isinstance(lin, QuantLinear) and lin.in_features == n_embd
+            and lin.out_features == (n_head + 2 * n_query_groups) * head_size
+            and bool(load_library().lga_qkv_attention_supported(n_embd, n_head, n_query_groups, head_size, n_splits,
+                                                                 lin.group, lin.fmt)))
+
+
+def qkv_attention_decode(x, norm_weight, eps, lin, k_cache, v_cache, cache_pos, rope_pos, cos, sin, n_head,
+                         n_query_groups, head_size, scale, n_splits, workspace: AttentionWorkspace, qkv_scratch,
+                         out=None):
+    """One decode token's attention half in ONE launch: RMSNorm(x) -> qkv Linear (rows bit-identical to
+    ``q4_gemv(x, ..., norm_weight)``) -> RoPE -> KV append at cache_pos[0] -> attention over keys 0..p. Returns y
+    (1, H*hs); qkv_scratch (G*3*hs bf16) receives the qkv row."""
+    if workspace is None or workspace.key != (1, n_head, n_query_groups, head_size, n_splits):
+        raise ValueError("qkv_attention_decode needs the layer's AttentionWorkspace")
+    y = out if out is not None else torch.empty(1, n_head * head_size, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_qkv_attention_decode(
+        _dev(x.reshape(-1), "x", torch.bfloat16), _dev(norm_weight, "norm_weight", torch.bfloat16), float(eps),
+        _dev(lin.qweight, "qweight", torch.uint8), _dev(lin.scales, "scales"), _opt(lin.bias, "bias", torch.bfloat16),
+        lin.group, lin.fmt, _dev(qkv_scratch, "qkv_scratch", torch.bfloat16), _dev(k_cache, "k_cache", torch.bfloat16),
+        _dev(v_cache, "v_cache", torch.bfloat16), _dev(cache_pos, "cache_pos", torch.int64),
+        _dev(rope_pos, "rope_pos", torch.int64), _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32),
+        cos.shape[0], _dev(y, "y", torch.bfloat16), _dev(workspace.partials, "workspace", torch.float32),
+        _dev(workspace.counters, "counters", torch.int32), _dev(workspace.group_sync, "group_sync", torch.int32),
+        n_head, n_query_groups, head_size, k_cache.shape[-2], n_splits, float(scale), _stream()))
     return y
 
 

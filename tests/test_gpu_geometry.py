@@ -151,6 +151,7 @@ def test_decode_out_projection_inside_attention_launch_bit_identical(name, mode)
     assert ops.decode_proj_supported(H, G, hs, ops.decode_splits(G, H // G, hs, T + N + 1), attn.proj)
     prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=3)).to(DEV)
     outs = {}
+    default = CausalSelfAttention.fuse_proj
     try:
         for fused in (False, True):
             CausalSelfAttention.fuse_proj = fused
@@ -165,24 +166,67 @@ def test_decode_out_projection_inside_attention_launch_bit_identical(name, mode)
                 tok = int(torch.argmax(lg))
             outs[fused] = torch.stack(seq)
     finally:
-        CausalSelfAttention.fuse_proj = True
+        CausalSelfAttention.fuse_proj = default
     assert torch.equal(outs[False], outs[True])
+
+
+@pytest.mark.parametrize("mode", ["bnb.int4", "bnb.nf4"])
+@torch.inference_mode()
+def test_decode_qkv_inside_attention_launch(mode):
+    """The opt-in fused decode launch (CausalSelfAttention.fuse_qkv, lga_qkv_attention_decode: RMSNorm + qkv GEMV +
+    RoPE + KV append + attention in one launch) against the default two launches, Llama-2-7B width: the same KV cache
+    rows (q, k, v are bit-identical) and logits within the fp32 summation order of the attention's online softmax."""
+    from generate.base import build_model
+    from lit_gpt import Config
+    from lit_gpt.model import CausalSelfAttention
+
+    from lit_gpt import ops
+
+    cfg = Config.from_name("Llama-2-7b-hf", n_layer=1)
+    T, N = 300, 5
+    model = build_model(cfg, quantize=mode, device=DEV, seed=4, max_seq_length=T + N + 1)
+    attn = model.transformer.h[0].attn
+    H, G, hs = cfg.n_head, cfg.n_query_groups, cfg.head_size
+    assert ops.qkv_attention_supported(cfg.n_embd, H, G, hs, ops.decode_splits(G, 1, hs, T + N + 1), attn.attn)
+    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=4)).to(DEV)
+    outs, caches = {}, {}
+    default = CausalSelfAttention.fuse_qkv
+    try:
+        for fused in (False, True):
+            CausalSelfAttention.fuse_qkv = fused
+            attn.kv_cache.reset_parameters()
+            lg = model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1]
+            tok, seq = int(torch.argmax(lg)), []
+            for i in range(N):
+                lg = model(torch.tensor([[tok]], device=DEV), torch.tensor([T + i], device=DEV),
+                           last_token_only=True)[0, -1]
+                seq.append(lg.float().clone())
+                tok = int(torch.argmax(lg))
+            outs[fused] = torch.stack(seq)
+            caches[fused] = (attn.kv_cache.k[..., : T + N, :].clone(), attn.kv_cache.v[..., : T + N, :].clone())
+    finally:
+        CausalSelfAttention.fuse_qkv = default
+    assert torch.equal(caches[False][0], caches[True][0]) and torch.equal(caches[False][1], caches[True][1])
+    tol = 2e-2 * outs[False].abs().max().item()  # bf16 y rounding of a one-block model's logits
+    assert (outs[False] - outs[True]).abs().max().item() <= tol
 
 
 @pytest.mark.timeout(900)
 @pytest.mark.parametrize("T", [8192, 32000])
 @torch.inference_mode()
-def test_mixtral_tp2_rank_geometry_long_prompt_prefill(T):
+def test_mixtral_long_prompt_prefill(T):
     """BASELINE config 5's long prompt (Mixtral block_size 32768, reference config.py:1294; generate/base.py:83-85
-    prefills the whole prompt in one forward): one full-width block at the TP=2 rank geometry (16 query heads, 4 KV
-    groups, experts of intermediate 7168), int4-g128, prefill of T tokens (MFMA GEMMs, grouped expert GEMMs over
-    2T routed rows, flash attention over T keys), then one decode step over the T-row cache. The last prefill row's
-    logits and the decode step's logits against the oracle (oracle.one_block_rows: the keys of every position, the
-    queries / MLP / head of those rows) in bf16 and float64 (tests/parity.py bounds)."""
+    prefills the whole prompt in one forward): one full-width Mixtral-8x7B block (32 heads, 8 KV groups, 8 experts
+    of 14336), int4-g128, prefill of T tokens (MFMA GEMMs, grouped expert GEMMs over 2T routed rows, flash attention
+    over T keys), then one decode step over the T-row cache. The last prefill row's logits and the decode step's
+    logits against the oracle (oracle.one_block_rows: the keys of every position, the queries / MLP / head of those
+    rows) in bf16 and float64 (tests/parity.py bounds). The TP=2 rank's attention shape (16 heads, 4 groups) at 32k
+    is test_prefill_flash_attention_32k_sampled_rows_vs_fp64: a rank's projections (K = 2048 of n_embd 4096) are not
+    a single-GPU Config."""
     from generate.base import build_model
     from lit_gpt import Config
 
-    cfg = Config.from_name("Mixtral-8x7B-v0.1", n_layer=1, n_head=16, n_query_groups=4, intermediate_size=7168)
+    cfg = Config.from_name("Mixtral-8x7B-v0.1", n_layer=1)
     model = build_model(cfg, quantize="int4-g128", device=DEV, seed=11, max_seq_length=T + 2)
     prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=11)).to(DEV)
     lg0 = model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1].float()
@@ -202,7 +246,7 @@ def test_mixtral_tp2_rank_geometry_long_prompt_prefill(T):
         del og
     worst = max(check_step(got[i], refs[torch.bfloat16][i], refs[torch.float64][i], f"T={T} row {i}")
                 for i in range(2))
-    print(f"\nMixtral TP=2 rank, T={T}: worst max|d logit| / max|logit| = {worst:.4%}")
+    print(f"\nMixtral one block, T={T}: worst max|d logit| / max|logit| = {worst:.4%}")
 
 
 @pytest.mark.timeout(600)

@@ -847,3 +847,56 @@ def test_fused_greedy_head_bit_identical(ops, mode, N, K, tie):
         if tie and it == 0:
             assert int(ib) == 7 or float(la[int(ib)]) > float(la[7])
     assert int(work.buf[-(9 * 256) // 8:].abs().sum()) == 0  # counters re-armed
+
+
+@pytest.mark.parametrize("mode,bias", [("int4-g128", False), ("nf4", False), ("int4-g128", True)])
+@pytest.mark.parametrize("S,positions", [(2304, [2047, 0, 1, 37, 2303, 2047, 2100]), (4096, [3000, 4095, 2463, 2464])])
+def test_qkv_attention_decode_matches_two_launches(ops, mode, bias, S, positions):
+    """RMSNorm + qkv GEMV + RoPE + KV append + attention in ONE launch (lga_qkv_attention_decode, Llama-2-7B
+    geometry) == lga_q4_gemv(norm) then lga_attention_decode_fused: the qkv row and both caches bit-identical, y
+    within fp32 summation order (tolerance as the fused-vs-two-launch attention test) and within bf16 rounding of an
+    fp64 softmax. Positions past 308 keys per split (S 4096) run the streamed remainder; a repeated position checks
+    the per-group hand-off counters across launches."""
+    from lit_gpt.quantize import QuantLinear
+
+    H = G = 32
+    hs, C = 128, 4096
+    N = (H + 2 * G) * hs
+    g = torch.Generator().manual_seed(S + len(mode))
+    w = torch.randn(N, C, generator=g) * 0.02
+    b = torch.randn(N, generator=g) * 0.5 if bias else None
+    lin = QuantLinear.from_float(w, b, mode, torch.device(DEV))
+    nw = (1.0 + torch.randn(C, generator=g) * 0.1).bfloat16().to(DEV)
+    k0 = (torch.randn(G, S, hs, generator=g)).bfloat16().to(DEV)
+    v0 = (torch.randn(G, S, hs, generator=g)).bfloat16().to(DEV)
+    cos, sin = om.build_rope_cache(S, hs, 10000)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    splits = ops.decode_splits(G, 1, hs, S)
+    assert ops.qkv_attention_supported(C, H, G, hs, splits, lin)
+    ws_a = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
+    ws_b = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
+    scratch = torch.empty(N, dtype=torch.bfloat16, device=DEV)
+    ka, va, kb, vb = k0.clone(), v0.clone(), k0.clone(), v0.clone()
+    scale = 1.0 / math.sqrt(hs)
+    for p in positions:
+        x = (torch.randn(1, C, generator=g) * 2).bfloat16().to(DEV)
+        pos = torch.tensor([p], device=DEV)
+        qkv = ops.q4_gemv(x.view(-1), lin.qweight, lin.scales, N, C, lin.group, lin.fmt, bias=lin.bias,
+                          norm_weight=nw, eps=1e-5)
+        ya = ops.attention_decode_fused(qkv.view(1, -1), ka, va, pos, pos, cos, sin, H, G, hs, hs, scale, splits,
+                                        workspace=ws_a).float()
+        yb = ops.qkv_attention_decode(x, nw, 1e-5, lin, kb, vb, pos, pos, cos, sin, H, G, hs, scale, splits, ws_b,
+                                      scratch).float()
+        assert torch.equal(qkv, scratch), p
+        assert torch.equal(ka, kb) and torch.equal(va, vb), p
+        assert torch.all((ya - yb).abs() <= ya.abs() * 2 ** -7 + 2e-3), (p, float((ya - yb).abs().max()))
+        # fp64 softmax from the (bit-exact) cache contents and the roped q
+        q = qkv.view(G, 3, hs)[:, 0].double().cpu()
+        c64, s64 = cos[p].double().cpu(), sin[p].double().cpu()
+        qr = torch.from_numpy(quant.bf16_bits_to_f32(quant.f32_to_bf16_bits(
+            (q * c64 + torch.cat((-q[:, hs // 2:], q[:, : hs // 2]), -1) * s64).float().numpy()))).double()
+        kd, vd = kb[:, : p + 1].double().cpu(), vb[:, : p + 1].double().cpu()
+        ref = torch.softmax(torch.einsum("gd,gkd->gk", qr, kd) * scale, -1)
+        ref = torch.einsum("gk,gkd->gd", ref, vd).reshape(-1)
+        assert torch.max((yb.double().cpu().view(-1) - ref).abs() - ref.abs() * 2 ** -7) <= 1e-4 + 2e-3, p
+    assert int(ws_b.counters.abs().sum()) == 0
