@@ -28,7 +28,14 @@ def build_rope_cache(seq_len: int, n_elem: int, base: int = 10000, condense_rati
     ``torch.arange(seq_len) / condense_ratio`` in (fp32 on CPU; bf16 under ``fabric.init_tensor()``
     with bf16-true — the "bf16 RoPE position quirk" of SURVEY §7)."""
     theta = 1.0 / (base ** (torch.arange(0, n_elem, 2, dtype=torch.float32) / n_elem))
-    seq_idx = torch.arange(seq_len, dtype=pos_dtype) / condense_ratio
+    # the reference's expression under that default dtype: an int64 range true-divided, i.e. each position rounded
+    # to nearest-even in pos_dtype (torch.arange(n, dtype=torch.bfloat16) itself rounds differently above 4096)
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(pos_dtype)
+    try:
+        seq_idx = torch.arange(seq_len) / condense_ratio
+    finally:
+        torch.set_default_dtype(prev)
     idx_theta = torch.outer(seq_idx, theta).repeat(1, 2)
     return torch.cos(idx_theta), torch.sin(idx_theta)
 
@@ -252,13 +259,16 @@ class OracleGPT:
         return self._lin("lm_head", x)
 
 
-def one_block_rows(og: OracleGPT, idx: torch.Tensor, rows: List[int]) -> torch.Tensor:
+def one_block_rows(og: OracleGPT, idx: torch.Tensor, rows: List[int],
+                   router_gaps: Optional[List[float]] = None) -> torch.Tensor:
     """Rows ``rows`` of GPT.forward's logits (model.py:499-519, no cache) for a ONE-block model over idx (T,),
     without the T x T work of a full forward: the qkv Linear and RoPE run over every position (the keys and values
     every query sees), the query, attention, projection, MLP and head only for the requested rows. Row t of the
     causal forward attends keys 0..t (SDPA is_causal, model.py:658-665) — exactly one query row over the prefix —
     and is also what a decode step at input_pos t computes from a cache filled by the prefix (model.py:509, 788-795).
-    Long-prompt prefill parity (32k tokens) at a cost linear in T."""
+    Long-prompt prefill parity (32k tokens) at a cost linear in T. ``router_gaps`` (a list, sparse-MoE configs):
+    receives per row the gap between the k-th and (k+1)-th router logit over max |router| — a row whose gap is at
+    the rounding noise can route to another expert in any other evaluation order (a parity test skips it)."""
     c = og.cfg
     if c.n_layer != 1 or c.parallel_residual:
         raise NotImplementedError("one_block_rows: one sequential-residual block")
@@ -279,7 +289,12 @@ def one_block_rows(og: OracleGPT, idx: torch.Tensor, rows: List[int]) -> torch.T
                                            scale=1.0 / math.sqrt(hs), enable_gqa=G != H)
         h = og._lin("transformer.h.0.attn.proj", y[0].transpose(0, 1).reshape(1, H * hs))
         xr = h + x[t:t + 1]
-        xr = og._mlp(0, og._norm("transformer.h.0.norm_2", xr)) + xr
+        n2 = og._norm("transformer.h.0.norm_2", xr)
+        if router_gaps is not None and c._mlp_class == "LLaMAMoE":
+            r = torch.sort(og._lin("transformer.h.0.mlp.gate", n2)[0].double(), descending=True)[0]
+            ne = c.n_expert_per_token
+            router_gaps.append(float((r[ne - 1] - r[ne]) / r.abs().max()))
+        xr = og._mlp(0, n2) + xr
         out.append(og._lin("lm_head", og._norm("transformer.ln_f", xr)))
     return torch.cat(out)
 

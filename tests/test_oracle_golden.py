@@ -257,5 +257,7 @@ def test_one_block_rows_equal_full_forward(name, kw):
     idx = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=4))
     full = og.forward(idx)
     rows = [0, 1, 33, T - 2, T - 1]
-    got = om.one_block_rows(og, idx, rows)
+    gaps = []
+    got = om.one_block_rows(og, idx, rows, router_gaps=gaps)
     assert torch.allclose(got, full[rows], rtol=1e-12, atol=1e-12)
+    assert len(gaps) == (len(rows) if cfg._mlp_class == "LLaMAMoE" else 0) and all(g >= 0 for g in gaps)
