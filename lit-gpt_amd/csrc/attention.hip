@@ -134,12 +134,19 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
       sn[i] = sr[i];
     }
   }
-  float qf[QPK][8];
+  // q stays packed bf16 (as the reference's bf16 q): scores are v_dot2_f32_bf16 chains — two exact bf16 products
+  // per instruction into an fp32 accumulator, half the VALU of unpack + fma (long contexts with q_per_kv > 1 are
+  // VALU-bound: tools/attn_sweep.py, round 5)
+  uint4 qp[QPK];
 #pragma unroll
-  for (int h = 0; h < QPK; ++h) {
-    if (FUSED) unpack8(rope8(qraw[h], cs, sn, sub), qf[h]);
-    else unpack8(qraw[h], qf[h]);
-  }
+  for (int h = 0; h < QPK; ++h) qp[h] = FUSED ? rope8(qraw[h], cs, sn, sub) : qraw[h];
+  auto dot8 = [](const uint4 a, const uint4 b) {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    float d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(s2, a.x), __builtin_bit_cast(s2, b.x), 0.0f, false);
+    d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(s2, a.y), __builtin_bit_cast(s2, b.y), d, false);
+    d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(s2, a.z), __builtin_bit_cast(s2, b.z), d, false);
+    return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(s2, a.w), __builtin_bit_cast(s2, b.w), d, false);
+  };
   // the first K/V batch AFTER the RoPE: issued beside q (ahead of the RoPE's wait) every split's first loads leave
   // in one burst at kernel start, measured 0.25-0.3 us slower per launch (tools/attn_ab.py, round 5)
   __builtin_amdgcn_sched_barrier(0);
@@ -166,12 +173,7 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
       float mx = m[h];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        float kf[8];
-        unpack8(kv[u], kf);
-        float d = 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) d = fmaf(qf[h][i], kf[i], d);
-        const float sd = row_group_sum<LPR>(d) * scale;  // whole row group active: DPP stays inside it
+        const float sd = row_group_sum<LPR>(dot8(qp[h], kv[u])) * scale;  // whole row group active: DPP inside it
         s[u] = (j0 + u * RG < k_end) ? sd : -INFINITY;
         mx = fmaxf(mx, s[u]);
       }
@@ -220,15 +222,11 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
       *(uint4*)(kc + ((size_t)g * max_seq + p) * HS + sub * 8) = kr;
       *(uint4*)(vc + ((size_t)g * max_seq + p) * HS + sub * 8) = vr;
     }
-    float kf[8], vf[8];
-    unpack8(kr, kf);
+    float vf[8];
     unpack8(vr, vf);
 #pragma unroll
     for (int h = 0; h < QPK; ++h) {
-      float d = 0.0f;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) d = fmaf(qf[h][i], kf[i], d);
-      const float s = row_group_sum<LPR>(d) * scale;
+      const float s = row_group_sum<LPR>(dot8(qp[h], kr)) * scale;
       const float mx = fmaxf(m[h], s);
       const float c = expf(m[h] - mx);
       const float e = expf(s - mx);

@@ -548,8 +548,11 @@ def decode_splits(n_query_groups: int, q_per_kv: int, head_size: int, max_seq: i
     """Sequence splits for T = 1 attention: one workgroup per CU across all query groups, at most 16 splits
     (tools/attn_sweep.py on MI355X, p = 2048..4000: 8 splits beat 16 for Llama-2-7B's 32 groups; with the few
     groups per rank of tensor parallelism 16 splits beat 32/64/128 — G = 4: 7.8 vs 10.9 us at 64 splits; G = 1,
-    8 heads per group: 21 vs 34 us at 64 — because the last-arriving split's combine grows with the split count)."""
-    s = max(1, min(n_cu // max(1, n_query_groups), 16))
+    8 heads per group: 21 vs 34 us at 64 — because the last-arriving split's combine grows with the split count).
+    Caches of >= 16k rows (a long prompt: generate/base.py sizes the cache to prompt + new tokens) take up to 32:
+    at p = 32066 Mixtral 35.0 vs 38.0 us, its TP = 2 rank 23.6 vs 26.4; at p = 16000 the two tie, at 8000 16 wins
+    (tools/attn_sweep.py, round 5, profiles/r05z_attn_long_context.txt)."""
+    s = max(1, min(n_cu // max(1, n_query_groups), 32 if max_seq >= 16384 else 16))
     return min(s, max(1, max_seq // 16), 256)
 
 

@@ -46,7 +46,7 @@ def sweep(H, G, hs, S, layers, mode="both"):
     sin = torch.randn(S, hs, device=dev)
     y = torch.empty(1, H * hs, device=dev, dtype=torch.bfloat16)
     scale = 1.0 / math.sqrt(hs)
-    for p in (128, 1024, 2048, 2303, 4000):
+    for p in [int(x) for x in os.environ.get("ATTN_POS", "128,1024,2048,2303,4000").split(",")]:
         pos = torch.tensor([p], device=dev)
         nbytes = 2 * G * (p + 1) * hs * 2
         for splits in [int(x) for x in os.environ.get("ATTN_SPLITS", "4,8,12,16,24,32,48,64").split(",")]:
