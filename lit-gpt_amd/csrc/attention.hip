@@ -135,8 +135,8 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
     }
   }
   // q stays packed bf16 (as the reference's bf16 q): scores are v_dot2_f32_bf16 chains — two exact bf16 products
-  // per instruction into an fp32 accumulator, half the VALU of unpack + fma (long contexts with q_per_kv > 1 are
-  // VALU-bound: tools/attn_sweep.py, round 5)
+  // per instruction into an fp32 accumulator, half the VALU of unpack + fma. Interleaved A/B (tools/attn_ab.py,
+  // round 5) at p = 32066, 32 splits: Mixtral 34.8 -> 33.8 us, its TP = 2 rank 24.8 -> 23.5; Llama-2-7B neutral
   uint4 qp[QPK];
 #pragma unroll
   for (int h = 0; h < QPK; ++h) qp[h] = FUSED ? rope8(qraw[h], cs, sn, sub) : qraw[h];

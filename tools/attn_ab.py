@@ -1,6 +1,7 @@
 """A/B of decode-attention builds in ONE process on one box (box-to-box spread is ~4 %, larger than the effects).
 
 usage: AB_LIBS=lit-gpt_amd/lit_gpt/_lib/liblitgpt_amd.so,tools/_lab5/attn_old.so python tools/attn_ab.py
+       (AB_HEADS=32 AB_GROUPS=AB_HEADS AB_CACHE=2304 AB_LAYERS=32 AB_SPLITS=product AB_POS=2063,2302 AB_PROJ=1)
 Per library: 32 fused decode-attention launches (Llama-2-7B geometry, one KV cache per block, 8 splits) captured in
 one HIP graph, replayed back to back — bench.py's time_attention — at several positions; rounds alternate the
 libraries so drift hits both. Prints us per launch (median over rounds).
@@ -22,8 +23,10 @@ from lit_gpt import ops  # noqa: E402
 
 def main():
     libs = os.environ["AB_LIBS"].split(",")
-    H = G = int(os.environ.get("AB_HEADS", "32"))
-    hs, S, layers = 128, 2304, 32
+    H = int(os.environ.get("AB_HEADS", "32"))
+    G = int(os.environ.get("AB_GROUPS", str(H)))
+    hs, S = 128, int(os.environ.get("AB_CACHE", "2304"))
+    layers = int(os.environ.get("AB_LAYERS", "32"))
     positions = [int(v) for v in os.environ.get("AB_POS", "2063,2302").split(",")]
     rounds = int(os.environ.get("AB_ROUNDS", "5"))
     dev = torch.device("cuda")
@@ -32,17 +35,20 @@ def main():
               for _ in range(layers)]
     qkv = torch.randn(1, (H + 2 * G) * hs, device=dev).bfloat16()
     cos, sin = torch.randn(S, hs, device=dev), torch.randn(S, hs, device=dev)
-    splits = ops.decode_splits(G, H // G, hs, S)
+    split_list = [int(v) for v in os.environ.get("AB_SPLITS", "0").split(",")]
+    split_list = [v or ops.decode_splits(G, H // G, hs, S) for v in split_list]
+    splits = split_list[0]
+    variants = [(i, sp) for i in range(len(libs)) for sp in split_list]  # (library, split count)
     out = torch.empty(1, H * hs, device=dev, dtype=torch.bfloat16)
     res = {}
     for p in positions:
         pos = torch.tensor([p], device=dev)
         graphs = []
-        for lib in loaded:
-            ops._lib = lib
-            ws = ops.AttentionWorkspace(1, H, G, hs, splits, dev)
+        for li, sp in variants:
+            ops._lib = loaded[li]
+            ws = ops.AttentionWorkspace(1, H, G, hs, sp, dev)
 
-            def launch_all(ws=ws):
+            def launch_all(ws=ws, splits=sp):
                 for kc, vc in caches:
                     ops.attention_decode_fused(qkv, kc, vc, pos, pos, cos, sin, H, G, hs, hs, 1.0 / math.sqrt(hs),
                                                splits, workspace=ws, out=out)
@@ -68,11 +74,11 @@ def main():
         proj_ab(loaded[0], caches, qkv, cos, sin, H, G, hs, S, splits, positions, rounds, dev)
     for p in positions:
         nbytes = 2 * G * hs * 2 * (p + 1) + (H + 2 * G) * hs * 2 + H * hs * 2
-        for i, lib in enumerate(libs):
+        for i, (li, sp) in enumerate(variants):
             v = res[(p, i)]
             med = float(np.median(v))
-            print(f"p={p} {Path(lib).name:28s} {med:7.2f} us  (min {min(v):.2f} max {max(v):.2f})  "
-                  f"{nbytes / med / 1e6:7.1f} GB/s = {nbytes / med / 1e6 / 8000:.3f} of 8 TB/s", flush=True)
+            print(f"p={p} {Path(libs[li]).name:28s} splits {sp:3d} {med:7.2f} us  (min {min(v):.2f} max {max(v):.2f})  "
+                  f"{nbytes / med / 1e3:7.1f} GB/s = {nbytes / med / 1e3 / 8000:.3f} of 8 TB/s", flush=True)
 
 
 def proj_ab(lib, caches, qkv, cos, sin, H, G, hs, S, splits, positions, rounds, dev):
