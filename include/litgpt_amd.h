@@ -193,6 +193,19 @@ int lga_moe_route(const void* logits, int T, int n_expert, int k, int32_t* exper
 int lga_moe_gate_route(const void* x, const uint8_t* qweight, const void* scales, const void* norm_weight,
                        float norm_eps, int n_expert, int K, int group, int fmt, int k, int32_t* expert_ids, void* probs,
                        lga_stream_t stream);
+/* lga_q4_gemv_gate_route: one token of a sparse-MoE block without tensor parallelism — the attention
+ * out-projection + Block residual (`x = self.attn(...) + x`, model.py:591, 656; lga_q4_gemv with a residual) into
+ * y [N], AND the router gate of the MLP that follows on y (RMSNorm norm_2 fused, model.py:592, 736) with its top-k
+ * routing (model.py:737-738) into expert_ids [k] int32 / probs [k] bf16, in one launch: y bit-identical to
+ * lga_q4_gemv, the routing bit-identical to lga_moe_gate_route on y. `counter`: one caller-zeroed word, re-armed by
+ * the kernel. Coverage: lga_q4_gemv_gate_route_supported (N, K multiples of 32 up to 6144, gate format = the
+ * projection's). */
+int lga_q4_gemv_gate_route_supported(int N, int K, int group, int fmt, int n_expert, int k, int gate_group,
+                                     int gate_fmt);
+int lga_q4_gemv_gate_route(const void* x, const uint8_t* qweight, const void* scales, const void* residual, void* y,
+                           int N, int K, int group, int fmt, const uint8_t* gate_qweight, const void* gate_scales,
+                           int gate_group, int gate_fmt, const void* norm_weight, float norm_eps, int n_expert, int k,
+                           int32_t* expert_ids, void* probs, unsigned* counter, lga_stream_t stream);
 /* lga_q4_gemv_experts_combine: one token, k = 2 — the routed proj GEMVs of both slots (x [2][K], expert_ids [2],
  * weights stacked as lga_q4_gemv_experts) and lga_moe_combine with the residual in one launch:
  * y [N] = residual + sum in ascending expert id of bf16(probs[s] * expert_out[s]), bit-identical to

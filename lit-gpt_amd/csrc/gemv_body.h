@@ -76,7 +76,7 @@ template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, int NW = 4,
           bool MOE2 = false, bool XWAIT = false>
 __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char* smem) {
   static_assert(!MOE2 || (!DUAL && RES && !NORM && !LDS_OUT), "MOE2 runs as RES, without dual / norm / LDS output");
-  static_assert(!XWAIT || (!MOE2 && !NORM && !DUAL), "XWAIT: a plain (residual) projection");
+  static_assert(!XWAIT || (!MOE2 && !DUAL), "XWAIT: a plain projection (optionally RMS-normalised)");
   if (a.eidx) {  // wave-uniform: one scalar load of the routed expert id, then plain pointer offsets
     const long long e = min(max(a.eidx[blockIdx.y], 0), a.n_expert - 1);
     a.qw += e * a.ew;
@@ -112,14 +112,14 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
   // 1. activation (and norm weight) share of this thread: uint4 t, t+NT, ... (clamped, branch-free)
   uint4 xr[XI], nr[XI], xr2[MOE2 ? XI : 1];
 #pragma unroll
-  for (int i = 0; i < (XWAIT ? 0 : XI); ++i) {
+  for (int i = 0; i < (XWAIT && !NORM ? 0 : XI); ++i) {  // XWAIT: x itself comes after the weights (below)
     const int u = min(t + NT * i, n8 - 1);
     if (MOE2) xr2[MOE2 ? i : 0] = ((const uint4*)(a.x + a.xs))[u];
 #ifdef LGA_LAB_NOX  // lab builds only: cost of the activation fetch
     xr[i] = make_uint4(0x3F803F80u + u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
     if (NORM) nr[i] = xr[i];
 #else
-    xr[i] = ((const uint4*)a.x)[u];
+    if (!XWAIT) xr[i] = ((const uint4*)a.x)[u];
     if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
 #endif
   }

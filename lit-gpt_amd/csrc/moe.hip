@@ -136,6 +136,53 @@ __global__ void __launch_bounds__(NW * 64, NW == 8 ? 4 : 1) moe_down_combine_ker
   gemv_q4_body<RPR, CPT, FMT, false, false, true, NW, false, true>(a, blockIdx.x, smem);
 }
 
+// Decode (one token, sparse-MoE block, no tensor parallelism): the attention out-projection + Block residual (the
+// lga_q4_gemv kernel the shape dispatches to: 4 waves x 4 rows, CPT chunks per lane) AND, in the workgroup that
+// arrives last, the router gate GEMV + top-k routing of the MLP that follows on the projection's output
+// (moe_gate_route_kernel's body and route_row, bit for bit) — one launch instead of two; the gate launch was pure
+// ramp (6.4 us for 16 KB of weights). Hand-off (MI355X_MICROARCH.md "Valid forms" row 1): every
+// workgroup stages its 16 bf16 rows in LDS, one wave stores them as two 16-B write-through (sc1) pieces and drains,
+// a workgroup barrier, one agent-scope add on the launch counter; the last arriver re-reads the whole row with sc1
+// loads (the XWAIT form of the body, its poll already satisfied) and re-arms the counter.
+template <int RPR, int CPT, int FMT, int GCPT>
+__global__ void __launch_bounds__(256) gemv_gate_route_kernel(GemvArgs a, GemvArgs gate, int k,
+                                                              int32_t* __restrict__ ids, uint16_t* __restrict__ probs,
+                                                              unsigned* __restrict__ counter) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ KV sq[8];
+  __shared__ unsigned s_ticket;
+  gemv_q4_body<RPR, CPT, FMT, false, false, true, 4, true>(a, blockIdx.x, smem);
+  __syncthreads();
+  if (threadIdx.x < 2) {  // the workgroup's 16 rows (N % 16 == 0: all real) as two 16-B sc1 stores
+    const __amdgpu_buffer_rsrc_t yrs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, a.N * 2, 0x00020000);
+    const uint4 v = ((const uint4*)gemv_out_lds(smem, a.K))[threadIdx.x];
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), yrs,
+                                           (blockIdx.x * 16 + threadIdx.x * 8) * 2, 0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_ticket != gridDim.x - 1) return;
+  gate.x = a.y;
+  gate.xwait = counter;
+  gate.xwait_target = gridDim.x;  // every workgroup has arrived: the body's poll passes at once
+  gemv_q4_body<4, GCPT, FMT, false, true, false, 4, true, false, true>(gate, 0, smem);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    route_row(gemv_out_lds(smem, gate.K), gate.N, k, ids, probs, sq);
+    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next launch
+  }
+}
+
+template <int CPT, int GCPT, int FMT>
+static void launch_gemv_gate_route(const GemvArgs& a, const GemvArgs& gate, int k, int32_t* ids, uint16_t* probs,
+                                   unsigned* counter, hipStream_t stream) {
+  const size_t lds = gemv_lds_bytes(a.K) > gemv_lds_bytes(gate.K) ? gemv_lds_bytes(a.K) : gemv_lds_bytes(gate.K);
+  gemv_gate_route_kernel<4, CPT, FMT, GCPT><<<a.N / 16, 256, lds, stream>>>(a, gate, k, ids, probs, counter);
+}
+
 template <int RPR, int CPT, int FMT>
 static void launch_down_combine(const GemvArgs& a, const int32_t* ids, hipStream_t stream) {
   // 16 waves, 8 per expert: 8 * RPR rows per workgroup, one workgroup per CU (both inputs staged in LDS)
@@ -241,6 +288,52 @@ extern "C" int lga_moe_route(const void* logits, int T, int n_expert, int k, int
                 "lga_moe_route: needs 1 <= k <= n_expert <= 8");
   lga::moe_route_kernel<<<(T + 63) / 64, 64, 0, stream>>>((const uint16_t*)logits, T, n_expert, k, expert_ids,
                                                           (uint16_t*)probs);
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_q4_gemv_gate_route_supported(int N, int K, int group, int fmt, int n_expert, int k, int gate_group,
+                                                int gate_fmt) {
+  // the gate's input is the projection's output: its K is N
+  return N > 0 && N % 32 == 0 && N <= 6144 && K > 0 && K % 32 == 0 && K <= 6144 && group >= 32 && group % 32 == 0 &&
+         K % group == 0 && gate_group >= 32 && gate_group % 32 == 0 && N % gate_group == 0 &&
+         (fmt == 0 || fmt == 1 || fmt == 3) && lga::kernel_fmt(gate_fmt) == lga::kernel_fmt(fmt) &&
+         (gate_fmt == 0 || gate_fmt == 1 || gate_fmt == 3) && n_expert >= 1 && n_expert <= 8 && k >= 1 &&
+         k <= n_expert && (long long)N / 16 <= 65535;
+}
+
+extern "C" int lga_q4_gemv_gate_route(const void* x, const uint8_t* qweight, const void* scales, const void* residual,
+                                      void* y, int N, int K, int group, int fmt, const uint8_t* gate_qweight,
+                                      const void* gate_scales, int gate_group, int gate_fmt, const void* norm_weight,
+                                      float norm_eps, int n_expert, int k, int32_t* expert_ids, void* probs,
+                                      unsigned* counter, hipStream_t stream) {
+  LGA_CHECK_ARG(x && qweight && scales && residual && y && gate_qweight && gate_scales && norm_weight && expert_ids &&
+                    probs && counter,
+                "lga_q4_gemv_gate_route: null pointer");
+  LGA_CHECK_ARG(lga_q4_gemv_gate_route_supported(N, K, group, fmt, n_expert, k, gate_group, gate_fmt),
+                "lga_q4_gemv_gate_route: geometry not covered (lga_q4_gemv_gate_route_supported)");
+  lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, nullptr, (const uint16_t*)residual, nullptr,
+                  (uint16_t*)y, N, K, group, 0.0f};
+  a.cb = lga::codebook_of(fmt);
+  lga::GemvArgs g{(const uint16_t*)y, gate_qweight, gate_scales, nullptr, nullptr, nullptr, nullptr,
+                  (const uint16_t*)norm_weight, nullptr, n_expert, N, gate_group, norm_eps};
+  g.cb = lga::codebook_of(gate_fmt);
+  const int cpt = (K / 32 + 63) / 64, gcpt = (N / 32 + 63) / 64, kf = lga::kernel_fmt(fmt);
+#define LGA_GG(CPT, GCPT)                                                                                             \
+  do {                                                                                                                \
+    if (kf == 0) lga::launch_gemv_gate_route<CPT, GCPT, 0>(a, g, k, expert_ids, (uint16_t*)probs, counter, stream);  \
+    else lga::launch_gemv_gate_route<CPT, GCPT, 1>(a, g, k, expert_ids, (uint16_t*)probs, counter, stream);          \
+  } while (0)
+#define LGA_GG_K(CPT)            \
+  do {                           \
+    if (gcpt == 1) LGA_GG(CPT, 1); \
+    else if (gcpt == 2) LGA_GG(CPT, 2); \
+    else LGA_GG(CPT, 3);         \
+  } while (0)
+  if (cpt == 1) LGA_GG_K(1);
+  else if (cpt == 2) LGA_GG_K(2);
+  else LGA_GG_K(3);
+#undef LGA_GG_K
+#undef LGA_GG
   LGA_LAUNCH_RETURN();
 }
 

@@ -257,13 +257,22 @@ class Block(nn.Module):
         from lit_gpt import comm
 
         ha = comm.tp_hook(self.attn)
+        hm = comm.tp_hook(self.mlp)
+        # a decode token of a sparse-MoE block: the router gate + routing ride the attention's out-projection launch
+        # (ops.q4_gemv_gate_route) when it covers the pair; the MLP then starts from the routing it left
+        route = None
+        if (ha is None and hm is None and x.size(1) == 1 and input_pos is not None and isinstance(self.mlp, LLaMAMoE)
+                and not self.attn._forward_hooks and not self.mlp._forward_hooks):
+            route = self.mlp.gate_route_request(self.norm_2, x.size(-1))
         if ha is not None:
             x = self.attn.forward(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x, reduce=ha)
         elif not self.attn._forward_hooks:
-            x = self.attn(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x)
+            x = self.attn(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x, route=route)
         else:
             x = ops.add(self.attn(self.norm_1(x), cos, sin, mask, input_pos).contiguous(), x.contiguous())
-        hm = comm.tp_hook(self.mlp)
+        if route is not None and route.done:
+            route.done = False
+            return self.mlp(x, norm=self.norm_2, residual=x, routed=route)
         if hm is not None and isinstance(self.mlp, LLaMAMLP):
             return self.mlp.forward(x, norm=self.norm_2, residual=x, reduce=hm)
         if hm is not None:
@@ -307,9 +316,10 @@ class CausalSelfAttention(nn.Module):
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
                 input_pos: Optional[torch.Tensor] = None, *, norm: Optional["RMSNorm"] = None,
-                residual: Optional[torch.Tensor] = None, reduce=None) -> torch.Tensor:
-        """``norm`` / ``residual`` / ``reduce`` are fusion hooks used by Block.forward: the RMSNorm runs in the qkv
-        GEMV prologue, the residual add (and under TP the all-reduce hook ``reduce``) in the proj epilogue. Without
+                residual: Optional[torch.Tensor] = None, reduce=None, route=None) -> torch.Tensor:
+        """``norm`` / ``residual`` / ``reduce`` / ``route`` are fusion hooks used by Block.forward: the RMSNorm runs in
+        the qkv GEMV prologue, the residual add (and under TP the all-reduce hook ``reduce``) in the proj epilogue, and
+        a following sparse-MoE's gate + routing (``route``, LLaMAMoE.gate_route_request) in the proj launch. Without
         them this is the reference forward."""
         B, T, C = x.size()
         c = self.config
@@ -317,7 +327,7 @@ class CausalSelfAttention(nn.Module):
         if T == 1 and input_pos is not None and norm is not None and self.fuse_qkv:
             y = self._qkv_attention_decode(x, cos, sin, input_pos, norm)
             if y is not None:
-                return _lin(self.proj, y.view(1, T, H * hs), residual=residual, reduce=reduce).view(B, T, -1)
+                return self._proj_out(y.view(1, T, H * hs), residual, reduce, route).view(B, T, -1)
         qkv = _lin(self.attn, x, norm_weight=None if norm is None else norm.weight,
                    norm_eps=c.norm_eps if norm is None else norm.eps).view(T, -1)
         dev = x.device
@@ -362,8 +372,21 @@ class CausalSelfAttention(nn.Module):
         else:
             q = ops.rope_kv_append(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem)
             y = ops.attention(q, kc, vc, pos, H, G, hs, 1.0 / math.sqrt(hs), n_splits, workspace=ws)
-        out = _lin(self.proj, y.view(1, T, H * hs), residual=residual, reduce=reduce)
+        out = self._proj_out(y.view(1, T, H * hs), residual, reduce, route)
         return out.view(B, T, -1)
+
+    def _proj_out(self, y: torch.Tensor, residual, reduce, route) -> torch.Tensor:
+        """The out-projection (+ residual / TP reduce); with ``route`` (one token, no reduce) the next MoE's gate and
+        routing in the same launch (ops.q4_gemv_gate_route: y and the routing bit-identical to the two launches)."""
+        if route is not None and route.proj_ok is None:
+            route.proj_ok = ops.gemv_gate_route_supported(self.proj, route.gate, route.k)
+        if (route is not None and route.proj_ok and reduce is None and residual is not None
+                and not self.proj._forward_hooks):
+            out = ops.q4_gemv_gate_route(y.reshape(-1).contiguous(), self.proj, residual.reshape(-1).contiguous(),
+                                         route.gate, route.norm.weight, route.norm.eps, route.k, route.ws)
+            route.done = True
+            return out.view(1, 1, -1)
+        return _lin(self.proj, y, residual=residual, reduce=reduce)
 
     # opt-in (LGA_FUSE_QKV=1): decode tokens of the geometry csrc/qkv_attention.hip covers (Llama-2-7B at TP = 1)
     # run RMSNorm + qkv GEMV + RoPE + KV append + attention as ONE launch (ops.qkv_attention_decode); q, k, v are
@@ -498,6 +521,16 @@ moe_gate_route = True
 moe_fused_combine = os.environ.get("LGA_MOE_FUSED_COMBINE", "0") == "1"
 
 
+class _RouteRequest:
+    """LLaMAMoE.gate_route_request's hook object: the gate, the norm it fuses, k, the routing outputs; ``done`` is
+    set by the attention when its out-projection launch produced the routing for this token."""
+
+    def __init__(self, gate, norm, k, ws) -> None:
+        self.gate, self.norm, self.k, self.ws = gate, norm, k, ws
+        self.done = False
+        self.proj_ok = None
+
+
 class LLaMAMoE(nn.Module):
     """Sparse MoE (lit_gpt/model.py:719-743): router gate, top-k experts per token, prob-weighted bf16 sum.
 
@@ -561,6 +594,24 @@ class LLaMAMoE(nn.Module):
         return (moe_gate_route and isinstance(g, QuantLinear) and g.bias is None and not g._forward_hooks
                 and g.in_features == C and ops.moe_gate_route_fits(g.out_features, C))
 
+    # opt-in (LGA_FOLD_GATE=1): the router gate + routing of a decode token inside the preceding out-projection
+    # launch (Block.forward, ops.q4_gemv_gate_route; bit-identical, tests compare). Off by default: Mixtral decode
+    # 2.284-2.291 vs 2.216-2.218 ms per step on one box (round 5) — the last-arriving workgroup's serial gate GEMV
+    # (cold gate weights, sc1 re-read of the row) + routing cost more than the gate launch's ramp saved
+    fold_gate = os.environ.get("LGA_FOLD_GATE", "0") == "1"
+
+    def gate_route_request(self, norm, C: int):
+        """A ``route`` hook for CausalSelfAttention.forward when the gate + routing can ride the out-projection
+        launch (the gate would otherwise run as lga_moe_gate_route with norm_2 fused), else None."""
+        if not (self.fold_gate and isinstance(norm, RMSNorm) and ops.gemv_fuses_norm(C, dual=True)
+                and self._gate_route_ok(C)):
+            return None
+        k = self.config.n_expert_per_token
+        req = getattr(self, "_route_req", None)
+        if req is None or req.norm is not norm or req.ws.ids.device != self.gate.qweight.device:
+            req = self._route_req = _RouteRequest(self.gate, norm, k, ops.GateRouteWorkspace(k, self.gate.qweight.device))
+        return req if req.proj_ok is not False else None
+
     def _expert_hooks(self, x: torch.Tensor, eout: torch.Tensor) -> torch.Tensor:
         hooks = [list(e._forward_hooks.values()) for e in self.experts]
         if any(len(h) != len(hooks[0]) for h in hooks):
@@ -571,7 +622,9 @@ class LLaMAMoE(nn.Module):
         return eout
 
     def forward(self, x: torch.Tensor, *, norm: Optional["RMSNorm"] = None,
-                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+                residual: Optional[torch.Tensor] = None, routed=None) -> torch.Tensor:
+        """``routed``: the routing of this decode token already computed by the out-projection launch
+        (gate_route_request)."""
         c = self.config
         lead, C = x.shape[:-1], x.shape[-1]
         x2 = x.reshape(-1, C).contiguous()
@@ -584,7 +637,9 @@ class LLaMAMoE(nn.Module):
             xin = x2 if (norm is None or fuse_norm) else norm(x2)
             nw = norm.weight if fuse_norm else None
             eps = norm.eps if fuse_norm else 1e-5
-            if self._gate_route_ok(C):  # gate GEMV + routing in one launch (same bits as the pair below)
+            if routed is not None:  # computed inside the attention's out-projection launch (same bits)
+                ids, probs = routed.ws.ids, routed.ws.probs
+            elif self._gate_route_ok(C):  # gate GEMV + routing in one launch (same bits as the pair below)
                 g = self.gate
                 ids, probs = ops.moe_gate_route(xin.view(-1), g.qweight, g.scales, E, C, g.group, g.fmt, k,
                                                 norm_weight=nw, eps=eps)

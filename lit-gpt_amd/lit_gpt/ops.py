@@ -74,6 +74,8 @@ SIGNATURES = {
     "lga_argmax_embed": [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P],
     "lga_moe_route": [_P, _I, _I, _I, _P, _P, _P],
     "lga_moe_gate_route": [_P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P],
+    "lga_q4_gemv_gate_route_supported": [_I, _I, _I, _I, _I, _I, _I, _I],
+    "lga_q4_gemv_gate_route": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _F, _I, _I, _P, _P, _P, _P],
     "lga_q4_gemv_experts_combine": [_P, _P, _P, _P, _P, _P, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _I, _I, _I,
                                     _I, _P],
     "lga_q4_gemv_experts": [_P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _I, _P, _I, _I, _I, _I,
@@ -717,6 +719,44 @@ def moe_gate_route(x, qweight, scales, n_expert, K, group, fmt, k, *, norm_weigh
                                              float(eps), n_expert, K, group, fmt, k, _dev(ids, "ids", torch.int32),
                                              _dev(probs, "probs", torch.bfloat16), _stream()))
     return ids, probs
+
+
+def gemv_gate_route_supported(proj, gate, k: int) -> bool:
+    """Whether lga_q4_gemv_gate_route covers this (out-projection, router gate) pair: both bias-free 4-bit
+    QuantLinears of one kernel format, the projection's N a multiple of 16, K <= 6144, n_expert <= 8."""
+    from lit_gpt.quantize import QuantLinear
+
+    if not (isinstance(proj, QuantLinear) and isinstance(gate, QuantLinear) and proj.bias is None
+            and gate.bias is None and gate.in_features == proj.out_features):
+        return False
+    return bool(load_library().lga_q4_gemv_gate_route_supported(proj.out_features, proj.in_features, proj.group,
+                                                                 proj.fmt, gate.out_features, k, gate.group,
+                                                                 gate.fmt))
+
+
+class GateRouteWorkspace:
+    """Persistent outputs of lga_q4_gemv_gate_route for one MoE block (allocate before graph capture): the routing
+    (ids (1, k) int32, probs (1, k) bf16) and the launch's arrival counter (zeroed once, re-armed by the kernel)."""
+
+    def __init__(self, k: int, device) -> None:
+        self.ids = torch.zeros(1, k, dtype=torch.int32, device=device)
+        self.probs = torch.zeros(1, k, dtype=torch.bfloat16, device=device)
+        self.counter = torch.zeros(ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
+
+
+def q4_gemv_gate_route(x, proj, residual, gate, norm_weight, eps, k, ws: GateRouteWorkspace, out=None):
+    """y = proj(x) + residual (bf16, as q4_gemv) and, on y, (ids, probs) = the routing of gate(rmsnorm(y)) (as
+    moe_gate_route) in ONE launch; the routing lands in ws.ids / ws.probs. Returns y."""
+    N, K = proj.out_features, proj.in_features
+    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_q4_gemv_gate_route(
+        _dev(x, "x", torch.bfloat16), _dev(proj.qweight, "qweight", torch.uint8), _dev(proj.scales, "scales"),
+        _dev(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16), N, K, proj.group, proj.fmt,
+        _dev(gate.qweight, "gate_qweight", torch.uint8), _dev(gate.scales, "gate_scales"), gate.group, gate.fmt,
+        _dev(norm_weight, "norm_weight", torch.bfloat16), float(eps), gate.out_features, k,
+        _dev(ws.ids, "ids", torch.int32), _dev(ws.probs, "probs", torch.bfloat16),
+        _dev(ws.counter, "counter", torch.int32), _stream()))
+    return y
 
 
 def _expert_strides(qweight, scales):

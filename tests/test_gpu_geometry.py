@@ -170,6 +170,45 @@ def test_decode_out_projection_inside_attention_launch_bit_identical(name, mode)
     assert torch.equal(outs[False], outs[True])
 
 
+@pytest.mark.parametrize("mode", ["int4-g128", "nf4"])
+@torch.inference_mode()
+def test_mixtral_gate_route_inside_out_projection_bit_identical(mode):
+    """Full-width Mixtral-8x7B block: the decode step's router gate + routing inside the attention's out-projection
+    launch (LLaMAMoE.fold_gate, ops.q4_gemv_gate_route) gives bit-identical logits to the separate
+    lga_moe_gate_route launch, eager and through the HIP-graph generate path."""
+    from generate.base import build_model, generate
+    from lit_gpt import Config
+    from lit_gpt.model import LLaMAMoE
+
+    cfg = Config.from_name("Mixtral-8x7B-v0.1", n_layer=2)
+    T, N = 300, 6
+    model = build_model(cfg, quantize=mode, device=DEV, seed=5, max_seq_length=T + N + 1)
+    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=5)).to(DEV)
+    outs, toks = {}, {}
+    default = LLaMAMoE.fold_gate
+    try:
+        for fold in (False, True):
+            LLaMAMoE.fold_gate = fold
+            for b in model.transformer.h:
+                b.attn.kv_cache.reset_parameters()
+            lg = model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1]
+            tok, seq = int(torch.argmax(lg)), []
+            for i in range(N):
+                lg = model(torch.tensor([[tok]], device=DEV), torch.tensor([T + i], device=DEV),
+                           last_token_only=True)[0, -1]
+                seq.append(lg.clone())
+                tok = int(torch.argmax(lg))
+            outs[fold] = torch.stack(seq)
+            for b in model.transformer.h:
+                b.attn.kv_cache.reset_parameters()
+            toks[fold] = generate(model, prompt, T + N, temperature=0.0)[T:].tolist()
+        assert model.transformer.h[0].mlp._route_req.proj_ok  # the fold ran
+    finally:
+        LLaMAMoE.fold_gate = default
+    assert torch.equal(outs[False], outs[True])
+    assert toks[False] == toks[True]
+
+
 @pytest.mark.parametrize("mode", ["int4-g128", "bnb.nf4"])
 @torch.inference_mode()
 def test_decode_qkv_inside_attention_launch(mode):

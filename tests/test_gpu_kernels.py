@@ -647,6 +647,56 @@ def test_experts_combine_matches_gemv_then_combine(ops, fmt, group, N, K):
         assert torch.equal(got.view(torch.int16), want.view(torch.int16)), (pair, (got.float() - want.float()).abs().max())
 
 
+@pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bnb.fp4", "int4-g32"])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (1024, 2048), (768, 6144), (2048, 1024)])
+def test_gemv_gate_route_matches_gemv_then_gate_route(ops, mode, N, K):
+    """lga_q4_gemv_gate_route (out-projection + residual, then in its last-arriving workgroup the next MoE's gate +
+    routing on the projection's output) == lga_q4_gemv + lga_moe_gate_route, bit for bit: y, expert ids and
+    probabilities, 8 / 4 experts, k = 1 / 2, tied gate rows; repeated launches (the counter re-arms) and a graph
+    replay."""
+    from lit_gpt.quantize import QuantLinear
+
+    g = torch.Generator().manual_seed(N + K)
+    proj = QuantLinear.from_float((torch.randn(N, K, generator=g) * 0.02).to(DEV), None, mode, DEV)
+    for E, k in ((8, 2), (4, 1), (8, 1)):
+        wg = torch.randn(E, N, generator=g) * 0.02
+        if E == 8:
+            wg[5] = wg[2]  # tied logits: the CPU torch.topk tie order decides
+        gate = QuantLinear.from_float(wg.to(DEV), None, mode, DEV)
+        assert ops.gemv_gate_route_supported(proj, gate, k)
+        nw = (1.0 + 0.1 * torch.randn(N, generator=g)).bfloat16().to(DEV)
+        ws = ops.GateRouteWorkspace(k, DEV)
+        for rep in range(3):
+            x = torch.randn(K, generator=g).bfloat16().to(DEV)
+            res = (torch.randn(N, generator=g) * 2).bfloat16().to(DEV)
+            want = ops.q4_gemv(x, proj.qweight, proj.scales, N, K, proj.group, proj.fmt, residual=res)
+            ids0, p0 = ops.moe_gate_route(want, gate.qweight, gate.scales, E, N, gate.group, gate.fmt, k,
+                                          norm_weight=nw, eps=1e-5)
+            got = ops.q4_gemv_gate_route(x, proj, res, gate, nw, 1e-5, k, ws)
+            assert torch.equal(got.view(torch.int16), want.view(torch.int16)), (mode, E, k, rep)
+            assert torch.equal(ws.ids, ids0) and torch.equal(ws.probs.view(torch.int16), p0.view(torch.int16)), \
+                (mode, E, k, rep, ws.ids, ids0)
+        assert int(ws.counter[0]) == 0  # re-armed
+    # graph replay: the captured launch recomputes from the buffers' current contents
+    x = torch.randn(K, generator=g).bfloat16().to(DEV)
+    res = torch.randn(N, generator=g).bfloat16().to(DEV)
+    out = torch.empty(N, dtype=torch.bfloat16, device=DEV)
+    ops.q4_gemv_gate_route(x, proj, res, gate, nw, 1e-5, k, ws, out=out)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ops.q4_gemv_gate_route(x, proj, res, gate, nw, 1e-5, k, ws, out=out)
+    for _ in range(2):
+        x.copy_(torch.randn(K, generator=g).bfloat16())
+        graph.replay()
+        torch.cuda.synchronize()
+        want = ops.q4_gemv(x, proj.qweight, proj.scales, N, K, proj.group, proj.fmt, residual=res)
+        ids0, p0 = ops.moe_gate_route(want, gate.qweight, gate.scales, gate.out_features, N, gate.group, gate.fmt,
+                                      k, norm_weight=nw, eps=1e-5)
+        assert torch.equal(out.view(torch.int16), want.view(torch.int16))
+        assert torch.equal(ws.ids, ids0) and torch.equal(ws.probs.view(torch.int16), p0.view(torch.int16))
+
+
 def test_moe_gate_route_rejects_bad_shapes(ops):
     x = torch.zeros(8192, dtype=torch.bfloat16, device=DEV)
     qw, sc = ops.quantize(torch.zeros(8, 8192, device=DEV), 0, 128)

@@ -54,7 +54,10 @@ def time_graph(fn, layers, reps=10):
 
 
 def q4(N, K, dev):
-    return ops.quantize(torch.randn(N, K, device=dev) * 0.02, ops.FMT_Q4G, 128)
+    from lit_gpt.quantize import _fit_group  # the group the product fits to a shard's K (e.g. 1376 at 7B TP = 8)
+
+    g = _fit_group(K, 128)
+    return ops.quantize(torch.randn(N, K, device=dev) * 0.02, ops.FMT_Q4G, g) + (g,)
 
 
 def run(name, C, H, G, I, tp, pos, layers, dev):
@@ -82,7 +85,7 @@ def run(name, C, H, G, I, tp, pos, layers, dev):
 
     def f_qkv():
         for w in W:
-            ops.q4_gemv(x, *w["qkv"], qkv_n, C, 128, 0, norm_weight=nw, out=qkv)
+            ops.q4_gemv(x, *w["qkv"][:2], qkv_n, C, w["qkv"][2], 0, norm_weight=nw, out=qkv)
 
     def f_attn():
         for w in W:
@@ -91,24 +94,24 @@ def run(name, C, H, G, I, tp, pos, layers, dev):
 
     def f_proj():
         for w in W:
-            ops.q4_gemv(y, *w["proj"], C, Kp, 128, 0, residual=x, out=o)
+            ops.q4_gemv(y, *w["proj"][:2], C, Kp, w["proj"][2], 0, residual=x, out=o)
 
     def f_fc():
         for w in W:
-            ops.q4_gemv_swiglu(x, *w["fc1"], *w["fc2"], Ir, C, 128, 0, norm_weight=nw, out=g)
+            ops.q4_gemv_swiglu(x, *w["fc1"][:2], *w["fc2"][:2], Ir, C, w["fc1"][2], 0, norm_weight=nw, out=g)
 
     def f_down():
         for w in W:
-            ops.q4_gemv(g, *w["down"], C, Ir, 128, 0, residual=x, out=o)
+            ops.q4_gemv(g, *w["down"][:2], C, Ir, w["down"][2], 0, residual=x, out=o)
 
     def f_layer():
         for w in W:
-            ops.q4_gemv(x, *w["qkv"], qkv_n, C, 128, 0, norm_weight=nw, out=qkv)
+            ops.q4_gemv(x, *w["qkv"][:2], qkv_n, C, w["qkv"][2], 0, norm_weight=nw, out=qkv)
             ops.attention_decode_fused(qkv.view(1, -1), w["kc"], w["vc"], p, p, cos, sin, Hr, Gr, hs, hs, scale,
                                        splits, workspace=ws, out=y.view(1, -1))
-            ops.q4_gemv(y, *w["proj"], C, Kp, 128, 0, residual=x, out=o)
-            ops.q4_gemv_swiglu(o, *w["fc1"], *w["fc2"], Ir, C, 128, 0, norm_weight=nw, out=g)
-            ops.q4_gemv(g, *w["down"], C, Ir, 128, 0, residual=o, out=x)
+            ops.q4_gemv(y, *w["proj"][:2], C, Kp, w["proj"][2], 0, residual=x, out=o)
+            ops.q4_gemv_swiglu(o, *w["fc1"][:2], *w["fc2"][:2], Ir, C, w["fc1"][2], 0, norm_weight=nw, out=g)
+            ops.q4_gemv(g, *w["down"][:2], C, Ir, w["down"][2], 0, residual=o, out=x)
 
     t = {k: time_graph(f, layers) for k, f in (("qkv", f_qkv), ("attn", f_attn), ("proj", f_proj), ("fc", f_fc),
                                                ("down", f_down), ("layer", f_layer))}
