@@ -140,6 +140,11 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
   uint4 qp[QPK];
 #pragma unroll
   for (int h = 0; h < QPK; ++h) qp[h] = FUSED ? rope8(qraw[h], cs, sn, sub) : qraw[h];
+  // the online softmax runs in log2 units (as the prefill's flash attention): scores scaled by scale * log2(e), every
+  // exponential one v_exp_f32 (exp2) instead of expf's 12-instruction range reduction — the long-context launches are
+  // VALU-bound (tools/attn_pmc.py: Mixtral at p = 32066, the waves VALU-active 40 % of their cycles, 2 per SIMD);
+  // the partials' m is in log2 units too (only this kernel's combine reads it)
+  const float sl2 = scale * 1.4426950408889634f;
   auto dot8 = [](const uint4 a, const uint4 b) {
     typedef short s2 __attribute__((ext_vector_type(2)));
     float d = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(s2, a.x), __builtin_bit_cast(s2, b.x), 0.0f, false);
@@ -173,17 +178,17 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
       float mx = m[h];
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const float sd = row_group_sum<LPR>(dot8(qp[h], kv[u])) * scale;  // whole row group active: DPP inside it
+        const float sd = row_group_sum<LPR>(dot8(qp[h], kv[u])) * sl2;  // whole row group active: DPP inside it
         s[u] = (j0 + u * RG < k_end) ? sd : -INFINITY;
         mx = fmaxf(mx, s[u]);
       }
-      const float c = expf(m[h] - mx);  // m = -inf (first step) -> 0
+      const float c = __builtin_amdgcn_exp2f(m[h] - mx);  // m = -inf (first step) -> 0
       l[h] *= c;
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[h][i] *= c;
 #pragma unroll
       for (int u = 0; u < UNR; ++u) {
-        const float e = expf(s[u] - mx);  // masked keys: exp(-inf) = 0
+        const float e = __builtin_amdgcn_exp2f(s[u] - mx);  // masked keys: exp(-inf) = 0
         l[h] += e;
         float vf[8];
         unpack8(vv[u], vf);
@@ -226,10 +231,10 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
     unpack8(vr, vf);
 #pragma unroll
     for (int h = 0; h < QPK; ++h) {
-      const float s = row_group_sum<LPR>(dot8(qp[h], kr)) * scale;
+      const float s = row_group_sum<LPR>(dot8(qp[h], kr)) * sl2;
       const float mx = fmaxf(m[h], s);
-      const float c = expf(m[h] - mx);
-      const float e = expf(s - mx);
+      const float c = __builtin_amdgcn_exp2f(m[h] - mx);
+      const float e = __builtin_amdgcn_exp2f(s - mx);
       l[h] = l[h] * c + e;
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[h][i] = fmaf(e, vf[i], o[h][i] * c);
@@ -243,8 +248,8 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
     for (int h = 0; h < QPK; ++h) {
       const float mo = __shfl_xor(m[h], off), lo = __shfl_xor(l[h], off);
       const float mn = fmaxf(m[h], mo);
-      const float ca = expf(m[h] - mn);  // m >= kMFloor: finite, never exp(-inf - -inf)
-      const float cb = expf(mo - mn);
+      const float ca = __builtin_amdgcn_exp2f(m[h] - mn);  // m >= kMFloor: finite, never exp(-inf - -inf)
+      const float cb = __builtin_amdgcn_exp2f(mo - mn);
       l[h] = l[h] * ca + lo * cb;
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[h][i] = o[h][i] * ca + __shfl_xor(o[h][i], off) * cb;
@@ -277,7 +282,7 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
     for (int w = 0; w < NW; ++w) bm = fmaxf(bm, sm[w][hq]);
 #pragma unroll
     for (int w = 0; w < NW; ++w) {
-      const float c = expf(sm[w][hq] - bm);
+      const float c = __builtin_amdgcn_exp2f(sm[w][hq] - bm);
       bl += sl[w][hq] * c;
       const float4 ov = *(const float4*)&so[w][hq][dq * 4];
       bo[0] += ov.x * c;
@@ -339,13 +344,13 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
         if (s0 + u >= n_splits) ml[u].x = -INFINITY;
         nm = fmaxf(nm, ml[u].x);
       }
-      const float c = expf(mx - nm);  // round 0: exp(-inf) = 0
+      const float c = __builtin_amdgcn_exp2f(mx - nm);  // round 0: exp(-inf) = 0
       lt *= c;
 #pragma unroll
       for (int i = 0; i < 4; ++i) ot[i] *= c;
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const float e = expf(ml[u].x - nm);
+        const float e = __builtin_amdgcn_exp2f(ml[u].x - nm);
         lt = fmaf(ml[u].y, e, lt);
         ot[0] = fmaf(o4[u].x, e, ot[0]);
         ot[1] = fmaf(o4[u].y, e, ot[1]);
