@@ -182,7 +182,7 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
         s[u] = (j0 + u * RG < k_end) ? sd : -INFINITY;
         mx = fmaxf(mx, s[u]);
       }
-      const float c = __builtin_amdgcn_exp2f(m[h] - mx);  // m = -inf (first step) -> 0
+      const float c = __builtin_amdgcn_exp2f(m[h] - mx);  // m = kMFloor (first step) -> 0
       l[h] *= c;
 #pragma unroll
       for (int i = 0; i < 8; ++i) o[h][i] *= c;

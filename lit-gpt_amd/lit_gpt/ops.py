@@ -551,10 +551,11 @@ def decode_splits(n_query_groups: int, q_per_kv: int, head_size: int, max_seq: i
     (tools/attn_sweep.py on MI355X, p = 2048..4000: 8 splits beat 16 for Llama-2-7B's 32 groups; with the few
     groups per rank of tensor parallelism 16 splits beat 32/64/128 — G = 4: 7.8 vs 10.9 us at 64 splits; G = 1,
     8 heads per group: 21 vs 34 us at 64 — because the last-arriving split's combine grows with the split count).
-    Caches of >= 20k rows (a long prompt: generate/base.py sizes the cache to prompt + new tokens) take up to 32:
-    at p = 32066 Mixtral 34.0 vs 35.7 us, its TP = 2 rank 23.5 vs 26.1; at 16000 16 still wins (22.1 vs 22.9), at
-    24000 32 does (28.5 vs 29.2) (tools/attn_ab.py interleaved, round 5, profiles/r05z_attn_long_context.txt)."""
-    s = max(1, min(n_cu // max(1, n_query_groups), 32 if max_seq >= 20480 else 16))
+    Caches of >= 12k rows (a long prompt: generate/base.py sizes the cache to prompt + new tokens) take up to 32:
+    with the log2-domain softmax, Mixtral 18.6 vs 19.3 us at p = 16000 and 28.4 vs 31.3 at 32066, its TP = 2 rank
+    13.8 vs 14.9 and 20.3 vs 24.4; at 8000 16 still wins for Mixtral (13.0 vs 14.4) and ties at TP = 2
+    (tools/attn_ab.py interleaved, round 5, profiles/r05z_attn_long_context.txt)."""
+    s = max(1, min(n_cu // max(1, n_query_groups), 32 if max_seq >= 12288 else 16))
     return min(s, max(1, max_seq // 16), 256)
 
 

@@ -104,7 +104,7 @@ def test_decode_attention_32k_context_mixtral_tp2_rank_shape():
 
     H, G, hs, S = 16, 4, 128, 32768
     splits = ops.decode_splits(G, H // G, hs, S)
-    assert splits == 32  # caches >= 20k rows (ops.decode_splits)
+    assert splits == 32  # caches >= 12k rows (ops.decode_splits)
     rng = np.random.default_rng(5)
     kc = torch.from_numpy(rng.standard_normal((G, S, hs), dtype=np.float32)).to(torch.bfloat16)
     vc = torch.from_numpy(rng.standard_normal((G, S, hs), dtype=np.float32)).to(torch.bfloat16)

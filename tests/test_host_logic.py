@@ -230,7 +230,7 @@ def test_topk_order_restatement_matches_cpu_torch_topk():
 
 def test_decode_attention_split_heuristic_per_tp_rank():
     """Sequence splits chosen for T = 1 attention (ops.decode_splits): 8 for Llama-2-7B's 32 groups, at most 16 for
-    the few groups a tensor-parallel rank keeps, 32 for caches of >= 20k rows (measured on MI355X,
+    the few groups a tensor-parallel rank keeps, 32 for caches of >= 12k rows (measured on MI355X,
     tools/attn_sweep.py)."""
     from lit_gpt import ops
 
@@ -240,7 +240,7 @@ def test_decode_attention_split_heuristic_per_tp_rank():
     assert ops.decode_splits(1, 8, 128, 2304) == 16  # 70B TP=8: one KV group, 8 heads per group
     assert ops.decode_splits(4, 4, 128, 32768) == 32  # Mixtral TP=2 at 32k context (long caches: up to 32)
     assert ops.decode_splits(8, 4, 128, 32068) == 32  # Mixtral TP=1, 32k prompt
-    assert ops.decode_splits(8, 4, 128, 20479) == 16
+    assert ops.decode_splits(8, 4, 128, 12287) == 16
     assert ops.decode_splits(32, 1, 128, 32768) == 8  # 7B at 32k: one workgroup per CU already
     assert ops.decode_splits(4, 1, 128, 64) == 4  # short caches: >= 16 keys per split
 
