@@ -46,6 +46,8 @@ def child(name):
 def main():
     if len(sys.argv) > 2 and sys.argv[1] == "--child":
         return child(sys.argv[2])
+    if "--gemv" in sys.argv:  # the decode GEMVs instead (tools/gemv_fetch.py's launches), per kernel
+        return gemv_pass()
     exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
     for name in GEOMS:
         out = Path(tempfile.mkdtemp(prefix="lga_apmc_"))
@@ -65,6 +67,28 @@ def main():
               f"  active_any {med['SQ_ACTIVE_INST_ANY'] / wc:.3f}  active_valu {med['SQ_ACTIVE_INST_VALU'] / wc:.3f};"
               f"  L2 hit {med['TCC_HIT_sum'] / (med['TCC_HIT_sum'] + med['TCC_MISS_sum']):.3f}", flush=True)
         shutil.rmtree(out, ignore_errors=True)
+
+
+def gemv_pass():
+    exe = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    out = Path(tempfile.mkdtemp(prefix="lga_gpmc_"))
+    cmd = ["timeout", "-s", "KILL", "120", exe, "--pmc", *COUNTERS, "--output-format", "csv", "-d", str(out),
+           "-o", "pmc", "--", sys.executable, str(REPO / "tools" / "gemv_fetch.py"), "--child"]
+    r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+    if r.returncode != 0:
+        print(f"gemv: rocprofv3 pass failed ({r.returncode}): {r.stderr[-400:]}", flush=True)
+        return 1
+    rows = [row for f in out.rglob("*counter_collection.csv") for row in csv.DictReader(open(f))
+            if "gemv" in row.get("Kernel_Name", "")]
+    for kname in sorted({rw["Kernel_Name"] for rw in rows}):
+        med = {c: statistics.median(float(rw["Counter_Value"]) for rw in rows
+                                    if rw["Counter_Name"] == c and rw["Kernel_Name"] == kname) for c in COUNTERS}
+        wc = med["SQ_WAVE_CYCLES"]
+        print(f"{kname[:64]}: wait_any {med['SQ_WAIT_ANY'] / wc:.3f}  wait_inst {med['SQ_WAIT_INST_ANY'] / wc:.3f}"
+              f"  active_any {med['SQ_ACTIVE_INST_ANY'] / wc:.3f}  active_valu {med['SQ_ACTIVE_INST_VALU'] / wc:.3f}"
+              f"  insts_valu {med['SQ_INSTS_VALU']:.4g}  L2 hit "
+              f"{med['TCC_HIT_sum'] / (med['TCC_HIT_sum'] + med['TCC_MISS_sum']):.3f}", flush=True)
+    shutil.rmtree(out, ignore_errors=True)
 
 
 if __name__ == "__main__":
