@@ -147,6 +147,32 @@ def test_tp2_xgmi_graph_decode_matches_tp1(mode, tmp_path):
 
 
 @pytest.mark.timeout(600)
+def test_tp2_sampled_decode_ranks_agree(tmp_path):
+    """Sampled decode under TP: generate(temperature=0.8, top_k=200) — the device sampler inside the
+    captured decode graph — after the same torch.manual_seed on every rank. Each rank draws its tokens itself
+    (replicated sampling, generate/tp.py), so the ranks' streams must be identical, or their KV caches would
+    silently diverge. Against TP = 1 of the same seed the draw uses the same uniform, but the random-init model's
+    top-200 probabilities are nearly flat (≈ 1/200 each), so the TP reduction order alone moves the inverse CDF to a
+    neighbouring kept index (measured: token 23411 vs 23476 at step 0); the check there is that each first token is
+    in the top-200 set of its own step-0 logits and that the two sets agree."""
+    outs = {}
+    for n in (1, 2):
+        d = tmp_path / f"tp{n}"
+        d.mkdir()
+        _launch("tp_geometry_worker.py", n, [d / "r.npz", "--model", "Llama-2-7b-hf", "--layers", "2", "--T", "32",
+                                             "--steps", "10", "--sampled", "--tmp", d], timeout=280)
+        outs[n] = np.load(d / "r.npz")
+        assert bool(outs[n]["sampled_same"]), f"TP={n}: ranks drew different tokens"
+        assert len(outs[n]["sampled_tokens"]) == 10
+    tops = {}
+    for n in (1, 2):
+        l0 = outs[n]["tp"][0]  # logits of the prompt's last row = the first draw's distribution
+        tops[n] = set(np.argsort(l0)[-200:].tolist())
+        assert int(outs[n]["sampled_tokens"][0]) in tops[n], n
+    assert len(tops[1] & tops[2]) >= 190, len(tops[1] & tops[2])
+
+
+@pytest.mark.timeout(600)
 def test_tp2_mixtral_32k_context(tmp_path):
     """BASELINE config 5 per rank: Mixtral-8x7B int4 at TP=2 (16 query heads / 4 KV groups, experts sliced to
     7168 rows, gate replicated) decoding at positions 32,000+ over a synthetic 32k KV context, one full-width

@@ -106,6 +106,8 @@ def main():
     ap.add_argument("--allreduce", default="xgmi", choices=["xgmi", "gloo"])
     ap.add_argument("--graph", action="store_true", help="also run greedy decode through the HIP graph")
     ap.add_argument("--greedy", action="store_true", help="feed each step the previous argmax (eager generate)")
+    ap.add_argument("--sampled", action="store_true",
+                    help="also run generate(temperature=0.8, top_k=200) after torch.manual_seed(1234) on every rank")
     ap.add_argument("--tmp", required=True)
     args = ap.parse_args()
     world, rank = int(os.environ["WORLD_SIZE"]), int(os.environ["RANK"])
@@ -157,6 +159,18 @@ def main():
             b.attn.kv_cache.reset_parameters()
         y = generate(model, ids[:T].to(DEV), T + args.steps, temperature=0.0)
         graph_tokens = y[T:].cpu().numpy()
+    sampled_tokens = np.zeros(0, dtype=np.int64)
+    if args.sampled and not P:
+        from generate.base import generate
+
+        for b in model.transformer.h:
+            b.attn.kv_cache.reset_parameters()
+        torch.manual_seed(1234)  # every rank draws the same sampler seed from its generator (replicated sampling)
+        y = generate(model, ids[:T].to(DEV), T + args.steps, temperature=0.8, top_k=200)
+        sampled_tokens = y[T:].cpu().numpy().astype(np.int64)
+    sl = [None] * world
+    dist.all_gather_object(sl, sampled_tokens)
+    sampled_same = all(np.array_equal(sl[0], t) for t in sl)
     err = comm.get_default().errors() if comm.get_default() is not None else 0
     torch.cuda.synchronize()
     tmp = Path(args.tmp)
@@ -223,7 +237,8 @@ def main():
         ref_step_gaps = np.minimum(ref_step_gaps, gaps64)
         np.savez(args.out, tp=got, ref=exp, ref64=exp64, gaps=np.array(step_gaps),
                  ref_gaps=np.array(ref_step_gaps), same_across_ranks=same_across_ranks,
-                 comm_err=err, graph_tokens=graph_tokens, fed=np.array(fed), oracle_s=time.time() - t0)
+                 comm_err=err, graph_tokens=graph_tokens, fed=np.array(fed), oracle_s=time.time() - t0,
+                 sampled_tokens=sampled_tokens, sampled_same=sampled_same)
     dist.barrier()
     if comm.get_default() is not None:
         comm.get_default().close()
