@@ -848,7 +848,12 @@ namespace {
 int run_grouped(Args a, int fmt, bool dual, int bm, int max_tiles, hipStream_t stream) {
   Plan p;
   p.bm = bm;
-  p.bn = bm == 64 && dual ? 256 : 128;
+  // 256 x 256 tiles once the routed rows are many (one Mixtral block, bit-identical: T = 8192 prefill 9.09 -> 8.52 ms,
+  // T = 32000 43.9 -> 38.5 ms; at T = 2048, 8192 rows, 2.70 vs 2.79 ms: 256 x 128 stays; tools/moe_prefill_ab.py)
+  p.bn = (bm == 64 && dual) || (bm == 256 && a.M > 8192) ? 256 : 128;
+  if (const char* e = getenv("LGA_GROUPED_BN")) {  // lab A/B: force the column width of the bm = 256 tiles
+    if (bm == 256 && (atoi(e) == 128 || atoi(e) == 256)) p.bn = atoi(e);
+  }
   p.mt = max_tiles;
   p.tn = dual ? p.bn / 2 : p.bn;
   p.tiles = p.mt * ((a.N + p.tn - 1) / p.tn);
