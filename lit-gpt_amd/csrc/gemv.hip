@@ -130,13 +130,18 @@ static int dispatch(const GemvArgs& a, int variant, hipStream_t stream) {
   if (variant < 0) {
     const long rows = DUAL ? 2L * a.N : a.N;
     variant = rows >= 24000 ? 1 : 0;  // tall matrices: more rows per wave keep the grid ~3-4 workgroups per CU
+    // the out-projection shape (residual epilogue, 2048..4096 rows, K <= 6144): 2 rows per wave, twice the
+    // workgroups — attn.proj 4096 x 4096 3.81 vs 4.18 us (tools/gemv_variants.py, round 5); qkv / down unchanged
+    if (!DUAL && !a.eidx && a.residual && a.N >= 2048 && a.N <= 4096 && cpt <= 3) variant |= 8;
   }
   // A persistent, double-buffered streaming form of this kernel (few workgroups per CU walking row tiles) measured
   // 10-70 % slower on every decode shape (tools/gemv_sweep.py, round 1) and was dropped.
   const bool big = (variant & 1) != 0;
+  const bool half = (variant & 8) != 0;  // half the small variant's rows per wave (bit 3)
 #define LGA_L(RS, RB, CPT)                                                         \
   do {                                                                             \
     if (big) launch<(DUAL ? (RB) / 2 : (RB)), CPT, FMT, DUAL>(a, stream);          \
+    else if (half) launch<((RS) >= 4 ? (DUAL ? (RS) / 4 : (RS) / 2) : (DUAL ? (RS) / 2 : (RS))), CPT, FMT, DUAL>(a, stream); \
     else launch<(DUAL ? (RS) / 2 : (RS)), CPT, FMT, DUAL>(a, stream);              \
   } while (0)
   switch (cpt) {

@@ -85,6 +85,11 @@ class QuantLinear(nn.Module):
     buffer so code that inspects ``linear.weight`` (e.g. ``.device``/``.dtype``) keeps working.
     """
 
+    # lga_q4_gemv launch variant for one-token inputs (-1: the library's heuristic). The opt-in fused kernels
+    # (attention + out-projection, out-projection + MoE gate) reproduce the 4-rows-per-wave form (variant 0); their
+    # bit-identity A/B tests pin the unfused side to it
+    gemv_variant = -1
+
     def __init__(self, in_features: int, out_features: int, fmt: int, group: int,
                  bias: Optional[torch.Tensor] = None, device=None):
         super().__init__()
@@ -129,7 +134,7 @@ class QuantLinear(nn.Module):
                 x2, norm_weight = ops.rmsnorm(x2, norm_weight, norm_eps), None
             y = ops.q4_gemv(x2.view(-1), self.qweight, self.scales, self.out_features, self.in_features, self.group,
                             self.fmt, bias=self.bias, residual=None if res is None else res.view(-1),
-                            norm_weight=norm_weight, eps=norm_eps)
+                            norm_weight=norm_weight, eps=norm_eps, variant=self.gemv_variant)
         else:
             if norm_weight is not None:
                 x2 = ops.rmsnorm(x2, norm_weight, norm_eps)

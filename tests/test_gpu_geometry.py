@@ -150,8 +150,11 @@ def test_decode_out_projection_inside_attention_launch_bit_identical(name, mode)
     H, G, hs = cfg.n_head, cfg.n_query_groups, cfg.head_size
     assert ops.decode_proj_supported(H, G, hs, ops.decode_splits(G, H // G, hs, T + N + 1), attn.proj)
     prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=3)).to(DEV)
+    from lit_gpt.quantize import QuantLinear
+
     outs = {}
     default = CausalSelfAttention.fuse_proj
+    QuantLinear.gemv_variant = 0  # the fused kernel reproduces the 4-rows-per-wave projection GEMV
     try:
         for fused in (False, True):
             CausalSelfAttention.fuse_proj = fused
@@ -167,6 +170,7 @@ def test_decode_out_projection_inside_attention_launch_bit_identical(name, mode)
             outs[fused] = torch.stack(seq)
     finally:
         CausalSelfAttention.fuse_proj = default
+        QuantLinear.gemv_variant = -1
     assert torch.equal(outs[False], outs[True])
 
 
@@ -184,8 +188,11 @@ def test_mixtral_gate_route_inside_out_projection_bit_identical(mode):
     T, N = 300, 6
     model = build_model(cfg, quantize=mode, device=DEV, seed=5, max_seq_length=T + N + 1)
     prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=5)).to(DEV)
+    from lit_gpt.quantize import QuantLinear
+
     outs, toks = {}, {}
     default = LLaMAMoE.fold_gate
+    QuantLinear.gemv_variant = 0  # the fused kernel reproduces the 4-rows-per-wave projection GEMV
     try:
         for fold in (False, True):
             LLaMAMoE.fold_gate = fold
@@ -205,6 +212,7 @@ def test_mixtral_gate_route_inside_out_projection_bit_identical(mode):
         assert model.transformer.h[0].mlp._route_req.proj_ok  # the fold ran
     finally:
         LLaMAMoE.fold_gate = default
+        QuantLinear.gemv_variant = -1
     assert torch.equal(outs[False], outs[True])
     assert toks[False] == toks[True]
 

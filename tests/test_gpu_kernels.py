@@ -651,7 +651,8 @@ def test_experts_combine_matches_gemv_then_combine(ops, fmt, group, N, K):
 @pytest.mark.parametrize("N,K", [(4096, 4096), (1024, 2048), (768, 6144), (2048, 1024)])
 def test_gemv_gate_route_matches_gemv_then_gate_route(ops, mode, N, K):
     """lga_q4_gemv_gate_route (out-projection + residual, then in its last-arriving workgroup the next MoE's gate +
-    routing on the projection's output) == lga_q4_gemv + lga_moe_gate_route, bit for bit: y, expert ids and
+    routing on the projection's output) == lga_q4_gemv (variant 0: the 4-rows-per-wave form the fused kernel
+    reproduces) + lga_moe_gate_route, bit for bit: y, expert ids and
     probabilities, 8 / 4 experts, k = 1 / 2, tied gate rows; repeated launches (the counter re-arms) and a graph
     replay."""
     from lit_gpt.quantize import QuantLinear
@@ -669,7 +670,7 @@ def test_gemv_gate_route_matches_gemv_then_gate_route(ops, mode, N, K):
         for rep in range(3):
             x = torch.randn(K, generator=g).bfloat16().to(DEV)
             res = (torch.randn(N, generator=g) * 2).bfloat16().to(DEV)
-            want = ops.q4_gemv(x, proj.qweight, proj.scales, N, K, proj.group, proj.fmt, residual=res)
+            want = ops.q4_gemv(x, proj.qweight, proj.scales, N, K, proj.group, proj.fmt, residual=res, variant=0)
             ids0, p0 = ops.moe_gate_route(want, gate.qweight, gate.scales, E, N, gate.group, gate.fmt, k,
                                           norm_weight=nw, eps=1e-5)
             got = ops.q4_gemv_gate_route(x, proj, res, gate, nw, 1e-5, k, ws)
@@ -690,7 +691,7 @@ def test_gemv_gate_route_matches_gemv_then_gate_route(ops, mode, N, K):
         x.copy_(torch.randn(K, generator=g).bfloat16())
         graph.replay()
         torch.cuda.synchronize()
-        want = ops.q4_gemv(x, proj.qweight, proj.scales, N, K, proj.group, proj.fmt, residual=res)
+        want = ops.q4_gemv(x, proj.qweight, proj.scales, N, K, proj.group, proj.fmt, residual=res, variant=0)
         ids0, p0 = ops.moe_gate_route(want, gate.qweight, gate.scales, gate.out_features, N, gate.group, gate.fmt,
                                       k, norm_weight=nw, eps=1e-5)
         assert torch.equal(out.view(torch.int16), want.view(torch.int16))
@@ -809,7 +810,7 @@ def test_attention_decode_proj_bit_identical_to_two_launches(ops, H, G, mode, bi
         pos = torch.tensor([p], device=DEV)
         ya = ops.attention_decode_fused(qkv, ka, va, pos, pos, cos, sin, H, G, hs, hs, scale, splits, workspace=ws_a)
         oa = ops.q4_gemv(ya.view(-1), lin.qweight, lin.scales, C, C, lin.group, lin.fmt, bias=lin.bias,
-                         residual=res.view(-1))
+                         residual=res.view(-1), variant=0)  # the 4-rows-per-wave form the fused kernel reproduces
         ob, yb = ops.attention_decode_proj(qkv, kb, vb, pos, pos, cos, sin, H, G, hs, hs, scale, splits, ws_b, lin,
                                            res)
         assert torch.equal(ka, kb) and torch.equal(va, vb), p
@@ -855,7 +856,8 @@ def test_attention_decode_proj_graph_replay(ops):
         pos_a.fill_(2041 + step)
         ya = ops.attention_decode_fused(qkv, ka, va, pos_a, pos_a, cos, sin, H, G, hs, hs, scale, splits,
                                         workspace=ws_a)
-        oa = ops.q4_gemv(ya.view(-1), lin.qweight, lin.scales, C, C, lin.group, lin.fmt, residual=res.view(-1))
+        oa = ops.q4_gemv(ya.view(-1), lin.qweight, lin.scales, C, C, lin.group, lin.fmt, residual=res.view(-1),
+                         variant=0)
         g.replay()
         torch.cuda.synchronize()
         assert int(pos_g.item()) == 2042 + step
