@@ -225,6 +225,18 @@ int lga_q4_gemv_swiglu_experts(const void* x, const uint8_t* qweight1, const voi
                                const void* scales2, const int32_t* expert_ids, int n_slots, int n_expert,
                                long long w_stride, long long s_stride, const void* norm_weight, float norm_eps,
                                void* y, int N, int K, int group, int fmt, int variant, lga_stream_t stream);
+/* lga_q4_gemv_experts_pair_combine: one token, k = 2, no tensor parallelism — the routed proj GEMVs of both slots
+ * (x [2][K] = the slots' SwiGLU rows, experts stacked as lga_q4_gemv_experts, expert_ids [2], probs [2]) and
+ * lga_moe_combine with the Block residual in one launch: y [N] = residual + sum in ascending expert id of
+ * bf16(probs[s] * expert_out[s]), bit-identical to lga_q4_gemv_experts + lga_moe_combine. The second-arriving
+ * workgroup of each row block combines: `scratch` [2][N] bf16 holds the first one's rows (write-through),
+ * `counters` (lga_q4_gemv_experts_pair_counters(N) words, caller-zeroed once) are re-armed by the kernel. */
+int lga_q4_gemv_experts_pair_supported(int N, int K, int group, int fmt);
+size_t lga_q4_gemv_experts_pair_counters(int N);
+int lga_q4_gemv_experts_pair_combine(const void* x, const uint8_t* qweight, const void* scales,
+                                     const int32_t* expert_ids, const void* probs, const void* residual, int n_expert,
+                                     long long w_stride, long long s_stride, void* y, void* scratch,
+                                     unsigned* counters, int N, int K, int group, int fmt, lga_stream_t stream);
 /* y[t] = residual[t] (optional) + the bf16 sum, in ascending expert order, of bf16(probs[t][s] * expert_out[t][s])
  * (the `y[token_idx] += probs * expert(...)` loop, model.py:739-742, then Block's residual add model.py:592). */
 int lga_moe_combine(const void* expert_out, const void* probs, const int32_t* expert_ids, const void* residual,

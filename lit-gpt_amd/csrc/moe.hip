@@ -183,6 +183,89 @@ static void launch_gemv_gate_route(const GemvArgs& a, const GemvArgs& gate, int 
   gemv_gate_route_kernel<4, CPT, FMT, GCPT><<<a.N / 16, 256, lds, stream>>>(a, gate, k, ids, probs, counter);
 }
 
+// Decode (one token, k = 2, no tensor parallelism): the routed proj GEMVs of both slots — lga_q4_gemv_experts's kernel
+// body for the shape, grid (row blocks, 2 slots), rows to LDS — and lga_moe_combine (+ the Block residual) in ONE
+// launch, the combine done by the second-arriving workgroup of each row block: the first stores its bf16 rows
+// write-through and arrives (MI355X_MICROARCH.md "Valid forms" row 1: sc1 16-B stores, drain, barrier, one agent-scope
+// add); the second reads them with sc1 loads, adds both experts in ascending id order with lga_moe_combine's rounding
+// points and the residual, and re-arms the block's counter. Bit-identical to lga_q4_gemv_experts + lga_moe_combine.
+constexpr int kPairStride = 64;  // per-row-block counters 256 B apart
+template <int RPR, int CPT, int FMT>
+__global__ void __launch_bounds__(256) moe_down_pair_kernel(GemvArgs a, const uint16_t* __restrict__ residual,
+                                                            uint16_t* __restrict__ y, uint16_t* __restrict__ scratch,
+                                                            unsigned* __restrict__ counters) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ unsigned s_ticket;
+  constexpr int ROWS = 4 * RPR, PIECES = ROWS / 8;  // the workgroup's rows, their 16-B pieces
+  const int b = blockIdx.x, slot = blockIdx.y, t = threadIdx.x;
+  const int row0 = b * ROWS;
+  // everything the combine needs, read up front: both ids (order), both probabilities, this block's residual rows
+  const int id0 = a.eidx[0], id1 = a.eidx[1];
+  const float p0 = bf2f(a.probs[0]), p1 = bf2f(a.probs[1]);
+  uint4 rv = make_uint4(0, 0, 0, 0);
+  if (t < PIECES) rv = ((const uint4*)(residual + row0))[t];
+  gemv_q4_body<RPR, CPT, FMT, false, false, false, 4, true>(a, b, smem);
+  __syncthreads();
+  const uint4* mine = (const uint4*)gemv_out_lds(smem, a.K);
+  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc((void*)scratch, (short)0, 2 * a.N * 2, 0x00020000);
+  if (t < PIECES)
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, mine[t]), srs,
+                                           (slot * a.N + row0 + t * 8) * 2, 0, 16);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  unsigned* ctr = counters + (size_t)b * kPairStride;
+  if (t == 0) s_ticket = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (s_ticket == 0) return;  // the other slot's workgroup combines
+  if (t < PIECES) {
+    const u32x4_t ov = __builtin_amdgcn_raw_buffer_load_b128(srs, ((1 - slot) * a.N + row0 + t * 8) * 2, 0, 16);
+    const uint4 e_mine = mine[t], e_other = __builtin_bit_cast(uint4, ov);
+    const uint4 e0 = slot == 0 ? e_mine : e_other, e1 = slot == 0 ? e_other : e_mine;  // slot 0's, slot 1's rows
+    const bool swap = id1 < id0;  // lga_moe_combine's stable order by expert id
+    const uint4 ea = swap ? e1 : e0, eb = swap ? e0 : e1;
+    const float pa = swap ? p1 : p0, pb = swap ? p0 : p1;
+    const uint32_t da[4] = {ea.x, ea.y, ea.z, ea.w}, db[4] = {eb.x, eb.y, eb.z, eb.w};
+    const uint32_t dr[4] = {rv.x, rv.y, rv.z, rv.w};
+    uint32_t out[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      float lo = 0.0f, hi = 0.0f;
+      lo = round_bf(lo + round_bf(pa * bflo(da[q])));
+      hi = round_bf(hi + round_bf(pa * bfhi(da[q])));
+      lo = round_bf(lo + round_bf(pb * bflo(db[q])));
+      hi = round_bf(hi + round_bf(pb * bfhi(db[q])));
+      out[q] = pack2(bflo(dr[q]) + lo, bfhi(dr[q]) + hi);
+    }
+    *(uint4*)(y + row0 + t * 8) = make_uint4(out[0], out[1], out[2], out[3]);
+  }
+  if (t == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // both arrived: re-arm
+}
+
+template <int RPR, int CPT, int FMT>
+static void launch_down_pair(const GemvArgs& a, const uint16_t* residual, uint16_t* y, uint16_t* scratch,
+                             unsigned* counters, hipStream_t stream) {
+  const dim3 grid(a.N / (4 * RPR), 2);
+  moe_down_pair_kernel<RPR, CPT, FMT><<<grid, 256, gemv_lds_bytes(a.K), stream>>>(a, residual, y, scratch, counters);
+}
+
+// gemv.hip dispatch's one-shot tile for an expert GEMV of this K (variant 0)
+template <int FMT>
+static int dispatch_down_pair(const GemvArgs& a, const uint16_t* residual, uint16_t* y, uint16_t* scratch,
+                              unsigned* counters, hipStream_t stream) {
+  switch ((a.K / 32 + 63) / 64) {
+    case 1: launch_down_pair<4, 1, FMT>(a, residual, y, scratch, counters, stream); break;
+    case 2: launch_down_pair<4, 2, FMT>(a, residual, y, scratch, counters, stream); break;
+    case 3: launch_down_pair<4, 3, FMT>(a, residual, y, scratch, counters, stream); break;
+    case 4: launch_down_pair<2, 4, FMT>(a, residual, y, scratch, counters, stream); break;
+    case 5:
+    case 6: launch_down_pair<2, 6, FMT>(a, residual, y, scratch, counters, stream); break;
+    case 7:
+    case 8: launch_down_pair<2, 8, FMT>(a, residual, y, scratch, counters, stream); break;
+    default: launch_down_pair<2, 16, FMT>(a, residual, y, scratch, counters, stream); break;
+  }
+  return 0;
+}
+
 template <int RPR, int CPT, int FMT>
 static void launch_down_combine(const GemvArgs& a, const int32_t* ids, hipStream_t stream) {
   // 16 waves, 8 per expert: 8 * RPR rows per workgroup, one workgroup per CU (both inputs staged in LDS)
@@ -373,6 +456,38 @@ extern "C" int lga_q4_gemv_experts_combine(const void* x, const uint8_t* qweight
   a.probs = (const uint16_t*)probs;
   const int rc = fmt == 0 ? lga::dispatch_down_combine<0>(a, expert_ids, stream)
                           : lga::dispatch_down_combine<1>(a, expert_ids, stream);
+  if (rc) return rc;
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_q4_gemv_experts_pair_supported(int N, int K, int group, int fmt) {
+  const int cpt = (K / 32 + 63) / 64;
+  return N > 0 && N % 16 == 0 && N / 8 <= 65535 && K > 0 && K % 32 == 0 && cpt <= 16 && group >= 32 &&
+         group % 32 == 0 && K % group == 0 && (fmt == 0 || fmt == 1 || fmt == 3) && N < 24000;
+}
+
+extern "C" size_t lga_q4_gemv_experts_pair_counters(int N) { return (size_t)(N / 8) * lga::kPairStride; }
+
+extern "C" int lga_q4_gemv_experts_pair_combine(const void* x, const uint8_t* qweight, const void* scales,
+                                                const int32_t* expert_ids, const void* probs, const void* residual,
+                                                int n_expert, long long w_stride, long long s_stride, void* y,
+                                                void* scratch, unsigned* counters, int N, int K, int group, int fmt,
+                                                hipStream_t stream) {
+  LGA_CHECK_ARG(x && qweight && scales && expert_ids && probs && residual && y && scratch && counters,
+                "lga_q4_gemv_experts_pair_combine: null pointer");
+  LGA_CHECK_ARG(lga_q4_gemv_experts_pair_supported(N, K, group, fmt),
+                "lga_q4_gemv_experts_pair_combine: geometry not covered (lga_q4_gemv_experts_pair_supported)");
+  LGA_CHECK_ARG(n_expert > 0 && w_stride >= (long long)N * K / 2 && s_stride > 0,
+                "lga_q4_gemv_experts_pair_combine: bad expert geometry");
+  lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, N, K, group,
+                  0.0f, expert_ids, w_stride, s_stride, K, n_expert, 2};
+  a.cb = lga::codebook_of(fmt);
+  a.probs = (const uint16_t*)probs;
+  const int rc = lga::kernel_fmt(fmt) == 0
+                     ? lga::dispatch_down_pair<0>(a, (const uint16_t*)residual, (uint16_t*)y, (uint16_t*)scratch,
+                                                  counters, stream)
+                     : lga::dispatch_down_pair<1>(a, (const uint16_t*)residual, (uint16_t*)y, (uint16_t*)scratch,
+                                                  counters, stream);
   if (rc) return rc;
   LGA_LAUNCH_RETURN();
 }

@@ -519,6 +519,10 @@ moe_gate_route = True
 # decode k = 2: routed proj GEMVs + combine in one launch (lga_q4_gemv_experts_combine) — off by default: bit-identical
 # but slower on MI355X (Mixtral bench 443.6 vs 452.6-454.0 tok/s A/B on one box); tests A/B the two
 moe_fused_combine = os.environ.get("LGA_MOE_FUSED_COMBINE", "0") == "1"
+# one-token sparse-MoE: the routed proj GEMVs of both slots + the combine + residual in one launch whose second-arriving
+# workgroup per row block combines (lga_q4_gemv_experts_pair_combine, bit-identical to the two launches); False keeps
+# lga_q4_gemv_experts + lga_moe_combine
+moe_pair_combine = os.environ.get("LGA_MOE_PAIR_COMBINE", "1") != "0"
 
 
 class _RouteRequest:
@@ -653,6 +657,14 @@ class LLaMAMoE(nn.Module):
                 # the routed proj GEMVs and the combine (+ residual) in one launch, same bits as the three below
                 return ops.q4_gemv_experts_combine(act, qp, sp, ids.view(-1), probs.view(-1), res.view(-1),
                                                    pj.out_features, pj.in_features, pj.group, pj.fmt).view(*lead, C)
+            if (moe_pair_combine and res is not None and k == 2 and not any(e._forward_hooks for e in self.experts)
+                    and ops.experts_pair_supported(pj.out_features, pj.in_features, pj.group, pj.fmt)):
+                pw = getattr(self, "_pair_ws", None)
+                if pw is None or pw.scratch.numel() != 2 * pj.out_features or pw.scratch.device != act.device:
+                    pw = self._pair_ws = ops.ExpertsPairWorkspace(pj.out_features, act.device)
+                return ops.q4_gemv_experts_pair_combine(act, qp, sp, ids.view(-1), probs.view(-1), res.view(-1),
+                                                        pj.out_features, pj.in_features, pj.group, pj.fmt,
+                                                        pw).view(*lead, C)
             eout = ops.q4_gemv_experts(act, qp, sp, ids.view(-1), pj.out_features, pj.in_features, pj.group,
                                        pj.fmt).view(1, k, C)
         else:

@@ -76,6 +76,10 @@ SIGNATURES = {
     "lga_moe_gate_route": [_P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P],
     "lga_q4_gemv_gate_route_supported": [_I, _I, _I, _I, _I, _I, _I, _I],
     "lga_q4_gemv_gate_route": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _F, _I, _I, _P, _P, _P, _P],
+    "lga_q4_gemv_experts_pair_supported": [_I, _I, _I, _I],
+    "lga_q4_gemv_experts_pair_counters": [_I],
+    "lga_q4_gemv_experts_pair_combine": [_P, _P, _P, _P, _P, _P, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _P,
+                                         _P, _I, _I, _I, _I, _P],
     "lga_q4_gemv_experts_combine": [_P, _P, _P, _P, _P, _P, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _I, _I, _I,
                                     _I, _P],
     "lga_q4_gemv_experts": [_P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _I, _P, _I, _I, _I, _I,
@@ -107,7 +111,7 @@ SIGNATURES = {
     "lga_q4_gemv_allreduce": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P, _P,
                               _P],
 }
-_RESTYPES = {"lga_q4f_workspace_bytes": ctypes.c_size_t, "lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
+_RESTYPES = {"lga_q4_gemv_experts_pair_counters": ctypes.c_size_t, "lga_q4f_workspace_bytes": ctypes.c_size_t, "lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
              "lga_comm_mailbox_bytes": ctypes.c_size_t, "lga_q4_gemv_argmax_work_bytes": ctypes.c_size_t}
 
 _lib: Optional[ctypes.CDLL] = None
@@ -757,6 +761,36 @@ def q4_gemv_gate_route(x, proj, residual, gate, norm_weight, eps, k, ws: GateRou
         _dev(norm_weight, "norm_weight", torch.bfloat16), float(eps), gate.out_features, k,
         _dev(ws.ids, "ids", torch.int32), _dev(ws.probs, "probs", torch.bfloat16),
         _dev(ws.counter, "counter", torch.int32), _stream()))
+    return y
+
+
+def experts_pair_supported(N: int, K: int, group: int, fmt: int) -> bool:
+    """Whether lga_q4_gemv_experts_pair_combine covers this routed proj shape."""
+    return bool(load_library().lga_q4_gemv_experts_pair_supported(N, K, group, fmt))
+
+
+class ExpertsPairWorkspace:
+    """Persistent scratch of lga_q4_gemv_experts_pair_combine for one MoE block (allocate before graph capture): the
+    first-arriving slot's rows [2][N] bf16 and the per-row-block arrival counters (zeroed once, re-armed by the kernel)."""
+
+    def __init__(self, N: int, device) -> None:
+        self.scratch = torch.empty(2 * N, dtype=torch.bfloat16, device=device)
+        self.counters = torch.zeros(int(load_library().lga_q4_gemv_experts_pair_counters(N)), dtype=torch.int32,
+                                    device=device)
+
+
+def q4_gemv_experts_pair_combine(x, qweight, scales, ids, probs, residual, N, K, group, fmt, ws, out=None):
+    """One token, k = 2: y (N,) = residual + combine of the two routed proj GEMVs (slot s: x[s] against expert ids[s]
+    of the (E, N, K/2) stack), bit-identical to q4_gemv_experts + moe_combine, in one launch."""
+    if ids.numel() != 2 or probs.numel() != 2 or x.numel() != 2 * K or residual.numel() != N:
+        raise ValueError("q4_gemv_experts_pair_combine: needs 2 slots (ids, probs, x of 2 x K) and a residual of N")
+    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
+    ws_, ss_ = _expert_strides(qweight, scales)
+    _check(load_library().lga_q4_gemv_experts_pair_combine(
+        _dev(x, "x", torch.bfloat16), _dev(qweight, "qweight", torch.uint8), _dev(scales, "scales"),
+        _dev(ids, "ids", torch.int32), _dev(probs, "probs", torch.bfloat16), _dev(residual, "residual", torch.bfloat16),
+        qweight.size(0), ws_, ss_, _dev(y, "y", torch.bfloat16), _dev(ws.scratch, "scratch", torch.bfloat16),
+        _dev(ws.counters, "counters", torch.int32), N, K, group, fmt, _stream()))
     return y
 
 

@@ -176,6 +176,45 @@ def test_decode_out_projection_inside_attention_launch_bit_identical(name, mode)
 
 @pytest.mark.parametrize("mode", ["int4-g128", "nf4"])
 @torch.inference_mode()
+def test_mixtral_pair_combine_bit_identical(mode):
+    """Full-width Mixtral-8x7B (2 blocks): the decode step's routed proj GEMVs + combine + residual as one launch
+    (model.moe_pair_combine, lga_q4_gemv_experts_pair_combine) give bit-identical logits and generated tokens to
+    lga_q4_gemv_experts + lga_moe_combine, eager and through the HIP-graph generate path."""
+    from generate.base import build_model, generate
+    from lit_gpt import Config
+    from lit_gpt import model as M
+
+    cfg = Config.from_name("Mixtral-8x7B-v0.1", n_layer=2)
+    T, N = 300, 6
+    model = build_model(cfg, quantize=mode, device=DEV, seed=6, max_seq_length=T + N + 1)
+    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=6)).to(DEV)
+    outs, toks = {}, {}
+    default = M.moe_pair_combine
+    try:
+        for fused in (False, True):
+            M.moe_pair_combine = fused
+            for b in model.transformer.h:
+                b.attn.kv_cache.reset_parameters()
+            lg = model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1]
+            tok, seq = int(torch.argmax(lg)), []
+            for i in range(N):
+                lg = model(torch.tensor([[tok]], device=DEV), torch.tensor([T + i], device=DEV),
+                           last_token_only=True)[0, -1]
+                seq.append(lg.clone())
+                tok = int(torch.argmax(lg))
+            outs[fused] = torch.stack(seq)
+            for b in model.transformer.h:
+                b.attn.kv_cache.reset_parameters()
+            toks[fused] = generate(model, prompt, T + N, temperature=0.0)[T:].tolist()
+        assert getattr(model.transformer.h[0].mlp, "_pair_ws", None) is not None  # the paired launch ran
+    finally:
+        M.moe_pair_combine = default
+    assert torch.equal(outs[False], outs[True])
+    assert toks[False] == toks[True]
+
+
+@pytest.mark.parametrize("mode", ["int4-g128", "nf4"])
+@torch.inference_mode()
 def test_mixtral_gate_route_inside_out_projection_bit_identical(mode):
     """Full-width Mixtral-8x7B block: the decode step's router gate + routing inside the attention's out-projection
     launch (LLaMAMoE.fold_gate, ops.q4_gemv_gate_route) gives bit-identical logits to the separate

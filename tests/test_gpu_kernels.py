@@ -698,6 +698,52 @@ def test_gemv_gate_route_matches_gemv_then_gate_route(ops, mode, N, K):
         assert torch.equal(ws.ids, ids0) and torch.equal(ws.probs.view(torch.int16), p0.view(torch.int16))
 
 
+@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (3, 64), (0, 32)])
+@pytest.mark.parametrize("N,K", [(4096, 14336), (512, 384), (1024, 2080), (768, 4096), (640, 6144), (512, 11008)])
+def test_experts_pair_combine_matches_gemv_then_combine(ops, fmt, group, N, K):
+    """lga_q4_gemv_experts_pair_combine (both slots' routed proj GEMVs, the second-arriving workgroup of each row block
+    combining) == lga_q4_gemv_experts + lga_moe_combine (+ residual), bit for bit: both slot orders, every
+    chunks-per-lane template, repeated launches (the counters re-arm) and a graph replay."""
+    if K % group:
+        pytest.skip("K must be a multiple of the group")
+    assert ops.experts_pair_supported(N, K, group, fmt)
+    g = torch.Generator().manual_seed(N + K + fmt + 7)
+    E = 8
+    qw, sc = [], []
+    for e in range(E):
+        q, s_ = ops.quantize((torch.randn(N, K, generator=g) * 0.02).to(DEV), fmt, group)
+        qw.append(q)
+        sc.append(s_)
+    qw, sc = torch.stack(qw), torch.stack(sc)
+    ws = ops.ExpertsPairWorkspace(N, DEV)
+    for pair in ((1, 6), (6, 1), (0, 7), (3, 3)):
+        ids = torch.tensor(pair, dtype=torch.int32, device=DEV)
+        x = torch.randn(2, K, generator=g).bfloat16().to(DEV)
+        probs = torch.softmax(torch.randn(2, generator=g), 0).bfloat16().to(DEV)
+        res = (torch.randn(N, generator=g) * 2).bfloat16().to(DEV)
+        eout = ops.q4_gemv_experts(x, qw, sc, ids, N, K, group, fmt)
+        want = ops.moe_combine(eout.view(1, 2, N).contiguous(), probs.view(1, 2), ids.view(1, 2),
+                               residual=res.view(1, N)).view(-1)
+        got = ops.q4_gemv_experts_pair_combine(x, qw, sc, ids, probs, res, N, K, group, fmt, ws)
+        assert torch.equal(got.view(torch.int16), want.view(torch.int16)), (pair, (got.float() - want.float()).abs().max())
+    assert int(ws.counters.abs().sum()) == 0  # re-armed
+    out = torch.empty(N, dtype=torch.bfloat16, device=DEV)
+    ops.q4_gemv_experts_pair_combine(x, qw, sc, ids, probs, res, N, K, group, fmt, ws, out=out)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ops.q4_gemv_experts_pair_combine(x, qw, sc, ids, probs, res, N, K, group, fmt, ws, out=out)
+    for pair in ((5, 2), (2, 5)):
+        ids.copy_(torch.tensor(pair, dtype=torch.int32))
+        x.copy_(torch.randn(2, K, generator=g).bfloat16())
+        graph.replay()
+        torch.cuda.synchronize()
+        eout = ops.q4_gemv_experts(x, qw, sc, ids, N, K, group, fmt)
+        want = ops.moe_combine(eout.view(1, 2, N).contiguous(), probs.view(1, 2), ids.view(1, 2),
+                               residual=res.view(1, N)).view(-1)
+        assert torch.equal(out.view(torch.int16), want.view(torch.int16)), pair
+
+
 def test_moe_gate_route_rejects_bad_shapes(ops):
     x = torch.zeros(8192, dtype=torch.bfloat16, device=DEV)
     qw, sc = ops.quantize(torch.zeros(8, 8192, device=DEV), 0, 128)
