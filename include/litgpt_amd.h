@@ -225,6 +225,17 @@ int lga_q4_gemv_swiglu_experts(const void* x, const uint8_t* qweight1, const voi
                                const void* scales2, const int32_t* expert_ids, int n_slots, int n_expert,
                                long long w_stride, long long s_stride, const void* norm_weight, float norm_eps,
                                void* y, int N, int K, int group, int fmt, int variant, lga_stream_t stream);
+/* lga_moe_gate_fc: one token of a sparse-MoE block without tensor parallelism — the router gate (RMSNorm fused) +
+ * top-k routing (lga_moe_gate_route) AND the routed fc_1 || fc_2 + SwiGLU GEMVs (lga_q4_gemv_swiglu_experts with
+ * that routing, y [k][N]) in one launch; every workgroup derives the routing itself (identical arithmetic), workgroup
+ * (0, 0) stores it to expert_ids [k] / probs [k] for the routed proj. Bit-identical to the two launches.
+ * Coverage: lga_moe_gate_fc_supported (K <= 4096, n_expert <= 8, gate format = the experts'). */
+int lga_moe_gate_fc_supported(int n_expert, int k, int N, int K, int group, int gate_group, int fmt, int gate_fmt);
+int lga_moe_gate_fc(const void* x, const void* norm_weight, float norm_eps, const uint8_t* gate_qweight,
+                    const void* gate_scales, int gate_group, int gate_fmt, int n_expert, int k, const uint8_t* qweight1,
+                    const void* scales1, const uint8_t* qweight2, const void* scales2, long long w_stride,
+                    long long s_stride, int n_expert_stack, void* y, int N, int K, int group, int fmt,
+                    int32_t* expert_ids, void* probs, lga_stream_t stream);
 /* lga_q4_gemv_experts_pair_combine: one token, k = 2, no tensor parallelism — the routed proj GEMVs of both slots
  * (x [2][K] = the slots' SwiGLU rows, experts stacked as lga_q4_gemv_experts, expert_ids [2], probs [2]) and
  * lga_moe_combine with the Block residual in one launch: y [N] = residual + sum in ascending expert id of

@@ -296,6 +296,44 @@ static int dispatch_down_combine(const GemvArgs& a, const int32_t* ids, hipStrea
   return 0;
 }
 
+// Decode (one token, sparse MoE, no tensor parallelism): the router gate + top-k routing AND the routed fc_1 || fc_2
+// + SwiGLU GEMVs in ONE launch. Every workgroup first runs moe_gate_route_kernel's body (the gate rows with fused
+// RMSNorm, the lga_q4_gemv tile, then route_row) on its own — the same arithmetic on the same inputs, so every
+// workgroup derives the same routing — and then its rows of the routed GEMV (lga_q4_gemv_swiglu_experts's body for
+// the shape) for the expert of its slot; workgroup (0, 0) also writes the routing for the routed proj launch. The
+// gate's 16 KB of weights are read by every workgroup (L2 hits after the first); the expert weights can only be
+// requested once the routing is known, which is the trade against the gate's own launch.
+template <int RPR, int CPT, int GCPT, int FMT>
+__global__ void __launch_bounds__(256) moe_gate_fc_kernel(GemvArgs g, GemvArgs a, int k, int32_t* __restrict__ ids,
+                                                          uint16_t* __restrict__ probs) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ KV sq[8];
+  __shared__ int32_t s_ids[8];
+  __shared__ uint16_t s_probs[8];
+  gemv_q4_body<4, GCPT, FMT, false, true, false, 4, true>(g, 0, smem);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    route_row(gemv_out_lds(smem, g.K), g.N, k, s_ids, s_probs, sq);
+    if (blockIdx.x == 0 && blockIdx.y == 0)
+      for (int s = 0; s < k; ++s) {
+        ids[s] = s_ids[s];
+        probs[s] = s_probs[s];
+      }
+  }
+  __syncthreads();
+  a.eidx = s_ids;  // read through a generic pointer by the body (LDS)
+  gemv_q4_body<RPR, CPT, FMT, true, true, false>(a, blockIdx.x, smem);
+}
+
+template <int RPR, int CPT, int FMT>
+static void launch_gate_fc(const GemvArgs& g, const GemvArgs& a, int k, int32_t* ids, uint16_t* probs,
+                           hipStream_t stream) {
+  const int waves = (a.N + RPR - 1) / RPR;
+  const dim3 grid((waves + 3) / 4, k);
+  const size_t lds = gemv_lds_bytes(a.K);
+  moe_gate_fc_kernel<RPR, CPT, CPT, FMT><<<grid, 256, lds, stream>>>(g, a, k, ids, probs);
+}
+
 template <int CPT, int FMT>
 static void launch_gate_route(const GemvArgs& a, int k, int32_t* ids, uint16_t* probs, hipStream_t stream) {
   const size_t lds = gemv_lds_bytes(a.K);
@@ -489,6 +527,53 @@ extern "C" int lga_q4_gemv_experts_pair_combine(const void* x, const uint8_t* qw
                      : lga::dispatch_down_pair<1>(a, (const uint16_t*)residual, (uint16_t*)y, (uint16_t*)scratch,
                                                   counters, stream);
   if (rc) return rc;
+  LGA_LAUNCH_RETURN();
+}
+
+extern "C" int lga_moe_gate_fc_supported(int n_expert, int k, int N, int K, int group, int gate_group, int fmt,
+                                         int gate_fmt) {
+  return n_expert >= 1 && n_expert <= 8 && k >= 1 && k <= n_expert && N > 0 && K > 0 && K % 32 == 0 && K <= 4096 &&
+         group >= 32 && group % 32 == 0 && K % group == 0 && gate_group >= 32 && gate_group % 32 == 0 &&
+         K % gate_group == 0 && (fmt == 0 || fmt == 1 || fmt == 3) && (gate_fmt == 0 || gate_fmt == 1 || gate_fmt == 3) &&
+         lga::kernel_fmt(fmt) == lga::kernel_fmt(gate_fmt);
+}
+
+extern "C" int lga_moe_gate_fc(const void* x, const void* norm_weight, float norm_eps, const uint8_t* gate_qweight,
+                               const void* gate_scales, int gate_group, int gate_fmt, int n_expert, int k,
+                               const uint8_t* qweight1, const void* scales1, const uint8_t* qweight2,
+                               const void* scales2, long long w_stride, long long s_stride, int n_expert_stack, void* y,
+                               int N, int K, int group, int fmt, int32_t* expert_ids, void* probs,
+                               hipStream_t stream) {
+  LGA_CHECK_ARG(x && norm_weight && gate_qweight && gate_scales && qweight1 && scales1 && qweight2 && scales2 && y &&
+                    expert_ids && probs,
+                "lga_moe_gate_fc: null pointer");
+  LGA_CHECK_ARG(lga_moe_gate_fc_supported(n_expert, k, N, K, group, gate_group, fmt, gate_fmt),
+                "lga_moe_gate_fc: geometry not covered (lga_moe_gate_fc_supported)");
+  LGA_CHECK_ARG(n_expert_stack >= n_expert && w_stride >= (long long)N * K / 2 && s_stride > 0,
+                "lga_moe_gate_fc: bad expert geometry");
+  lga::GemvArgs g{(const uint16_t*)x, gate_qweight, gate_scales, nullptr, nullptr, nullptr, nullptr,
+                  (const uint16_t*)norm_weight, nullptr, n_expert, K, gate_group, norm_eps};
+  g.cb = lga::codebook_of(gate_fmt);
+  lga::GemvArgs a{(const uint16_t*)x, qweight1, scales1, qweight2, scales2, nullptr, nullptr,
+                  (const uint16_t*)norm_weight, (uint16_t*)y, N, K, group, norm_eps, nullptr, w_stride, s_stride, 0,
+                  n_expert_stack, k};
+  a.cb = lga::codebook_of(fmt);
+  // lga_q4_gemv_swiglu_experts's tile (gemv.hip dispatch, variant < 0): 2N rows >= 24000 -> 4 rows per wave, else 2
+  const int cpt = (K / 32 + 63) / 64, kf = lga::kernel_fmt(fmt);
+  const bool big = 2L * N >= 24000;
+#define LGA_GF(RPR, CPT)                                                                            \
+  do {                                                                                              \
+    if (kf == 0) lga::launch_gate_fc<RPR, CPT, 0>(g, a, k, expert_ids, (uint16_t*)probs, stream);   \
+    else lga::launch_gate_fc<RPR, CPT, 1>(g, a, k, expert_ids, (uint16_t*)probs, stream);           \
+  } while (0)
+  if (cpt == 1) {
+    if (big) LGA_GF(4, 1);
+    else LGA_GF(2, 1);
+  } else {
+    if (big) LGA_GF(4, 2);
+    else LGA_GF(2, 2);
+  }
+#undef LGA_GF
   LGA_LAUNCH_RETURN();
 }
 

@@ -523,6 +523,10 @@ moe_fused_combine = os.environ.get("LGA_MOE_FUSED_COMBINE", "0") == "1"
 # workgroup per row block combines (lga_q4_gemv_experts_pair_combine, bit-identical to the two launches); False keeps
 # lga_q4_gemv_experts + lga_moe_combine
 moe_pair_combine = os.environ.get("LGA_MOE_PAIR_COMBINE", "1") != "0"
+# opt-in (LGA_MOE_GATE_FC=1): the gate + routing folded into the routed fc_1 || fc_2 launch (lga_moe_gate_fc: every
+# workgroup derives the routing itself; bit-identical). Off by default: Mixtral decode 2.270-2.273 vs 2.087-2.088 ms
+# per step (round 5) — every workgroup's gate prologue holds back its expert weight stream
+moe_gate_fc = os.environ.get("LGA_MOE_GATE_FC", "0") == "1"
 
 
 class _RouteRequest:
@@ -641,8 +645,15 @@ class LLaMAMoE(nn.Module):
             xin = x2 if (norm is None or fuse_norm) else norm(x2)
             nw = norm.weight if fuse_norm else None
             eps = norm.eps if fuse_norm else 1e-5
+            act = None
             if routed is not None:  # computed inside the attention's out-projection launch (same bits)
                 ids, probs = routed.ws.ids, routed.ws.probs
+            elif (moe_gate_fc and nw is not None and self._gate_route_ok(C)
+                  and ops.moe_gate_fc_supported(self.gate, f1, k)):
+                # gate + routing + the routed fc_1 || fc_2 + SwiGLU GEMVs in one launch (same bits as the three below)
+                g = self.gate
+                act, ids, probs = ops.moe_gate_fc(xin.view(-1), nw, eps, g, q1, s1, q2, s2, f1.out_features, C,
+                                                  f1.group, f1.fmt, k)
             elif self._gate_route_ok(C):  # gate GEMV + routing in one launch (same bits as the pair below)
                 g = self.gate
                 ids, probs = ops.moe_gate_route(xin.view(-1), g.qweight, g.scales, E, C, g.group, g.fmt, k,
@@ -650,8 +661,9 @@ class LLaMAMoE(nn.Module):
             else:
                 router = _lin(self.gate, xin, norm_weight=nw, norm_eps=eps).view(1, E)
                 ids, probs = ops.moe_route(router, k)
-            act = ops.q4_gemv_swiglu_experts(xin.view(-1), q1, s1, q2, s2, ids.view(-1), f1.out_features, C,
-                                             f1.group, f1.fmt, norm_weight=nw, eps=eps)
+            if act is None:
+                act = ops.q4_gemv_swiglu_experts(xin.view(-1), q1, s1, q2, s2, ids.view(-1), f1.out_features, C,
+                                                 f1.group, f1.fmt, norm_weight=nw, eps=eps)
             if (moe_fused_combine and res is not None and not any(e._forward_hooks for e in self.experts)
                     and ops.q4_gemv_experts_combine_fits(k, pj.out_features, pj.in_features)):
                 # the routed proj GEMVs and the combine (+ residual) in one launch, same bits as the three below

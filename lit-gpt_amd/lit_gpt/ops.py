@@ -76,6 +76,9 @@ SIGNATURES = {
     "lga_moe_gate_route": [_P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P],
     "lga_q4_gemv_gate_route_supported": [_I, _I, _I, _I, _I, _I, _I, _I],
     "lga_q4_gemv_gate_route": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _F, _I, _I, _P, _P, _P, _P],
+    "lga_moe_gate_fc_supported": [_I, _I, _I, _I, _I, _I, _I, _I],
+    "lga_moe_gate_fc": [_P, _P, _F, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_longlong, ctypes.c_longlong, _I,
+                        _P, _I, _I, _I, _I, _P, _P, _P],
     "lga_q4_gemv_experts_pair_supported": [_I, _I, _I, _I],
     "lga_q4_gemv_experts_pair_counters": [_I],
     "lga_q4_gemv_experts_pair_combine": [_P, _P, _P, _P, _P, _P, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _P,
@@ -762,6 +765,32 @@ def q4_gemv_gate_route(x, proj, residual, gate, norm_weight, eps, k, ws: GateRou
         _dev(ws.ids, "ids", torch.int32), _dev(ws.probs, "probs", torch.bfloat16),
         _dev(ws.counter, "counter", torch.int32), _stream()))
     return y
+
+
+def moe_gate_fc_supported(gate, fc_1, k: int) -> bool:
+    """Whether lga_moe_gate_fc covers this (router gate, stacked fc_1 expert) pair (K <= 4096, E <= 8)."""
+    return bool(load_library().lga_moe_gate_fc_supported(gate.out_features, k, fc_1.out_features, fc_1.in_features,
+                                                          fc_1.group, gate.group, fc_1.fmt, gate.fmt))
+
+
+def moe_gate_fc(x, norm_weight, eps, gate, qw1, sc1, qw2, sc2, N, K, group, fmt, k, *, ids=None, probs=None,
+                out=None):
+    """One token: (y (k, N), ids (1, k), probs (1, k)) = the routed fc_1 || fc_2 + SwiGLU GEMVs of the experts the
+    gate (RMSNorm fused) picks, routing and GEMVs in ONE launch — bit-identical to moe_gate_route +
+    q4_gemv_swiglu_experts."""
+    ws_, ss_ = _expert_strides(qw1, sc1)
+    if _expert_strides(qw2, sc2) != (ws_, ss_):
+        raise ValueError("fc_1 and fc_2 expert stacks must share one stride")
+    ids = ids if ids is not None else torch.empty(1, k, dtype=torch.int32, device=x.device)
+    probs = probs if probs is not None else torch.empty(1, k, dtype=torch.bfloat16, device=x.device)
+    y = out if out is not None else torch.empty(k, N, dtype=torch.bfloat16, device=x.device)
+    _check(load_library().lga_moe_gate_fc(
+        _dev(x, "x", torch.bfloat16), _dev(norm_weight, "norm_weight", torch.bfloat16), float(eps),
+        _dev(gate.qweight, "gate_qweight", torch.uint8), _dev(gate.scales, "gate_scales"), gate.group, gate.fmt,
+        gate.out_features, k, _dev(qw1, "qw1", torch.uint8), _dev(sc1, "sc1"), _dev(qw2, "qw2", torch.uint8),
+        _dev(sc2, "sc2"), ws_, ss_, qw1.size(0), _dev(y, "y", torch.bfloat16), N, K, group, fmt,
+        _dev(ids, "ids", torch.int32), _dev(probs, "probs", torch.bfloat16), _stream()))
+    return y, ids, probs
 
 
 def experts_pair_supported(N: int, K: int, group: int, fmt: int) -> bool:

@@ -176,10 +176,12 @@ def test_decode_out_projection_inside_attention_launch_bit_identical(name, mode)
 
 @pytest.mark.parametrize("mode", ["int4-g128", "nf4"])
 @torch.inference_mode()
-def test_mixtral_pair_combine_bit_identical(mode):
+@pytest.mark.parametrize("flag", ["moe_pair_combine", "moe_gate_fc"])
+def test_mixtral_pair_combine_bit_identical(mode, flag):
     """Full-width Mixtral-8x7B (2 blocks): the decode step's routed proj GEMVs + combine + residual as one launch
-    (model.moe_pair_combine, lga_q4_gemv_experts_pair_combine) give bit-identical logits and generated tokens to
-    lga_q4_gemv_experts + lga_moe_combine, eager and through the HIP-graph generate path."""
+    (model.moe_pair_combine, lga_q4_gemv_experts_pair_combine), and the gate + routing folded into the routed fc launch
+    (model.moe_gate_fc, lga_moe_gate_fc), each give bit-identical logits and generated tokens to the launches they
+    replace, eager and through the HIP-graph generate path."""
     from generate.base import build_model, generate
     from lit_gpt import Config
     from lit_gpt import model as M
@@ -189,10 +191,10 @@ def test_mixtral_pair_combine_bit_identical(mode):
     model = build_model(cfg, quantize=mode, device=DEV, seed=6, max_seq_length=T + N + 1)
     prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=6)).to(DEV)
     outs, toks = {}, {}
-    default = M.moe_pair_combine
+    default = getattr(M, flag)
     try:
         for fused in (False, True):
-            M.moe_pair_combine = fused
+            setattr(M, flag, fused)
             for b in model.transformer.h:
                 b.attn.kv_cache.reset_parameters()
             lg = model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1]
@@ -206,9 +208,10 @@ def test_mixtral_pair_combine_bit_identical(mode):
             for b in model.transformer.h:
                 b.attn.kv_cache.reset_parameters()
             toks[fused] = generate(model, prompt, T + N, temperature=0.0)[T:].tolist()
-        assert getattr(model.transformer.h[0].mlp, "_pair_ws", None) is not None  # the paired launch ran
+        if flag == "moe_pair_combine":
+            assert getattr(model.transformer.h[0].mlp, "_pair_ws", None) is not None  # the paired launch ran
     finally:
-        M.moe_pair_combine = default
+        setattr(M, flag, default)
     assert torch.equal(outs[False], outs[True])
     assert toks[False] == toks[True]
 

@@ -744,6 +744,54 @@ def test_experts_pair_combine_matches_gemv_then_combine(ops, fmt, group, N, K):
         assert torch.equal(out.view(torch.int16), want.view(torch.int16)), pair
 
 
+@pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bnb.fp4", "int4-g32"])
+@pytest.mark.parametrize("N,K", [(14336, 4096), (1024, 2048), (3000, 4096), (640, 1024)])
+def test_moe_gate_fc_matches_gate_route_then_experts(ops, mode, N, K):
+    """lga_moe_gate_fc (the gate + routing derived by every workgroup, then the routed fc_1 || fc_2 + SwiGLU rows) ==
+    lga_moe_gate_route + lga_q4_gemv_swiglu_experts, bit for bit: y, expert ids and probabilities, 8 / 4 experts,
+    k = 2 / 1, tied gate rows, both tile forms (2N >= 24000: 4 rows per wave, else 2) and a graph replay."""
+    from lit_gpt.quantize import QuantLinear
+
+    g = torch.Generator().manual_seed(N + K + 11)
+    for E, k in ((8, 2), (4, 1)):
+        fc1 = [QuantLinear.from_float((torch.randn(N, K, generator=g) * 0.02).to(DEV), None, mode, DEV) for _ in range(E)]
+        fc2 = [QuantLinear.from_float((torch.randn(N, K, generator=g) * 0.02).to(DEV), None, mode, DEV) for _ in range(E)]
+        q1, s1 = torch.stack([l.qweight for l in fc1]), torch.stack([l.scales for l in fc1])
+        q2, s2 = torch.stack([l.qweight for l in fc2]), torch.stack([l.scales for l in fc2])
+        wg = torch.randn(E, K, generator=g) * 0.02
+        if E == 8:
+            wg[5] = wg[2]  # tied logits: the CPU torch.topk tie order decides
+        gate = QuantLinear.from_float(wg.to(DEV), None, mode, DEV)
+        assert ops.moe_gate_fc_supported(gate, fc1[0], k)
+        nw = (1.0 + 0.1 * torch.randn(K, generator=g)).bfloat16().to(DEV)
+        grp, fmt = fc1[0].group, fc1[0].fmt
+        for rep in range(2):
+            x = torch.randn(K, generator=g).bfloat16().to(DEV)
+            ids0, p0 = ops.moe_gate_route(x, gate.qweight, gate.scales, E, K, gate.group, gate.fmt, k, norm_weight=nw,
+                                          eps=1e-5)
+            want = ops.q4_gemv_swiglu_experts(x, q1, s1, q2, s2, ids0.view(-1), N, K, grp, fmt, norm_weight=nw,
+                                              eps=1e-5)
+            got, ids1, p1 = ops.moe_gate_fc(x, nw, 1e-5, gate, q1, s1, q2, s2, N, K, grp, fmt, k)
+            assert torch.equal(ids1, ids0) and torch.equal(p1.view(torch.int16), p0.view(torch.int16)), (E, k, rep)
+            assert torch.equal(got.view(torch.int16), want.view(torch.int16)), (mode, E, k, rep)
+    out = torch.empty(k, N, dtype=torch.bfloat16, device=DEV)
+    ids_b = torch.empty(1, k, dtype=torch.int32, device=DEV)
+    pr_b = torch.empty(1, k, dtype=torch.bfloat16, device=DEV)
+    ops.moe_gate_fc(x, nw, 1e-5, gate, q1, s1, q2, s2, N, K, grp, fmt, k, ids=ids_b, probs=pr_b, out=out)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ops.moe_gate_fc(x, nw, 1e-5, gate, q1, s1, q2, s2, N, K, grp, fmt, k, ids=ids_b, probs=pr_b, out=out)
+    for _ in range(2):
+        x.copy_(torch.randn(K, generator=g).bfloat16())
+        graph.replay()
+        torch.cuda.synchronize()
+        ids0, p0 = ops.moe_gate_route(x, gate.qweight, gate.scales, gate.out_features, K, gate.group, gate.fmt, k,
+                                      norm_weight=nw, eps=1e-5)
+        want = ops.q4_gemv_swiglu_experts(x, q1, s1, q2, s2, ids0.view(-1), N, K, grp, fmt, norm_weight=nw, eps=1e-5)
+        assert torch.equal(ids_b, ids0) and torch.equal(out.view(torch.int16), want.view(torch.int16))
+
+
 def test_moe_gate_route_rejects_bad_shapes(ops):
     x = torch.zeros(8192, dtype=torch.bfloat16, device=DEV)
     qw, sc = ops.quantize(torch.zeros(8, 8192, device=DEV), 0, 128)
