@@ -333,7 +333,7 @@ def test_rope_kv_append_bit_exact(ops, H, G, hs, n_elem):
 @pytest.mark.parametrize("H,G,hs", [(32, 32, 128), (64, 8, 128), (8, 1, 128), (4, 2, 64)])
 @pytest.mark.parametrize("T,positions", [(1, [0]), (1, [2047]), (1, [2302]), (5, [100, 101, 102, 103, 104]),
                                           (3, [0, 1, 2])])
-@pytest.mark.parametrize("splits", [1, 36, 256])
+@pytest.mark.parametrize("splits", [1, 8, 36, 256])
 def test_attention_matches_reference(ops, H, G, hs, T, positions, splits):
     S = 2304
     q = bf16_np(synth.normal((T, H, hs), "aq", 5, 1.0))
@@ -458,17 +458,19 @@ def test_attention_decode_fused_rejects_unsupported_geometry(ops):
         ops.attention_decode_fused(qkv, kc, kc.clone(), pos, pos, cos, cos, 4, 4, 64, 64, 0.125)
 
 
-def test_attention_split_counters_rearm_across_launches(ops):
-    """The in-launch split merge re-arms its counters: repeated launches on one workspace stay correct."""
+@pytest.mark.parametrize("splits", [16, 8])
+def test_attention_split_counters_rearm_across_launches(ops, splits):
+    """The in-launch split merge re-arms its counters: repeated launches on one workspace stay correct (16 splits x 32
+    groups: more workgroups than CUs; 8 x 32: Llama-2-7B's decode geometry, one workgroup per CU)."""
     H, G, hs, S = 32, 32, 128, 2304
     q = to_dev_bf16(synth.normal((1, H, hs), "rq", 5, 1.0))
     k = to_dev_bf16(synth.normal((G, S, hs), "rk", 5, 1.0))
     v = to_dev_bf16(synth.normal((G, S, hs), "rv", 5, 1.0))
-    ws = ops.AttentionWorkspace(1, H, G, hs, 16, DEV)
+    ws = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
     outs = []
     for p in (2047, 5, 2047, 0, 2047):
         pos = torch.tensor([p], device=DEV)
-        outs.append(ops.attention(q, k, v, pos, H, G, hs, 0.1, n_splits=16, workspace=ws).clone())
+        outs.append(ops.attention(q, k, v, pos, H, G, hs, 0.1, n_splits=splits, workspace=ws).clone())
     assert torch.equal(outs[0], outs[2]) and torch.equal(outs[0], outs[4])
     assert int(ws.counters.abs().sum()) == 0
     ref0 = v[:, 0].reshape(-1)  # position 0: softmax over one key -> exactly v[0]
