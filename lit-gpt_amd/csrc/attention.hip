@@ -63,6 +63,9 @@ __device__ __forceinline__ uint4 ld_kv(const uint16_t* p) {
 // kernel start) — eight polled lines instead of one. The combiner whose add completes the launch moves sync[kBase] to
 // base + C: every workgroup has read the base by then (each holds an arrival ticket of some combined head, and a head
 // combines only after all its splits arrived).
+#ifndef LGA_ATTN_SOLO
+#define LGA_ATTN_SOLO 1  // lab A/B: 0 = the workgroup-barrier publish for every slice width
+#endif
 constexpr int kReplicas = 8, kBase = kReplicas * 64;  // sync words: replica r at r * 64 (256 B apart), then the base
 
 template <int HS, int QPK, int UNR, int NW, bool FUSED, bool PIPE, bool PROJ>
@@ -303,6 +306,10 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
   // ---- publish (m, l, o), then the last-arriving split of this (t, group) merges all splits (MI355X_MICROARCH.md
   // "Valid forms" row 1: 16-B sc1 stores, every storing wave drains, a workgroup barrier, one lane's agent-scope
   // add; the last arriver's loads are sc1 too). Per (head row, split): {m, l, 0, 0, o[HS]} fp32 ----
+  // SOLO: every output quad sits in wave 0 (QPK * HS / 4 <= 64), so wave 0 alone stores, drains, counts and, when
+  // last, combines: the same row-1 form with one storing wave, no workgroup barrier or LDS ticket on the tail
+  constexpr bool SOLO = !PROJ && LGA_ATTN_SOLO && NQ <= 64;
+  if (SOLO && wave != 0) return;
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(ws + row0 * n_splits * (HS + 4)), (short)0, QPK * n_splits * (HS + 4) * 4, 0x00020000);
   if (has_item) {
@@ -314,13 +321,21 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
                                              0, 16);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   unsigned* ctr = cnt + ((size_t)t * gridDim.y + gy) * kCounterStride;
-  if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
+  unsigned ticket;
+  if constexpr (SOLO) {
+    unsigned tk = 0;
+    if (lane == 0) tk = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = __builtin_amdgcn_readfirstlane(tk);  // lane 0's
+  } else {
+    __syncthreads();
+    if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    ticket = s_ticket;
+  }
   LGA_TRACE(5);
-  if (s_ticket != (unsigned)(n_splits - 1)) {
-    if (PROJ) *role = (int)s_ticket;  // a publisher: its arrival ticket (uniform, from LDS)
+  if (ticket != (unsigned)(n_splits - 1)) {
+    if (PROJ) *role = (int)ticket;  // a publisher: its arrival ticket (uniform)
     return;
   }
   if (PROJ) *role = -1;  // the combiner of this (t, group slice)
