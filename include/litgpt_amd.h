@@ -149,37 +149,6 @@ int lga_attention_decode_fused(const void* qkv, void* k_cache, void* v_cache, co
                                const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, void* y,
                                float* workspace, unsigned* counters, int n_head, int n_query_groups, int head_size,
                                int rope_n_elem, int max_seq, int n_splits, float scale, lga_stream_t stream);
-/* lga_qkv_attention_decode: the decode step's attention half in ONE launch — RMSNorm(norm_1) of x, the fused 4-bit
- * qkv Linear (`self.attn(x)`, lit_gpt/model.py:619; rows [G][q, k, v][hs] bit-identical to lga_q4_gemv with the
- * norm fused), RoPE of q and k, KVCache.forward's append at cache_pos[0] and the attention over keys 0..p
- * (lga_attention_decode_fused's math; y within fp32 summation order of it). The K/V rows before p are issued at
- * kernel start, beside the qkv weights. qkv_scratch: [n_query_groups * 3 * hs] bf16 (written, the rows handed between
- * workgroups); workspace / counters as lga_attention_decode_fused; group_sync: 2 * n_query_groups * 64 zeroed
- * uint32 (never re-zeroed). Geometry: lga_qkv_attention_supported (Llama-2-7B at TP = 1: C 4096, MHA, hs 128, 8
- * splits); caller checks it. */
-int lga_qkv_attention_supported(int n_embd, int n_head, int n_query_groups, int head_size, int n_splits, int group,
-                                int fmt);
-int lga_qkv_attention_decode(const void* x, const void* norm_weight, float norm_eps, const uint8_t* qweight,
-                             const void* scales, const void* bias, int group, int fmt, void* qkv_scratch, void* k_cache,
-                             void* v_cache, const int64_t* cache_pos, const int64_t* rope_pos, const float* cos,
-                             const float* sin, int rope_rows, void* y, float* workspace, unsigned* counters,
-                             unsigned* group_sync, int n_head, int n_query_groups, int head_size, int max_seq,
-                             int n_splits, float scale, lga_stream_t stream);
-/* lga_attention_decode_proj: lga_attention_decode_fused followed, in the SAME launch, by the out-projection
- * `self.proj(y)` (lit_gpt/model.py:656; the 4-bit Linear bnb's gemv_4bit serves at reference generate/base.py:128-136)
- * and the Block residual add `x + h` (model.py:591): out (N) = bf16(proj(y) [+ bias]) + residual, bit-identical to
- * lga_q4_gemv(y, ..., residual). y (n_head*hs bf16) still receives the attention row. sync: 1024 zeroed uint32 per
- * workspace (hand-off counter + base; never re-zeroed). Covers the geometries lga_attention_decode_proj_supported
- * reports (hs 128, n_splits >= 2, K = n_head*hs = 4096, q_per_kv slice 1 or 2, grid <= CUs); TP's row-parallel
- * projection keeps its own launch. */
-int lga_attention_decode_proj_supported(int n_head, int n_query_groups, int head_size, int n_splits, int N, int K,
-                                        int group, int fmt);
-int lga_attention_decode_proj(const void* qkv, void* k_cache, void* v_cache, const int64_t* cache_pos,
-                              const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows, void* y,
-                              float* workspace, unsigned* counters, unsigned* sync, int n_head, int n_query_groups,
-                              int head_size, int rope_n_elem, int max_seq, int n_splits, float scale,
-                              const uint8_t* proj_qweight, const void* proj_scales, const void* proj_bias,
-                              const void* residual, void* out, int N, int group, int fmt, lga_stream_t stream);
 
 /* -- sparse MoE (LLaMAMoE.forward, lit_gpt/model.py:727-743; Mixtral) ------------------------------------------
  * lga_moe_route: per token row of router logits [T][n_expert] bf16 -> expert_ids [T][k] int32 and probs [T][k]
@@ -193,26 +162,6 @@ int lga_moe_route(const void* logits, int T, int n_expert, int k, int32_t* exper
 int lga_moe_gate_route(const void* x, const uint8_t* qweight, const void* scales, const void* norm_weight,
                        float norm_eps, int n_expert, int K, int group, int fmt, int k, int32_t* expert_ids, void* probs,
                        lga_stream_t stream);
-/* lga_q4_gemv_gate_route: one token of a sparse-MoE block without tensor parallelism — the attention
- * out-projection + Block residual (`x = self.attn(...) + x`, model.py:591, 656; lga_q4_gemv with a residual) into
- * y [N], AND the router gate of the MLP that follows on y (RMSNorm norm_2 fused, model.py:592, 736) with its top-k
- * routing (model.py:737-738) into expert_ids [k] int32 / probs [k] bf16, in one launch: y bit-identical to
- * lga_q4_gemv, the routing bit-identical to lga_moe_gate_route on y. `counter`: one caller-zeroed word, re-armed by
- * the kernel. Coverage: lga_q4_gemv_gate_route_supported (N, K multiples of 32 up to 6144, gate format = the
- * projection's). */
-int lga_q4_gemv_gate_route_supported(int N, int K, int group, int fmt, int n_expert, int k, int gate_group,
-                                     int gate_fmt);
-int lga_q4_gemv_gate_route(const void* x, const uint8_t* qweight, const void* scales, const void* residual, void* y,
-                           int N, int K, int group, int fmt, const uint8_t* gate_qweight, const void* gate_scales,
-                           int gate_group, int gate_fmt, const void* norm_weight, float norm_eps, int n_expert, int k,
-                           int32_t* expert_ids, void* probs, unsigned* counter, lga_stream_t stream);
-/* lga_q4_gemv_experts_combine: one token, k = 2 — the routed proj GEMVs of both slots (x [2][K], expert_ids [2],
- * weights stacked as lga_q4_gemv_experts) and lga_moe_combine with the residual in one launch:
- * y [N] = residual + sum in ascending expert id of bf16(probs[s] * expert_out[s]), bit-identical to
- * lga_q4_gemv_experts + lga_moe_combine. N < 24000, K <= 16384. */
-int lga_q4_gemv_experts_combine(const void* x, const uint8_t* qweight, const void* scales, const int32_t* expert_ids,
-                                const void* probs, const void* residual, int n_expert, long long w_stride,
-                                long long s_stride, void* y, int N, int K, int group, int fmt, lga_stream_t stream);
 /* Routed expert GEMVs (the per-expert `expert(x[token_idx])` calls, model.py:741-742, for one token): slot s
  * (0..n_slots-1) uses expert e = expert_ids[s], whose packed weights / scales start at qweight + e * w_stride
  * bytes / scales + e * s_stride bytes (experts stacked with a uniform stride). lga_q4_gemv_experts reads
@@ -225,17 +174,6 @@ int lga_q4_gemv_swiglu_experts(const void* x, const uint8_t* qweight1, const voi
                                const void* scales2, const int32_t* expert_ids, int n_slots, int n_expert,
                                long long w_stride, long long s_stride, const void* norm_weight, float norm_eps,
                                void* y, int N, int K, int group, int fmt, int variant, lga_stream_t stream);
-/* lga_moe_gate_fc: one token of a sparse-MoE block without tensor parallelism — the router gate (RMSNorm fused) +
- * top-k routing (lga_moe_gate_route) AND the routed fc_1 || fc_2 + SwiGLU GEMVs (lga_q4_gemv_swiglu_experts with
- * that routing, y [k][N]) in one launch; every workgroup derives the routing itself (identical arithmetic), workgroup
- * (0, 0) stores it to expert_ids [k] / probs [k] for the routed proj. Bit-identical to the two launches.
- * Coverage: lga_moe_gate_fc_supported (K <= 4096, n_expert <= 8, gate format = the experts'). */
-int lga_moe_gate_fc_supported(int n_expert, int k, int N, int K, int group, int gate_group, int fmt, int gate_fmt);
-int lga_moe_gate_fc(const void* x, const void* norm_weight, float norm_eps, const uint8_t* gate_qweight,
-                    const void* gate_scales, int gate_group, int gate_fmt, int n_expert, int k, const uint8_t* qweight1,
-                    const void* scales1, const uint8_t* qweight2, const void* scales2, long long w_stride,
-                    long long s_stride, int n_expert_stack, void* y, int N, int K, int group, int fmt,
-                    int32_t* expert_ids, void* probs, lga_stream_t stream);
 /* lga_q4_gemv_experts_pair_combine: one token, k = 2, no tensor parallelism — the routed proj GEMVs of both slots
  * (x [2][K] = the slots' SwiGLU rows, experts stacked as lga_q4_gemv_experts, expert_ids [2], probs [2]) and
  * lga_moe_combine with the Block residual in one launch: y [N] = residual + sum in ascending expert id of

@@ -18,7 +18,6 @@
 #include <cstdlib>
 
 #include "decode_ops.h"
-#include "gemv_body.h"
 
 namespace lga {
 
@@ -55,27 +54,17 @@ __device__ __forceinline__ uint4 ld_kv(const uint16_t* p) {
 // q heads itself, and the workgroup whose split owns the new position p ropes k, appends k and v to the cache
 // at p (KVCache.forward, lit_gpt/model.py:788-795) and scores that key from registers — replacing the separate
 // lga_rope_kv_append launch of the decode step.
-// PROJ (decode, fused, tensor parallelism off): the attention output row y is handed to the out-projection GEMV that
-// the publishing (non-combining) workgroups of the SAME launch run afterwards (attn_proj_kernel). The combining splits
-// store y write-through (sc1), drain, and add 1 to each of kReplicas replicas of a counter (one wave instruction, one
-// lane per replica: MI355X_MICROARCH.md "Valid forms" row 2); a projection workgroup issues its weight loads first,
-// then polls ONE replica until it reaches base + C (C = combining workgroups per launch, base = sync[kBase] read at
-// kernel start) — eight polled lines instead of one. The combiner whose add completes the launch moves sync[kBase] to
-// base + C: every workgroup has read the base by then (each holds an arrival ticket of some combined head, and a head
-// combines only after all its splits arrived).
 #ifndef LGA_ATTN_SOLO
 #define LGA_ATTN_SOLO 1  // lab A/B: 0 = the workgroup-barrier publish for every slice width
 #endif
-constexpr int kReplicas = 8, kBase = kReplicas * 64;  // sync words: replica r at r * 64 (256 B apart), then the base
 
-template <int HS, int QPK, int UNR, int NW, bool FUSED, bool PIPE, bool PROJ>
+template <int HS, int QPK, int UNR, int NW, bool FUSED, bool PIPE>
 __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
                                           uint16_t* __restrict__ vc, const int64_t* __restrict__ input_pos,
                                           uint16_t* __restrict__ y, float* __restrict__ ws,
                                           unsigned* __restrict__ cnt, int n_head, int max_seq, float scale,
                                           const int64_t* __restrict__ rope_pos, const float* __restrict__ cos,
-                                          const float* __restrict__ sin, int rope_rows, int hsplit,
-                                          unsigned* __restrict__ sync, unsigned base, int* role = nullptr) {
+                                          const float* __restrict__ sin, int rope_rows, int hsplit) {
   constexpr int LPR = HS / 8;    // lanes per key row
   constexpr int RGW = 64 / LPR;  // row groups per wave
   constexpr int RG = NW * RGW;   // row groups per workgroup
@@ -308,7 +297,7 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
   // add; the last arriver's loads are sc1 too). Per (head row, split): {m, l, 0, 0, o[HS]} fp32 ----
   // SOLO: every output quad sits in wave 0 (QPK * HS / 4 <= 64), so wave 0 alone stores, drains, counts and, when
   // last, combines: the same row-1 form with one storing wave, no workgroup barrier or LDS ticket on the tail
-  constexpr bool SOLO = !PROJ && LGA_ATTN_SOLO && NQ <= 64;
+  constexpr bool SOLO = LGA_ATTN_SOLO && NQ <= 64;
   if (SOLO && wave != 0) return;
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       (void*)(ws + row0 * n_splits * (HS + 4)), (short)0, QPK * n_splits * (HS + 4) * 4, 0x00020000);
@@ -334,11 +323,7 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
     ticket = s_ticket;
   }
   LGA_TRACE(5);
-  if (ticket != (unsigned)(n_splits - 1)) {
-    if (PROJ) *role = (int)ticket;  // a publisher: its arrival ticket (uniform)
-    return;
-  }
-  if (PROJ) *role = -1;  // the combiner of this (t, group slice)
+  if (ticket != (unsigned)(n_splits - 1)) return;
   // one output column quad per thread, 8 splits per round with every load of the round in flight at once and an
   // online rescale across rounds. Split 0 always holds key 0, so the running max is finite after round 0; empty
   // splits carry m = kMFloor, l = 0, o = 0 and clamped out-of-range slots are forced to m = -inf: both weigh 0.
@@ -376,24 +361,9 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
     }
     uint16_t* yr = y + (row0 + hq) * HS + dq * 4;
     const uint2 yv = make_uint2(pack2(ot[0] / lt, ot[1] / lt), pack2(ot[2] / lt, ot[3] / lt));
-    if (PROJ)  // handed to other workgroups of this launch: write-through
-      __hip_atomic_store((unsigned long long*)yr, ((unsigned long long)yv.y << 32) | yv.x, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    else
-      *(uint2*)yr = yv;
+    *(uint2*)yr = yv;
   }
   if (threadIdx.x == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
-  if (PROJ) {  // y of this (t, group slice) is out: every storing wave drains, a barrier, one instruction counts it
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x < kReplicas) {
-      const unsigned C = gridDim.y * gridDim.z;
-      const unsigned prev =
-          __hip_atomic_fetch_add(sync + threadIdx.x * 64, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (threadIdx.x == 0 && prev == base + C - 1u)
-        __hip_atomic_store(sync + kBase, base + C, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
   LGA_TRACE(6);
 }
 
@@ -404,51 +374,8 @@ __global__ void __launch_bounds__(NW * 64) attn_kernel(const uint16_t* __restric
                                                    unsigned* __restrict__ cnt, int n_head, int max_seq, float scale,
                                                    const int64_t* __restrict__ rope_pos, const float* __restrict__ cos,
                                                    const float* __restrict__ sin, int rope_rows, int hsplit) {
-  attn_body<HS, QPK, UNR, NW, FUSED, PIPE, false>(q, kc, vc, input_pos, y, ws, cnt, n_head, max_seq, scale, rope_pos,
-                                                  cos, sin, rope_rows, hsplit, nullptr, 0u);
-}
-
-// The out-projection (CausalSelfAttention.proj, lit_gpt/model.py:656) + the Block residual add (:591) of a decode
-// token inside the attention launch: after its attention role (publish, or combine) every workgroup computes the
-// GEMV rows blk = its flat index with gemv_q4_body's exact arithmetic (bit-identical to lga_q4_gemv with a
-// residual), its weight loads issued before it waits for y. Replaces the separate proj launch: its ramp, and the
-// boundary in front of it, overlap the attention's tail.
-struct ProjArgs {
-  const uint8_t* qw;
-  const void* sc;
-  const uint16_t* bias;
-  const uint16_t* residual;
-  uint16_t* out;
-  unsigned* sync;
-  int N, K, group, cb;
-};
-
-// Row blocks of NW * RPR rows: publisher `slot` (its head slice gy * (n_splits - 1) + its arrival ticket) takes two
-// adjacent blocks while slot < n2 (one GEMV of 2 RPR rows per wave), one block after: n2 = blocks - publishers, so
-// every row is covered and the combiners — the last splits to finish — compute none.
-template <int HS, int QPK, int UNR, int NW, int RPR, int CPT, int FMT>
-__global__ void __launch_bounds__(NW * 64) attn_proj_kernel(const uint16_t* __restrict__ q, uint16_t* __restrict__ kc,
-                                                        uint16_t* __restrict__ vc, const int64_t* __restrict__ input_pos,
-                                                        uint16_t* __restrict__ y, float* __restrict__ ws,
-                                                        unsigned* __restrict__ cnt, int n_head, int max_seq,
-                                                        float scale, const int64_t* __restrict__ rope_pos,
-                                                        const float* __restrict__ cos, const float* __restrict__ sin,
-                                                        int rope_rows, int hsplit, ProjArgs pa) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const unsigned base = pa.sync[kBase];  // written only by the previous launch's last combiner (kernel boundary)
-  int role = -1;
-  attn_body<HS, QPK, UNR, NW, true, LGA_ATTN_PIPE != 0, true>(q, kc, vc, input_pos, y, ws, cnt, n_head, max_seq,
-                                                              scale, rope_pos, cos, sin, rope_rows, hsplit, pa.sync,
-                                                              base, &role);
-  if (role < 0) return;  // combiners compute no projection rows
-  const int slot = blockIdx.y * (gridDim.x - 1) + role;
-  const int publishers = gridDim.y * (gridDim.x - 1), blocks = pa.N / (NW * RPR), n2 = blocks - publishers;
-  GemvArgs a{y, pa.qw, pa.sc, nullptr, nullptr, pa.bias, pa.residual, nullptr, pa.out, pa.N, pa.K, pa.group, 0.0f};
-  a.cb = pa.cb;
-  a.xwait = pa.sync + ((blockIdx.x + blockIdx.y) % kReplicas) * 64;
-  a.xwait_target = base + gridDim.y * gridDim.z;
-  if (slot < n2) gemv_q4_body<2 * RPR, CPT, FMT, false, false, true, NW, false, false, true>(a, slot, smem);
-  else gemv_q4_body<RPR, CPT, FMT, false, false, true, NW, false, false, true>(a, 2 * n2 + (slot - n2), smem);
+  attn_body<HS, QPK, UNR, NW, FUSED, PIPE>(q, kc, vc, input_pos, y, ws, cnt, n_head, max_seq, scale, rope_pos, cos,
+                                           sin, rope_rows, hsplit);
 }
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
@@ -1051,24 +978,6 @@ static int launch_hs(const void* q, void* kc, void* vc, const int64_t* pos, void
   return 0;
 }
 
-// attn_proj_kernel geometry: the decode-attention config a q_per_kv slice runs (as launch_hs picks it) x the proj
-// GEMV's row tile (gemv.hip dispatch: K = 4096 -> 4 rows x 2 chunks per lane). Returns 0 when not covered.
-static int proj_shape(int H, int G, int hs, int n_splits, int N, int K, int group, int fmt, int* hsplit_out) {
-  if (hs != 128 || n_splits < 2 || H % G || K != H * hs || K != 4096 || N % 16 || group < 32 || group % 32 ||
-      K % group || (fmt != 0 && fmt != 1 && fmt != 3))
-    return 0;
-  const int hsplit = attn_hsplit(1, G, H / G, n_splits);
-  const int qpk = H / G / hsplit;
-  if (qpk != 1 && qpk != 2) return 0;
-  if (qpk == 1 && G * hsplit <= 16) return 0;  // the 8-wave few-groups config: not instantiated
-  const long wgs = (long)n_splits * G * hsplit, publishers = (long)(n_splits - 1) * G * hsplit, blocks = N / 16;
-  // the publishers hold one or two 16-row blocks of the projection each, and the whole grid must be resident at once
-  // (the projection's workgroups wait for heads combined by others of the same launch)
-  if (blocks < publishers || blocks > 2 * publishers || wgs > num_cu()) return 0;
-  if (hsplit_out) *hsplit_out = hsplit;
-  return qpk;
-}
-
 }  // namespace lga
 
 int lga::preload_attention() {
@@ -1149,49 +1058,6 @@ extern "C" int lga_attention_decode_fused(const void* qkv, void* k_cache, void* 
                                            n_query_groups, max_seq, n_splits, scale, rope_pos, cos, sin, rope_rows,
                                            stream);
   if (rc) return rc;
-  LGA_LAUNCH_RETURN();
-}
-
-extern "C" int lga_attention_decode_proj_supported(int n_head, int n_query_groups, int head_size, int n_splits, int N,
-                                                   int K, int group, int fmt) {
-  if (n_head <= 0 || n_query_groups <= 0) return 0;
-  return lga::proj_shape(n_head, n_query_groups, head_size, n_splits, N, K, group, fmt, nullptr) ? 1 : 0;
-}
-
-extern "C" int lga_attention_decode_proj(const void* qkv, void* k_cache, void* v_cache, const int64_t* cache_pos,
-                                         const int64_t* rope_pos, const float* cos, const float* sin, int rope_rows,
-                                         void* y, float* workspace, unsigned* counters, unsigned* sync, int n_head,
-                                         int n_query_groups, int head_size, int rope_n_elem, int max_seq, int n_splits,
-                                         float scale, const uint8_t* proj_qweight, const void* proj_scales,
-                                         const void* proj_bias, const void* residual, void* out, int N, int group,
-                                         int fmt, hipStream_t stream) {
-  LGA_CHECK_ARG(qkv && k_cache && v_cache && cache_pos && rope_pos && cos && sin && y && workspace && counters && sync &&
-                    proj_qweight && proj_scales && residual && out,
-                "lga_attention_decode_proj: null pointer");
-  LGA_CHECK_ARG(n_query_groups > 0 && n_head % n_query_groups == 0, "lga_attention_decode_proj: bad head geometry");
-  LGA_CHECK_ARG(head_size == 128 && rope_n_elem == 128, "lga_attention_decode_proj: needs head_size == rope_n_elem == 128");
-  LGA_CHECK_ARG(rope_rows > 0 && max_seq > 0, "lga_attention_decode_proj: empty rope cache or kv cache");
-  const int K = n_head * head_size;
-  int hsplit = 1;
-  const int qpk = lga::proj_shape(n_head, n_query_groups, head_size, n_splits, N, K, group, fmt, &hsplit);
-  LGA_CHECK_ARG(qpk != 0, "lga_attention_decode_proj: geometry not covered (lga_attention_decode_proj_supported)");
-  const dim3 grid(n_splits, n_query_groups * hsplit, 1);
-  const size_t lds = lga::gemv_lds_bytes(K);
-  lga::ProjArgs pa{proj_qweight, proj_scales, (const uint16_t*)proj_bias, (const uint16_t*)residual, (uint16_t*)out,
-                   sync, N, K, group, lga::codebook_of(fmt)};
-#define LGA_AP(QPK, FMT)                                                                                              \
-  lga::attn_proj_kernel<128, QPK, 4, 4, 4, 2, FMT><<<grid, 256, lds, stream>>>(                                      \
-      (const uint16_t*)qkv, (uint16_t*)k_cache, (uint16_t*)v_cache, cache_pos, (uint16_t*)y, workspace, counters,    \
-      n_head, max_seq, scale, rope_pos, cos, sin, rope_rows, hsplit, pa)
-  const int kf = lga::kernel_fmt(fmt);
-  if (qpk == 1) {
-    if (kf == 0) LGA_AP(1, 0);
-    else LGA_AP(1, 1);
-  } else {
-    if (kf == 0) LGA_AP(2, 0);
-    else LGA_AP(2, 1);
-  }
-#undef LGA_AP
   LGA_LAUNCH_RETURN();
 }
 

@@ -45,38 +45,20 @@ struct GemvArgs {
   long long ew, es;
   int xs, n_expert, slots;
   int cb = 0;  // codebook row of kCode4 (FMT 1): 0 nf4, 1 fp4
-  // MOE2 (lga_q4_gemv_experts_combine): qw/sc = slot 0's expert, qw2/sc2 = slot 1's, x / x + xs = their inputs;
-  // probs = the 2 routing probabilities, moe_swap = slot 1's expert id is the lower (it is added first)
-  const uint16_t* probs = nullptr;
-  int moe_swap = 0;
-  float moe_pa = 0.0f, moe_pb = 0.0f;  // MOE2: the probabilities in addition order (read at kernel start)
-  // XWAIT (the out-projection inside the decode-attention launch): x is produced by other workgroups of the same
-  // launch; the body issues its weight / scale / residual loads first, then waits until *xwait reaches
-  // xwait_target (wrap-safe) and reads x with sc1 loads
-  const unsigned* xwait = nullptr;
-  unsigned xwait_target = 0;
+  const uint16_t* probs = nullptr;  // routing probabilities (lga_q4_gemv_experts_pair_combine)
 };
 
 // LDS of gemv_q4_body: x pairs (2K B), chunk sums (K/32 floats), norm partials (16), codebook (16), then (LDS_OUT)
 // the workgroup's output rows at a 16-B-aligned offset
 __host__ __device__ inline size_t gemv_out_offset(int K) { return ((size_t)K * 2 + (K / 32) * 4 + 128 + 15) & ~(size_t)15; }
 __host__ __device__ inline size_t gemv_lds_bytes(int K) { return gemv_out_offset(K) + 256; }
-// MOE2: the second input's x pairs and chunk sums follow at gemv_lds_bytes(K)
-__host__ __device__ inline size_t gemv_moe2_lds_bytes(int K) { return gemv_lds_bytes(K) + (size_t)K * 2 + (K / 32) * 4; }
 __device__ __forceinline__ uint16_t* gemv_out_lds(unsigned char* smem, int K) { return (uint16_t*)(smem + gemv_out_offset(K)); }
 
 // One wave of a decode GEMV (see gemv.hip for the design). NW waves per workgroup (each its own row slot); the
 // workgroup stages x once for all of them. LDS_OUT (gemv_ar.hip): the workgroup's NW * RPR bf16 rows go to LDS
 // (gemv_out_lds) instead of a.y, for an epilogue that moves them on as 16-B pieces.
-// MOE2 (with RES): the two routed experts of one token — waves 0 .. NW/2-1 compute the workgroup's rows for slot 0's
-// expert against its input a.x, the other half the SAME rows for slot 1's expert against a.x + a.xs, each row exactly
-// as the single-expert GEMV computes it — then the rows' two results meet in LDS and are summed as lga_moe_combine
-// does (ascending expert id, bf16 rounding points, + residual): the routed proj GEMV and the combine in one launch.
-template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, int NW = 4, bool LDS_OUT = false,
-          bool MOE2 = false, bool XWAIT = false>
+template <int RPR, int CPT, int FMT, bool DUAL, bool NORM, bool RES, int NW = 4, bool LDS_OUT = false>
 __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char* smem) {
-  static_assert(!MOE2 || (!DUAL && RES && !NORM && !LDS_OUT), "MOE2 runs as RES, without dual / norm / LDS output");
-  static_assert(!XWAIT || (!MOE2 && !DUAL), "XWAIT: a plain projection (optionally RMS-normalised)");
   if (a.eidx) {  // wave-uniform: one scalar load of the routed expert id, then plain pointer offsets
     const long long e = min(max(a.eidx[blockIdx.y], 0), a.n_expert - 1);
     a.qw += e * a.ew;
@@ -92,34 +74,26 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
   float* xsum = (float*)(smem + (size_t)a.K * 2);  // K/32 chunk sums
   float* red = xsum + a.K / 32;                    // NW (<= 16)
   float* nf4 = red + 16;                           // 16
-  uint4* xl2 = (uint4*)(smem + gemv_lds_bytes(a.K));  // MOE2: slot 1's input
-  float* xsum2 = (float*)((unsigned char*)xl2 + (size_t)a.K * 2);
   constexpr int NT = NW * 64;
   constexpr int XI = (CPT * 4 + NW - 1) / NW;      // x uint4 per thread (CPT * 256 >= K / 8)
   static_assert(NW == 4 || NW == 8 || NW == 16, "4, 8 or 16 waves per workgroup");
   constexpr int R = DUAL ? 2 * RPR : RPR;          // values per lane entering the butterfly
   const int t = threadIdx.x, wave = t >> 6, lane = t & 63;
   const int NC = a.K / 32, n8 = a.K / 8, groups = a.K / a.G;
-  const int slot = MOE2 ? wave / (NW / 2) : 0;  // MOE2: which expert this wave computes (wave-uniform)
-  const int row0 = MOE2 ? (blk * (NW / 2) + wave % (NW / 2)) * RPR : (blk * NW + wave) * RPR;
-  if (MOE2 && slot) {
-    a.qw = a.qw2;
-    a.sc = a.sc2;
-  }
+  const int row0 = (blk * NW + wave) * RPR;
   if (FMT == 1 && t < 16) nf4[t] = kCode4[a.cb][t];
   LGA_GTRACE_NOWAIT(0);
 
   // 1. activation (and norm weight) share of this thread: uint4 t, t+NT, ... (clamped, branch-free)
-  uint4 xr[XI], nr[XI], xr2[MOE2 ? XI : 1];
+  uint4 xr[XI], nr[XI];
 #pragma unroll
-  for (int i = 0; i < (XWAIT && !NORM ? 0 : XI); ++i) {  // XWAIT: x itself comes after the weights (below)
+  for (int i = 0; i < XI; ++i) {
     const int u = min(t + NT * i, n8 - 1);
-    if (MOE2) xr2[MOE2 ? i : 0] = ((const uint4*)(a.x + a.xs))[u];
 #ifdef LGA_LAB_NOX  // lab builds only: cost of the activation fetch
     xr[i] = make_uint4(0x3F803F80u + u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u);
     if (NORM) nr[i] = xr[i];
 #else
-    if (!XWAIT) xr[i] = ((const uint4*)a.x)[u];
+    xr[i] = ((const uint4*)a.x)[u];
     if (NORM) nr[i] = ((const uint4*)a.norm_w)[u];
 #endif
   }
@@ -155,26 +129,6 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
   if (RES) res = a.residual[min(row0 + (lane & (RPR - 1)), a.N - 1)];
   __builtin_amdgcn_sched_barrier(0);  // nothing that waits on x may move above the weight loads
   LGA_GTRACE_NOWAIT(1);
-  if (XWAIT) {
-    // x comes from other workgroups of this launch (MI355X_MICROARCH.md "Valid forms" row 1): one lane polls the
-    // producers' agent-scope counter with sc1 loads, a workgroup barrier, then every x load is an sc1 load. The
-    // weights above stay in flight meanwhile. Bounded (1 s at 100 MHz) so a broken hand-off cannot hang the GPU.
-    if (t == 0) {
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      while ((int)(__hip_atomic_load(a.xwait, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - a.xwait_target) < 0 &&
-             __builtin_amdgcn_s_memrealtime() - t0 < 100000000ull)
-        __builtin_amdgcn_s_sleep(2);
-    }
-    __syncthreads();
-    const __amdgpu_buffer_rsrc_t xrs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.K * 2, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < XI; ++i) {
-      const int u = min(t + NT * i, n8 - 1);
-      const u32x4_t v = __builtin_amdgcn_raw_buffer_load_b128(xrs, u * 16, 0, 16);  // sc1
-      xr[i] = make_uint4(v.x, v.y, v.z, v.w);
-    }
-  }
 
   // 3. stage x into LDS (RMS-normalised when NORM) while the weights stream
   float rs = 1.0f;
@@ -222,17 +176,6 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
       xl[u] = xv;  // (x0,x4) (x1,x5) (x2,x6) (x3,x7) pairs (stage_x8)
       if ((u & 3) == 0) xsum[u >> 2] = cs;
     }
-    if (MOE2) {
-      const uint32_t d2[4] = {xr2[MOE2 ? i : 0].x, xr2[MOE2 ? i : 0].y, xr2[MOE2 ? i : 0].z, xr2[MOE2 ? i : 0].w};
-      uint4 xv2;
-      float cs2 = stage_x8<FMT>(d2, xv2);
-      cs2 += __shfl_xor(cs2, 1);
-      cs2 += __shfl_xor(cs2, 2);
-      if (u < n8) {
-        xl2[u] = xv2;
-        if ((u & 3) == 0) xsum2[u >> 2] = cs2;
-      }
-    }
   }
   __syncthreads();
   LGA_GTRACE_NOWAIT(3);
@@ -248,8 +191,8 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
     const int c = lane + 64 * j;
     const bool ok = c < NC;
     const int cc = min(c, NC - 1);
-    const uint4* xc = (MOE2 && slot ? xl2 : xl) + cc * 4;
-    const float xs = MOE2 && slot ? xsum2[cc] : xsum[cc];
+    const uint4* xc = xl + cc * 4;
+    const float xs = xsum[cc];
 #ifdef LGA_LAB_NOCOMPUTE  // lab builds only: cost of the dequant-dot (weights folded, not multiplied)
 #pragma unroll
     for (int i = 0; i < RPR; ++i) {
@@ -300,23 +243,6 @@ __device__ __forceinline__ void gemv_q4_body(GemvArgs a, int blk, unsigned char*
     const uint16_t ob = f2bf(__fmul_rn(g, round_bf(other)));  // * bf16(fc_2 x)
     if ((lane & (GROUP - 1)) == 0 && (vi & 1) == 0 && row < a.N) {
       a.y[row] = ob;
-    }
-    LGA_GTRACE(5);
-  } else if (MOE2) {
-    // the expert outputs as lga_q4_gemv_experts stores them (bf16), exchanged through LDS, then lga_moe_combine
-    uint16_t* ex = gemv_out_lds(smem, a.K);  // [slot][NW / 2 * RPR]
-    const int lr = (wave % (NW / 2)) * RPR + vi;
-    if ((lane & (GROUP - 1)) == 0) ex[slot * (NW / 2) * RPR + lr] = f2bf(tot);
-    __syncthreads();
-    const int row = row0 + vi;
-    if (slot == 0) {
-      const float e0 = bf2f(ex[lr]), e1 = bf2f(ex[(NW / 2) * RPR + lr]);
-      const float ea = a.moe_swap ? e1 : e0, eb = a.moe_swap ? e0 : e1;
-      float acc = 0.0f;
-      acc = round_bf(acc + round_bf(a.moe_pa * ea));
-      acc = round_bf(acc + round_bf(a.moe_pb * eb));
-      acc = __uint_as_float(((uint32_t)__shfl(res, vi)) << 16) + acc;
-      if ((lane & (GROUP - 1)) == 0 && row < a.N) a.y[row] = f2bf(acc);
     }
     LGA_GTRACE(5);
   } else {

@@ -116,73 +116,6 @@ __global__ void __launch_bounds__(256) moe_gate_route_kernel(GemvArgs a, int k, 
   if (threadIdx.x == 0) route_row(gemv_out_lds(smem, a.K), a.N, k, ids, probs, sq);
 }
 
-// Decode (one token, k = 2): the routed proj GEMVs of both experts and lga_moe_combine in ONE launch. A workgroup
-// computes its rows for both experts (each against its own SwiGLU input), so no partial leaves the workgroup before
-// the weighted sum: y = residual + bf16 sum in ascending expert id of bf16(p * expert_out), bit-identical to
-// lga_q4_gemv_experts + lga_moe_combine (the rows / chunks per lane are the ones lga_q4_gemv picks for the shape).
-template <int RPR, int CPT, int FMT, int NW = 16>
-__global__ void __launch_bounds__(NW * 64, NW == 8 ? 4 : 1) moe_down_combine_kernel(GemvArgs a,
-                                                                                 const int32_t* __restrict__ ids) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  const long long e0 = min(max(ids[0], 0), a.n_expert - 1), e1 = min(max(ids[1], 0), a.n_expert - 1);
-  a.moe_swap = ids[1] < ids[0];  // lga_moe_combine's stable order by expert id
-  // the probabilities are read here, with the ids (scalar loads), not after the GEMV (a dependent round trip there)
-  a.moe_pa = bf2f(a.probs[a.moe_swap ? 1 : 0]);
-  a.moe_pb = bf2f(a.probs[a.moe_swap ? 0 : 1]);
-  a.qw2 = a.qw + e1 * a.ew;
-  a.sc2 = (const unsigned char*)a.sc + e1 * a.es;
-  a.qw += e0 * a.ew;
-  a.sc = (const unsigned char*)a.sc + e0 * a.es;
-  gemv_q4_body<RPR, CPT, FMT, false, false, true, NW, false, true>(a, blockIdx.x, smem);
-}
-
-// Decode (one token, sparse-MoE block, no tensor parallelism): the attention out-projection + Block residual (the
-// lga_q4_gemv kernel the shape dispatches to: 4 waves x 4 rows, CPT chunks per lane) AND, in the workgroup that
-// arrives last, the router gate GEMV + top-k routing of the MLP that follows on the projection's output
-// (moe_gate_route_kernel's body and route_row, bit for bit) — one launch instead of two; the gate launch was pure
-// ramp (6.4 us for 16 KB of weights). Hand-off (MI355X_MICROARCH.md "Valid forms" row 1): every
-// workgroup stages its 16 bf16 rows in LDS, one wave stores them as two 16-B write-through (sc1) pieces and drains,
-// a workgroup barrier, one agent-scope add on the launch counter; the last arriver re-reads the whole row with sc1
-// loads (the XWAIT form of the body, its poll already satisfied) and re-arms the counter.
-template <int RPR, int CPT, int FMT, int GCPT>
-__global__ void __launch_bounds__(256) gemv_gate_route_kernel(GemvArgs a, GemvArgs gate, int k,
-                                                              int32_t* __restrict__ ids, uint16_t* __restrict__ probs,
-                                                              unsigned* __restrict__ counter) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ KV sq[8];
-  __shared__ unsigned s_ticket;
-  gemv_q4_body<RPR, CPT, FMT, false, false, true, 4, true>(a, blockIdx.x, smem);
-  __syncthreads();
-  if (threadIdx.x < 2) {  // the workgroup's 16 rows (N % 16 == 0: all real) as two 16-B sc1 stores
-    const __amdgpu_buffer_rsrc_t yrs =
-        __builtin_amdgcn_make_buffer_rsrc((void*)a.y, (short)0, a.N * 2, 0x00020000);
-    const uint4 v = ((const uint4*)gemv_out_lds(smem, a.K))[threadIdx.x];
-    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, v), yrs,
-                                           (blockIdx.x * 16 + threadIdx.x * 8) * 2, 0, 16);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) s_ticket = __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  if (s_ticket != gridDim.x - 1) return;
-  gate.x = a.y;
-  gate.xwait = counter;
-  gate.xwait_target = gridDim.x;  // every workgroup has arrived: the body's poll passes at once
-  gemv_q4_body<4, GCPT, FMT, false, true, false, 4, true, false, true>(gate, 0, smem);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    route_row(gemv_out_lds(smem, gate.K), gate.N, k, ids, probs, sq);
-    __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm for the next launch
-  }
-}
-
-template <int CPT, int GCPT, int FMT>
-static void launch_gemv_gate_route(const GemvArgs& a, const GemvArgs& gate, int k, int32_t* ids, uint16_t* probs,
-                                   unsigned* counter, hipStream_t stream) {
-  const size_t lds = gemv_lds_bytes(a.K) > gemv_lds_bytes(gate.K) ? gemv_lds_bytes(a.K) : gemv_lds_bytes(gate.K);
-  gemv_gate_route_kernel<4, CPT, FMT, GCPT><<<a.N / 16, 256, lds, stream>>>(a, gate, k, ids, probs, counter);
-}
-
 // Decode (one token, k = 2, no tensor parallelism): the routed proj GEMVs of both slots — lga_q4_gemv_experts's kernel
 // body for the shape, grid (row blocks, 2 slots), rows to LDS — and lga_moe_combine (+ the Block residual) in ONE
 // launch, the combine done by the second-arriving workgroup of each row block: the first stores its bf16 rows
@@ -266,74 +199,6 @@ static int dispatch_down_pair(const GemvArgs& a, const uint16_t* residual, uint1
   return 0;
 }
 
-template <int RPR, int CPT, int FMT>
-static void launch_down_combine(const GemvArgs& a, const int32_t* ids, hipStream_t stream) {
-  // 16 waves, 8 per expert: 8 * RPR rows per workgroup, one workgroup per CU (both inputs staged in LDS)
-  static const int nw = getenv("LGA_MOE_NW") ? atoi(getenv("LGA_MOE_NW")) : 16;  // lab A/B: 8 = two 8-wave workgroups per CU
-  if (nw == 8) {
-    moe_down_combine_kernel<RPR, CPT, FMT, 8><<<(a.N + 4 * RPR - 1) / (4 * RPR), 512, gemv_moe2_lds_bytes(a.K), stream>>>(a, ids);
-    return;
-  }
-  const int blocks = (a.N + 8 * RPR - 1) / (8 * RPR);
-  moe_down_combine_kernel<RPR, CPT, FMT><<<blocks, 1024, gemv_moe2_lds_bytes(a.K), stream>>>(a, ids);
-}
-
-template <int FMT>
-static int dispatch_down_combine(const GemvArgs& a, const int32_t* ids, hipStream_t stream) {
-  switch ((a.K / 32 + 63) / 64) {  // gemv.hip dispatch's (rows per wave, chunks per lane) for one-expert rows < 24000
-    case 1: launch_down_combine<4, 1, FMT>(a, ids, stream); break;
-    case 2: launch_down_combine<4, 2, FMT>(a, ids, stream); break;
-    case 3: launch_down_combine<4, 3, FMT>(a, ids, stream); break;
-    case 4: launch_down_combine<2, 4, FMT>(a, ids, stream); break;
-    case 5:
-    case 6: launch_down_combine<2, 6, FMT>(a, ids, stream); break;
-    case 7:
-    case 8: launch_down_combine<2, 8, FMT>(a, ids, stream); break;
-    default:
-      lga_set_error("lga_q4_gemv_experts_combine: K must be at most 16384");
-      return (int)hipErrorInvalidValue;
-  }
-  return 0;
-}
-
-// Decode (one token, sparse MoE, no tensor parallelism): the router gate + top-k routing AND the routed fc_1 || fc_2
-// + SwiGLU GEMVs in ONE launch. Every workgroup first runs moe_gate_route_kernel's body (the gate rows with fused
-// RMSNorm, the lga_q4_gemv tile, then route_row) on its own — the same arithmetic on the same inputs, so every
-// workgroup derives the same routing — and then its rows of the routed GEMV (lga_q4_gemv_swiglu_experts's body for
-// the shape) for the expert of its slot; workgroup (0, 0) also writes the routing for the routed proj launch. The
-// gate's 16 KB of weights are read by every workgroup (L2 hits after the first); the expert weights can only be
-// requested once the routing is known, which is the trade against the gate's own launch.
-template <int RPR, int CPT, int GCPT, int FMT>
-__global__ void __launch_bounds__(256) moe_gate_fc_kernel(GemvArgs g, GemvArgs a, int k, int32_t* __restrict__ ids,
-                                                          uint16_t* __restrict__ probs) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ KV sq[8];
-  __shared__ int32_t s_ids[8];
-  __shared__ uint16_t s_probs[8];
-  gemv_q4_body<4, GCPT, FMT, false, true, false, 4, true>(g, 0, smem);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    route_row(gemv_out_lds(smem, g.K), g.N, k, s_ids, s_probs, sq);
-    if (blockIdx.x == 0 && blockIdx.y == 0)
-      for (int s = 0; s < k; ++s) {
-        ids[s] = s_ids[s];
-        probs[s] = s_probs[s];
-      }
-  }
-  __syncthreads();
-  a.eidx = s_ids;  // read through a generic pointer by the body (LDS)
-  gemv_q4_body<RPR, CPT, FMT, true, true, false>(a, blockIdx.x, smem);
-}
-
-template <int RPR, int CPT, int FMT>
-static void launch_gate_fc(const GemvArgs& g, const GemvArgs& a, int k, int32_t* ids, uint16_t* probs,
-                           hipStream_t stream) {
-  const int waves = (a.N + RPR - 1) / RPR;
-  const dim3 grid((waves + 3) / 4, k);
-  const size_t lds = gemv_lds_bytes(a.K);
-  moe_gate_fc_kernel<RPR, CPT, CPT, FMT><<<grid, 256, lds, stream>>>(g, a, k, ids, probs);
-}
-
 template <int CPT, int FMT>
 static void launch_gate_route(const GemvArgs& a, int k, int32_t* ids, uint16_t* probs, hipStream_t stream) {
   const size_t lds = gemv_lds_bytes(a.K);
@@ -412,52 +277,6 @@ extern "C" int lga_moe_route(const void* logits, int T, int n_expert, int k, int
   LGA_LAUNCH_RETURN();
 }
 
-extern "C" int lga_q4_gemv_gate_route_supported(int N, int K, int group, int fmt, int n_expert, int k, int gate_group,
-                                                int gate_fmt) {
-  // the gate's input is the projection's output: its K is N
-  return N > 0 && N % 32 == 0 && N <= 6144 && K > 0 && K % 32 == 0 && K <= 6144 && group >= 32 && group % 32 == 0 &&
-         K % group == 0 && gate_group >= 32 && gate_group % 32 == 0 && N % gate_group == 0 &&
-         (fmt == 0 || fmt == 1 || fmt == 3) && lga::kernel_fmt(gate_fmt) == lga::kernel_fmt(fmt) &&
-         (gate_fmt == 0 || gate_fmt == 1 || gate_fmt == 3) && n_expert >= 1 && n_expert <= 8 && k >= 1 &&
-         k <= n_expert && (long long)N / 16 <= 65535;
-}
-
-extern "C" int lga_q4_gemv_gate_route(const void* x, const uint8_t* qweight, const void* scales, const void* residual,
-                                      void* y, int N, int K, int group, int fmt, const uint8_t* gate_qweight,
-                                      const void* gate_scales, int gate_group, int gate_fmt, const void* norm_weight,
-                                      float norm_eps, int n_expert, int k, int32_t* expert_ids, void* probs,
-                                      unsigned* counter, hipStream_t stream) {
-  LGA_CHECK_ARG(x && qweight && scales && residual && y && gate_qweight && gate_scales && norm_weight && expert_ids &&
-                    probs && counter,
-                "lga_q4_gemv_gate_route: null pointer");
-  LGA_CHECK_ARG(lga_q4_gemv_gate_route_supported(N, K, group, fmt, n_expert, k, gate_group, gate_fmt),
-                "lga_q4_gemv_gate_route: geometry not covered (lga_q4_gemv_gate_route_supported)");
-  lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, nullptr, (const uint16_t*)residual, nullptr,
-                  (uint16_t*)y, N, K, group, 0.0f};
-  a.cb = lga::codebook_of(fmt);
-  lga::GemvArgs g{(const uint16_t*)y, gate_qweight, gate_scales, nullptr, nullptr, nullptr, nullptr,
-                  (const uint16_t*)norm_weight, nullptr, n_expert, N, gate_group, norm_eps};
-  g.cb = lga::codebook_of(gate_fmt);
-  const int cpt = (K / 32 + 63) / 64, gcpt = (N / 32 + 63) / 64, kf = lga::kernel_fmt(fmt);
-#define LGA_GG(CPT, GCPT)                                                                                             \
-  do {                                                                                                                \
-    if (kf == 0) lga::launch_gemv_gate_route<CPT, GCPT, 0>(a, g, k, expert_ids, (uint16_t*)probs, counter, stream);  \
-    else lga::launch_gemv_gate_route<CPT, GCPT, 1>(a, g, k, expert_ids, (uint16_t*)probs, counter, stream);          \
-  } while (0)
-#define LGA_GG_K(CPT)            \
-  do {                           \
-    if (gcpt == 1) LGA_GG(CPT, 1); \
-    else if (gcpt == 2) LGA_GG(CPT, 2); \
-    else LGA_GG(CPT, 3);         \
-  } while (0)
-  if (cpt == 1) LGA_GG_K(1);
-  else if (cpt == 2) LGA_GG_K(2);
-  else LGA_GG_K(3);
-#undef LGA_GG_K
-#undef LGA_GG
-  LGA_LAUNCH_RETURN();
-}
-
 extern "C" int lga_moe_gate_route(const void* x, const uint8_t* qweight, const void* scales, const void* norm_weight,
                                   float norm_eps, int n_expert, int K, int group, int fmt, int k, int32_t* expert_ids,
                                   void* probs, hipStream_t stream) {
@@ -472,28 +291,6 @@ extern "C" int lga_moe_gate_route(const void* x, const uint8_t* qweight, const v
   a.cb = lga::codebook_of(fmt);
   const int rc = fmt == 0 ? lga::dispatch_gate_route<0>(a, k, expert_ids, (uint16_t*)probs, stream)
                           : lga::dispatch_gate_route<1>(a, k, expert_ids, (uint16_t*)probs, stream);
-  if (rc) return rc;
-  LGA_LAUNCH_RETURN();
-}
-
-extern "C" int lga_q4_gemv_experts_combine(const void* x, const uint8_t* qweight, const void* scales,
-                                           const int32_t* expert_ids, const void* probs, const void* residual,
-                                           int n_expert, long long w_stride, long long s_stride, void* y, int N, int K,
-                                           int group, int fmt, hipStream_t stream) {
-  LGA_CHECK_ARG(x && qweight && scales && expert_ids && probs && residual && y,
-                "lga_q4_gemv_experts_combine: null pointer");
-  LGA_CHECK_ARG(N > 0 && N < 24000 && K > 0 && K % 32 == 0 && K <= 16384,
-                "lga_q4_gemv_experts_combine: needs N < 24000 and K a multiple of 32, at most 16384");
-  LGA_CHECK_ARG(group >= 32 && group % 32 == 0 && K % group == 0, "lga_q4_gemv_experts_combine: bad group");
-  LGA_CHECK_ARG(fmt == 0 || fmt == 1 || fmt == 3, "lga_q4_gemv_experts_combine: fmt must be 0, 1 or 3");
-  LGA_CHECK_ARG(n_expert > 0 && w_stride >= (long long)N * K / 2 && s_stride > 0,
-                "lga_q4_gemv_experts_combine: bad expert geometry");
-  lga::GemvArgs a{(const uint16_t*)x, qweight, scales, nullptr, nullptr, nullptr, (const uint16_t*)residual, nullptr,
-                  (uint16_t*)y, N, K, group, 0.0f, nullptr, w_stride, s_stride, K, n_expert, 2};
-  a.cb = lga::codebook_of(fmt);
-  a.probs = (const uint16_t*)probs;
-  const int rc = fmt == 0 ? lga::dispatch_down_combine<0>(a, expert_ids, stream)
-                          : lga::dispatch_down_combine<1>(a, expert_ids, stream);
   if (rc) return rc;
   LGA_LAUNCH_RETURN();
 }
@@ -527,53 +324,6 @@ extern "C" int lga_q4_gemv_experts_pair_combine(const void* x, const uint8_t* qw
                      : lga::dispatch_down_pair<1>(a, (const uint16_t*)residual, (uint16_t*)y, (uint16_t*)scratch,
                                                   counters, stream);
   if (rc) return rc;
-  LGA_LAUNCH_RETURN();
-}
-
-extern "C" int lga_moe_gate_fc_supported(int n_expert, int k, int N, int K, int group, int gate_group, int fmt,
-                                         int gate_fmt) {
-  return n_expert >= 1 && n_expert <= 8 && k >= 1 && k <= n_expert && N > 0 && K > 0 && K % 32 == 0 && K <= 4096 &&
-         group >= 32 && group % 32 == 0 && K % group == 0 && gate_group >= 32 && gate_group % 32 == 0 &&
-         K % gate_group == 0 && (fmt == 0 || fmt == 1 || fmt == 3) && (gate_fmt == 0 || gate_fmt == 1 || gate_fmt == 3) &&
-         lga::kernel_fmt(fmt) == lga::kernel_fmt(gate_fmt);
-}
-
-extern "C" int lga_moe_gate_fc(const void* x, const void* norm_weight, float norm_eps, const uint8_t* gate_qweight,
-                               const void* gate_scales, int gate_group, int gate_fmt, int n_expert, int k,
-                               const uint8_t* qweight1, const void* scales1, const uint8_t* qweight2,
-                               const void* scales2, long long w_stride, long long s_stride, int n_expert_stack, void* y,
-                               int N, int K, int group, int fmt, int32_t* expert_ids, void* probs,
-                               hipStream_t stream) {
-  LGA_CHECK_ARG(x && norm_weight && gate_qweight && gate_scales && qweight1 && scales1 && qweight2 && scales2 && y &&
-                    expert_ids && probs,
-                "lga_moe_gate_fc: null pointer");
-  LGA_CHECK_ARG(lga_moe_gate_fc_supported(n_expert, k, N, K, group, gate_group, fmt, gate_fmt),
-                "lga_moe_gate_fc: geometry not covered (lga_moe_gate_fc_supported)");
-  LGA_CHECK_ARG(n_expert_stack >= n_expert && w_stride >= (long long)N * K / 2 && s_stride > 0,
-                "lga_moe_gate_fc: bad expert geometry");
-  lga::GemvArgs g{(const uint16_t*)x, gate_qweight, gate_scales, nullptr, nullptr, nullptr, nullptr,
-                  (const uint16_t*)norm_weight, nullptr, n_expert, K, gate_group, norm_eps};
-  g.cb = lga::codebook_of(gate_fmt);
-  lga::GemvArgs a{(const uint16_t*)x, qweight1, scales1, qweight2, scales2, nullptr, nullptr,
-                  (const uint16_t*)norm_weight, (uint16_t*)y, N, K, group, norm_eps, nullptr, w_stride, s_stride, 0,
-                  n_expert_stack, k};
-  a.cb = lga::codebook_of(fmt);
-  // lga_q4_gemv_swiglu_experts's tile (gemv.hip dispatch, variant < 0): 2N rows >= 24000 -> 4 rows per wave, else 2
-  const int cpt = (K / 32 + 63) / 64, kf = lga::kernel_fmt(fmt);
-  const bool big = 2L * N >= 24000;
-#define LGA_GF(RPR, CPT)                                                                            \
-  do {                                                                                              \
-    if (kf == 0) lga::launch_gate_fc<RPR, CPT, 0>(g, a, k, expert_ids, (uint16_t*)probs, stream);   \
-    else lga::launch_gate_fc<RPR, CPT, 1>(g, a, k, expert_ids, (uint16_t*)probs, stream);           \
-  } while (0)
-  if (cpt == 1) {
-    if (big) LGA_GF(4, 1);
-    else LGA_GF(2, 1);
-  } else {
-    if (big) LGA_GF(4, 2);
-    else LGA_GF(2, 2);
-  }
-#undef LGA_GF
   LGA_LAUNCH_RETURN();
 }
 
@@ -657,5 +407,5 @@ extern "C" int lga_moe_group(const int32_t* expert_ids, int T, int k, int n_expe
 int lga::preload_moe() {  // the sparse-MoE prefill's routing, grouping and combine kernels
   return lga::preload(lga::moe_route_kernel) + lga::preload(lga::moe_combine_kernel) +
          lga::preload(lga::moe_group_kernel) + lga::preload(lga::moe_gate_route_kernel<2, 0, true>) +
-         lga::preload(lga::moe_gate_route_kernel<2, 1, true>) + lga::preload(lga::moe_down_combine_kernel<2, 8, 0>);
+         lga::preload(lga::moe_gate_route_kernel<2, 1, true>) + lga::preload(lga::moe_down_pair_kernel<2, 8, 0>);
 }

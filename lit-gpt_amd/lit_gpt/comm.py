@@ -29,6 +29,9 @@ _default: Optional["XgmiAllReduce"] = None
 fallback_reason: Optional[str] = None  # why init_distributed fell back to RCCL (None: it did not)
 
 
+# lga_comm_trace's device buffer: allocated once per process and never freed (graphs may hold its pointer)
+_TRACE_BUF = None
+
 class XgmiUnavailable(RuntimeError):
     """Raised on EVERY rank (the outcome is agreed over the group) when the peer mailboxes cannot be mapped or the
     start-up self-test of the one-shot all-reduce fails."""
@@ -200,9 +203,17 @@ class XgmiAllReduce:
     def enable_trace(self, n_records: int = 256) -> None:
         """Diagnostics (lga_comm_trace): every later all-reduce launch of this process records its call — entry,
         flags-raised and wait-done times, timeout, the peers' flag words seen — in a device buffer (``traces()``).
-        Process-wide; install it before capturing graphs that should record."""
-        self._trace = torch.zeros(n_records, 16, dtype=torch.int64, device=self.device)
-        ops._check(ops.load_library().lga_comm_trace(self._trace.data_ptr(), n_records))
+        Process-wide; install it before capturing graphs that should record. Graphs captured with tracing on keep its
+        device pointer, so the buffer lives for the rest of the process: a second call (or one after ``close()``)
+        re-installs the same buffer instead of freeing it under such graphs; asking for more records raises."""
+        global _TRACE_BUF
+        if _TRACE_BUF is None:
+            _TRACE_BUF = torch.zeros(n_records, 16, dtype=torch.int64, device=self.device)
+        elif _TRACE_BUF.size(0) < n_records or _TRACE_BUF.device != torch.device(self.device):
+            raise ValueError("enable_trace: the process-wide trace buffer exists with fewer records or on another "
+                             "device; it cannot be replaced while captured graphs may still write into it")
+        self._trace = _TRACE_BUF
+        ops._check(ops.load_library().lga_comm_trace(self._trace.data_ptr(), self._trace.size(0)))
 
     def traces(self):
         """The recorded calls as a (n, 16) int64 numpy array (rows of calls not made are zero); syncs."""
@@ -222,7 +233,7 @@ class XgmiAllReduce:
         lib = ops.load_library()
         torch.cuda.synchronize(self.device)
         if getattr(self, "_trace", None) is not None:
-            lib.lga_comm_trace(None, 0)
+            lib.lga_comm_trace(None, 0)  # later launches stop recording; _TRACE_BUF itself stays alive (enable_trace)
             self._trace = None
         self._mailboxes = None
         for p in self._opened:

@@ -258,21 +258,12 @@ class Block(nn.Module):
 
         ha = comm.tp_hook(self.attn)
         hm = comm.tp_hook(self.mlp)
-        # a decode token of a sparse-MoE block: the router gate + routing ride the attention's out-projection launch
-        # (ops.q4_gemv_gate_route) when it covers the pair; the MLP then starts from the routing it left
-        route = None
-        if (ha is None and hm is None and x.size(1) == 1 and input_pos is not None and isinstance(self.mlp, LLaMAMoE)
-                and not self.attn._forward_hooks and not self.mlp._forward_hooks):
-            route = self.mlp.gate_route_request(self.norm_2, x.size(-1))
         if ha is not None:
             x = self.attn.forward(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x, reduce=ha)
         elif not self.attn._forward_hooks:
-            x = self.attn(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x, route=route)
+            x = self.attn(x, cos, sin, mask, input_pos, norm=self.norm_1, residual=x)
         else:
             x = ops.add(self.attn(self.norm_1(x), cos, sin, mask, input_pos).contiguous(), x.contiguous())
-        if route is not None and route.done:
-            route.done = False
-            return self.mlp(x, norm=self.norm_2, residual=x, routed=route)
         if hm is not None and isinstance(self.mlp, LLaMAMLP):
             return self.mlp.forward(x, norm=self.norm_2, residual=x, reduce=hm)
         if hm is not None:
@@ -309,25 +300,16 @@ class CausalSelfAttention(nn.Module):
     # decode tokens (T = 1) with full 128-dim rotary use lga_attention_decode_fused; False keeps the two-launch
     # rope_kv_append + attention path (bit-identical; tests compare the two)
     fuse_decode = True
-    # ... and the decode out-projection + residual inside that launch (lga_attention_decode_proj) where it covers the
-    # geometry: bit-identical to the separate proj GEMV launch, but measured slower (16.5 vs 15.6 us per block,
-    # DESIGN.md §8b), so it is opt-in (LGA_FUSE_PROJ=1); tests compare the two
-    fuse_proj = os.environ.get("LGA_FUSE_PROJ", "0") == "1"
 
     def forward(self, x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor, mask: Optional[torch.Tensor] = None,
                 input_pos: Optional[torch.Tensor] = None, *, norm: Optional["RMSNorm"] = None,
-                residual: Optional[torch.Tensor] = None, reduce=None, route=None) -> torch.Tensor:
-        """``norm`` / ``residual`` / ``reduce`` / ``route`` are fusion hooks used by Block.forward: the RMSNorm runs in
-        the qkv GEMV prologue, the residual add (and under TP the all-reduce hook ``reduce``) in the proj epilogue, and
-        a following sparse-MoE's gate + routing (``route``, LLaMAMoE.gate_route_request) in the proj launch. Without
+                residual: Optional[torch.Tensor] = None, reduce=None) -> torch.Tensor:
+        """``norm`` / ``residual`` / ``reduce`` are fusion hooks used by Block.forward: the RMSNorm runs in the qkv
+        GEMV prologue, the residual add (and under TP the all-reduce hook ``reduce``) in the proj epilogue. Without
         them this is the reference forward."""
         B, T, C = x.size()
         c = self.config
         H, G, hs = c.n_head, c.n_query_groups, c.head_size
-        if T == 1 and input_pos is not None and norm is not None and self.fuse_qkv:
-            y = self._qkv_attention_decode(x, cos, sin, input_pos, norm)
-            if y is not None:
-                return self._proj_out(y.view(1, T, H * hs), residual, reduce, route).view(B, T, -1)
         qkv = _lin(self.attn, x, norm_weight=None if norm is None else norm.weight,
                    norm_eps=c.norm_eps if norm is None else norm.eps).view(T, -1)
         dev = x.device
@@ -359,66 +341,14 @@ class CausalSelfAttention(nn.Module):
             if ws is None or ws.key != (1, H, G, hs, n_splits) or ws.counters.device != dev:
                 ws = self._attn_ws = ops.AttentionWorkspace(1, H, G, hs, n_splits, dev)
         if T == 1 and self.fuse_decode and ops.decode_fusable(hs, c.rope_n_elem) and qkv.dtype == torch.bfloat16:
-            if (self.fuse_proj and reduce is None and residual is not None and not self.proj._forward_hooks
-                    and ops.decode_proj_supported(H, G, hs, n_splits, self.proj)):
-                # decode token: RoPE + KV-append + attention + out-projection + residual in a single launch
-                out, _ = ops.attention_decode_proj(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem,
-                                                   1.0 / math.sqrt(hs), n_splits, ws, self.proj,
-                                                   residual.reshape(1, -1).contiguous())
-                return out.view(B, T, -1)
             # decode token: RoPE + KV-append + attention in a single launch
             y = ops.attention_decode_fused(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem,
                                            1.0 / math.sqrt(hs), n_splits, workspace=ws)
         else:
             q = ops.rope_kv_append(qkv, kc, vc, pos, rope_pos, cos, sin, H, G, hs, c.rope_n_elem)
             y = ops.attention(q, kc, vc, pos, H, G, hs, 1.0 / math.sqrt(hs), n_splits, workspace=ws)
-        out = self._proj_out(y.view(1, T, H * hs), residual, reduce, route)
+        out = _lin(self.proj, y.view(1, T, H * hs), residual=residual, reduce=reduce)
         return out.view(B, T, -1)
-
-    def _proj_out(self, y: torch.Tensor, residual, reduce, route) -> torch.Tensor:
-        """The out-projection (+ residual / TP reduce); with ``route`` (one token, no reduce) the next MoE's gate and
-        routing in the same launch (ops.q4_gemv_gate_route: y and the routing bit-identical to the two launches)."""
-        if route is not None and route.proj_ok is None:
-            route.proj_ok = ops.gemv_gate_route_supported(self.proj, route.gate, route.k)
-        if (route is not None and route.proj_ok and reduce is None and residual is not None
-                and not self.proj._forward_hooks):
-            out = ops.q4_gemv_gate_route(y.reshape(-1).contiguous(), self.proj, residual.reshape(-1).contiguous(),
-                                         route.gate, route.norm.weight, route.norm.eps, route.k, route.ws)
-            route.done = True
-            return out.view(1, 1, -1)
-        return _lin(self.proj, y, residual=residual, reduce=reduce)
-
-    # opt-in (LGA_FUSE_QKV=1): decode tokens of the geometry csrc/qkv_attention.hip covers (Llama-2-7B at TP = 1)
-    # run RMSNorm + qkv GEMV + RoPE + KV append + attention as ONE launch (ops.qkv_attention_decode); q, k, v are
-    # bit-identical, y within fp32 order. Off by default: measured 28 us per block against 19.3 us for the qkv GEMV
-    # launch + lga_attention_decode_fused (tools/qkv_attn_ab.py, round 5; csrc/qkv_attention.hip STATUS)
-    fuse_qkv = os.environ.get("LGA_FUSE_QKV", "0") == "1"
-
-    def _qkv_attention_decode(self, x, cos, sin, input_pos, norm) -> Optional[torch.Tensor]:
-        """The fused decode launch when it covers this step, else None (the caller runs the two launches)."""
-        c = self.config
-        H, G, hs = c.n_head, c.n_query_groups, c.head_size
-        kv = self.kv_cache
-        if (not isinstance(kv, KVCache) or self.attn._forward_hooks or not self.fuse_decode
-                or not ops.decode_fusable(hs, c.rope_n_elem) or x.dtype != torch.bfloat16 or not x.is_cuda
-                or kv.k.dtype != torch.bfloat16 or cos.size(0) == 1):
-            return None
-        S = kv.k.size(-2)
-        n_splits = ops.decode_splits(G, H // G, hs, S)
-        if not ops.qkv_attention_supported(c.n_embd, H, G, hs, n_splits, self.attn):
-            return None
-        dev = x.device
-        ws = getattr(self, "_attn_ws", None)
-        if ws is None or ws.key != (1, H, G, hs, n_splits) or ws.counters.device != dev:
-            ws = self._attn_ws = ops.AttentionWorkspace(1, H, G, hs, n_splits, dev)
-        scratch = getattr(self, "_qkv_scratch", None)
-        if scratch is None or scratch.device != dev:
-            scratch = self._qkv_scratch = torch.empty((H + 2 * G) * hs, dtype=torch.bfloat16, device=dev)
-        pos = input_pos.to(device=dev, dtype=torch.int64)
-        return ops.qkv_attention_decode(x, norm.weight, norm.eps, self.attn, kv.k, kv.v, pos, pos,
-                                        cos.to(device=dev, dtype=torch.float32).contiguous(),
-                                        sin.to(device=dev, dtype=torch.float32).contiguous(), H, G, hs,
-                                        1.0 / math.sqrt(hs), n_splits, ws, scratch)
 
     def scaled_dot_product_attention(self, q: torch.Tensor, k: torch.Tensor, v: torch.Tensor,
                                      mask: Optional[torch.Tensor] = None) -> torch.Tensor:
@@ -516,27 +446,10 @@ class LLaMAMLP(nn.Module):
 # decode routing through the fused gate + route launch (lga_moe_gate_route); False keeps lga_q4_gemv + lga_moe_route
 # (tests A/B the two)
 moe_gate_route = True
-# decode k = 2: routed proj GEMVs + combine in one launch (lga_q4_gemv_experts_combine) — off by default: bit-identical
-# but slower on MI355X (Mixtral bench 443.6 vs 452.6-454.0 tok/s A/B on one box); tests A/B the two
-moe_fused_combine = os.environ.get("LGA_MOE_FUSED_COMBINE", "0") == "1"
 # one-token sparse-MoE: the routed proj GEMVs of both slots + the combine + residual in one launch whose second-arriving
 # workgroup per row block combines (lga_q4_gemv_experts_pair_combine, bit-identical to the two launches); False keeps
 # lga_q4_gemv_experts + lga_moe_combine
 moe_pair_combine = os.environ.get("LGA_MOE_PAIR_COMBINE", "1") != "0"
-# opt-in (LGA_MOE_GATE_FC=1): the gate + routing folded into the routed fc_1 || fc_2 launch (lga_moe_gate_fc: every
-# workgroup derives the routing itself; bit-identical). Off by default: Mixtral decode 2.270-2.273 vs 2.087-2.088 ms
-# per step (round 5) — every workgroup's gate prologue holds back its expert weight stream
-moe_gate_fc = os.environ.get("LGA_MOE_GATE_FC", "0") == "1"
-
-
-class _RouteRequest:
-    """LLaMAMoE.gate_route_request's hook object: the gate, the norm it fuses, k, the routing outputs; ``done`` is
-    set by the attention when its out-projection launch produced the routing for this token."""
-
-    def __init__(self, gate, norm, k, ws) -> None:
-        self.gate, self.norm, self.k, self.ws = gate, norm, k, ws
-        self.done = False
-        self.proj_ok = None
 
 
 class LLaMAMoE(nn.Module):
@@ -602,24 +515,6 @@ class LLaMAMoE(nn.Module):
         return (moe_gate_route and isinstance(g, QuantLinear) and g.bias is None and not g._forward_hooks
                 and g.in_features == C and ops.moe_gate_route_fits(g.out_features, C))
 
-    # opt-in (LGA_FOLD_GATE=1): the router gate + routing of a decode token inside the preceding out-projection
-    # launch (Block.forward, ops.q4_gemv_gate_route; bit-identical, tests compare). Off by default: Mixtral decode
-    # 2.284-2.291 vs 2.216-2.218 ms per step on one box (round 5) — the last-arriving workgroup's serial gate GEMV
-    # (cold gate weights, sc1 re-read of the row) + routing cost more than the gate launch's ramp saved
-    fold_gate = os.environ.get("LGA_FOLD_GATE", "0") == "1"
-
-    def gate_route_request(self, norm, C: int):
-        """A ``route`` hook for CausalSelfAttention.forward when the gate + routing can ride the out-projection
-        launch (the gate would otherwise run as lga_moe_gate_route with norm_2 fused), else None."""
-        if not (self.fold_gate and isinstance(norm, RMSNorm) and ops.gemv_fuses_norm(C, dual=True)
-                and self._gate_route_ok(C)):
-            return None
-        k = self.config.n_expert_per_token
-        req = getattr(self, "_route_req", None)
-        if req is None or req.norm is not norm or req.ws.ids.device != self.gate.qweight.device:
-            req = self._route_req = _RouteRequest(self.gate, norm, k, ops.GateRouteWorkspace(k, self.gate.qweight.device))
-        return req if req.proj_ok is not False else None
-
     def _expert_hooks(self, x: torch.Tensor, eout: torch.Tensor) -> torch.Tensor:
         hooks = [list(e._forward_hooks.values()) for e in self.experts]
         if any(len(h) != len(hooks[0]) for h in hooks):
@@ -630,9 +525,9 @@ class LLaMAMoE(nn.Module):
         return eout
 
     def forward(self, x: torch.Tensor, *, norm: Optional["RMSNorm"] = None,
-                residual: Optional[torch.Tensor] = None, routed=None) -> torch.Tensor:
-        """``routed``: the routing of this decode token already computed by the out-projection launch
-        (gate_route_request)."""
+                residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``norm`` / ``residual``: Block fusion hooks (norm_2 in the gate / fc GEMV prologues, the residual in the
+        combine)."""
         c = self.config
         lead, C = x.shape[:-1], x.shape[-1]
         x2 = x.reshape(-1, C).contiguous()
@@ -645,30 +540,15 @@ class LLaMAMoE(nn.Module):
             xin = x2 if (norm is None or fuse_norm) else norm(x2)
             nw = norm.weight if fuse_norm else None
             eps = norm.eps if fuse_norm else 1e-5
-            act = None
-            if routed is not None:  # computed inside the attention's out-projection launch (same bits)
-                ids, probs = routed.ws.ids, routed.ws.probs
-            elif (moe_gate_fc and nw is not None and self._gate_route_ok(C)
-                  and ops.moe_gate_fc_supported(self.gate, f1, k)):
-                # gate + routing + the routed fc_1 || fc_2 + SwiGLU GEMVs in one launch (same bits as the three below)
-                g = self.gate
-                act, ids, probs = ops.moe_gate_fc(xin.view(-1), nw, eps, g, q1, s1, q2, s2, f1.out_features, C,
-                                                  f1.group, f1.fmt, k)
-            elif self._gate_route_ok(C):  # gate GEMV + routing in one launch (same bits as the pair below)
+            if self._gate_route_ok(C):  # gate GEMV + routing in one launch (same bits as the pair below)
                 g = self.gate
                 ids, probs = ops.moe_gate_route(xin.view(-1), g.qweight, g.scales, E, C, g.group, g.fmt, k,
                                                 norm_weight=nw, eps=eps)
             else:
                 router = _lin(self.gate, xin, norm_weight=nw, norm_eps=eps).view(1, E)
                 ids, probs = ops.moe_route(router, k)
-            if act is None:
-                act = ops.q4_gemv_swiglu_experts(xin.view(-1), q1, s1, q2, s2, ids.view(-1), f1.out_features, C,
-                                                 f1.group, f1.fmt, norm_weight=nw, eps=eps)
-            if (moe_fused_combine and res is not None and not any(e._forward_hooks for e in self.experts)
-                    and ops.q4_gemv_experts_combine_fits(k, pj.out_features, pj.in_features)):
-                # the routed proj GEMVs and the combine (+ residual) in one launch, same bits as the three below
-                return ops.q4_gemv_experts_combine(act, qp, sp, ids.view(-1), probs.view(-1), res.view(-1),
-                                                   pj.out_features, pj.in_features, pj.group, pj.fmt).view(*lead, C)
+            act = ops.q4_gemv_swiglu_experts(xin.view(-1), q1, s1, q2, s2, ids.view(-1), f1.out_features, C,
+                                             f1.group, f1.fmt, norm_weight=nw, eps=eps)
             if (moe_pair_combine and res is not None and k == 2 and not any(e._forward_hooks for e in self.experts)
                     and ops.experts_pair_supported(pj.out_features, pj.in_features, pj.group, pj.fmt)):
                 pw = getattr(self, "_pair_ws", None)

@@ -62,29 +62,16 @@ SIGNATURES = {
     "lga_attention": [_P, _P, _P, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
     "lga_attention_workspace_bytes": [_I, _I, _I, _I],
     "lga_attention_decode_fused": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P],
-    "lga_qkv_attention_supported": [_I, _I, _I, _I, _I, _I, _I],
-    "lga_qkv_attention_decode": [_P, _P, _F, _P, _P, _P, _I, _I, _P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I,
-                                 _I, _I, _I, _I, _F, _P],
-    "lga_attention_decode_proj_supported": [_I, _I, _I, _I, _I, _I, _I, _I],
-    "lga_attention_decode_proj": [_P, _P, _P, _P, _P, _P, _P, _I, _P, _P, _P, _P, _I, _I, _I, _I, _I, _I, _F, _P, _P,
-                                  _P, _P, _P, _I, _I, _I, _P],
     "lga_argmax": [_P, _I, _P, _P, _P, _P],
     "lga_q4_gemv_argmax_work_bytes": [_I, _I],
     "lga_q4_gemv_argmax_embed": [_P, _P, _P, _P, _F, _P, _I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _I, _P, _P],
     "lga_argmax_embed": [_P, _I, _P, _P, _P, _P, _I, _I, _P, _P],
     "lga_moe_route": [_P, _I, _I, _I, _P, _P, _P],
     "lga_moe_gate_route": [_P, _P, _P, _P, _F, _I, _I, _I, _I, _I, _P, _P, _P],
-    "lga_q4_gemv_gate_route_supported": [_I, _I, _I, _I, _I, _I, _I, _I],
-    "lga_q4_gemv_gate_route": [_P, _P, _P, _P, _P, _I, _I, _I, _I, _P, _P, _I, _I, _P, _F, _I, _I, _P, _P, _P, _P],
-    "lga_moe_gate_fc_supported": [_I, _I, _I, _I, _I, _I, _I, _I],
-    "lga_moe_gate_fc": [_P, _P, _F, _P, _P, _I, _I, _I, _I, _P, _P, _P, _P, ctypes.c_longlong, ctypes.c_longlong, _I,
-                        _P, _I, _I, _I, _I, _P, _P, _P],
     "lga_q4_gemv_experts_pair_supported": [_I, _I, _I, _I],
     "lga_q4_gemv_experts_pair_counters": [_I],
     "lga_q4_gemv_experts_pair_combine": [_P, _P, _P, _P, _P, _P, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _P,
                                          _P, _I, _I, _I, _I, _P],
-    "lga_q4_gemv_experts_combine": [_P, _P, _P, _P, _P, _P, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _I, _I, _I,
-                                    _I, _P],
     "lga_q4_gemv_experts": [_P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _I, _P, _I, _I, _I, _I,
                             _I, _P],
     "lga_q4_gemv_swiglu_experts": [_P, _P, _P, _P, _P, _P, _I, _I, ctypes.c_longlong, ctypes.c_longlong, _P, _F,
@@ -368,10 +355,6 @@ class AttentionWorkspace:
         # one counter per (row, query group, head slice): at most n_head of them per row (csrc/attention.hip
         # attn_hsplit deals a group's heads to up to q_per_kv workgroups when the groups are few)
         self.counters = torch.zeros(T * n_head * ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
-        # lga_attention_decode_proj's hand-off words (a monotonic counter and its per-launch base; never re-zeroed)
-        self.sync = torch.zeros(1024, dtype=torch.int32, device=device)
-        # lga_qkv_attention_decode's per-group row counters and their bases (monotonic; never re-zeroed)
-        self.group_sync = torch.zeros(2 * n_query_groups * ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
 
 
 def attention(q, k_cache, v_cache, input_pos, n_head, n_query_groups, head_size, scale, n_splits=1,
@@ -422,76 +405,6 @@ def attention_decode_fused(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin,
         cos.shape[0], _dev(y, "y", torch.bfloat16), ws, cnt, n_head, n_query_groups, head_size, rope_n_elem, max_seq,
         n_splits, float(scale), _stream()))
     return y
-
-
-def qkv_attention_supported(n_embd, n_head, n_query_groups, head_size, n_splits, lin) -> bool:
-    """Whether lga_qkv_attention_decode covers this decode step (the qkv Linear a 4-bit QuantLinear of the geometry
-    csrc/qkv_attention.hip is built for: Llama-2-7B at TP = 1)."""
-    from lit_gpt.quantize import QuantLinear
-
-    return (isinstance(lin, QuantLinear) and lin.in_features == n_embd
-            and lin.out_features == (n_head + 2 * n_query_groups) * head_size
-            and bool(load_library().lga_qkv_attention_supported(n_embd, n_head, n_query_groups, head_size, n_splits,
-                                                                 lin.group, lin.fmt)))
-
-
-def qkv_attention_decode(x, norm_weight, eps, lin, k_cache, v_cache, cache_pos, rope_pos, cos, sin, n_head,
-                         n_query_groups, head_size, scale, n_splits, workspace: AttentionWorkspace, qkv_scratch,
-                         out=None):
-    """One decode token's attention half in ONE launch: RMSNorm(x) -> qkv Linear (rows bit-identical to
-    ``q4_gemv(x, ..., norm_weight)``) -> RoPE -> KV append at cache_pos[0] -> attention over keys 0..p. Returns y
-    (1, H*hs); qkv_scratch (G*3*hs bf16) receives the qkv row."""
-    if workspace is None or workspace.key != (1, n_head, n_query_groups, head_size, n_splits):
-        raise ValueError("qkv_attention_decode needs the layer's AttentionWorkspace")
-    y = out if out is not None else torch.empty(1, n_head * head_size, dtype=torch.bfloat16, device=x.device)
-    _check(load_library().lga_qkv_attention_decode(
-        _dev(x.reshape(-1), "x", torch.bfloat16), _dev(norm_weight, "norm_weight", torch.bfloat16), float(eps),
-        _dev(lin.qweight, "qweight", torch.uint8), _dev(lin.scales, "scales"), _opt(lin.bias, "bias", torch.bfloat16),
-        lin.group, lin.fmt, _dev(qkv_scratch, "qkv_scratch", torch.bfloat16), _dev(k_cache, "k_cache", torch.bfloat16),
-        _dev(v_cache, "v_cache", torch.bfloat16), _dev(cache_pos, "cache_pos", torch.int64),
-        _dev(rope_pos, "rope_pos", torch.int64), _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32),
-        cos.shape[0], _dev(y, "y", torch.bfloat16), _dev(workspace.partials, "workspace", torch.float32),
-        _dev(workspace.counters, "counters", torch.int32), _dev(workspace.group_sync, "group_sync", torch.int32),
-        n_head, n_query_groups, head_size, k_cache.shape[-2], n_splits, float(scale), _stream()))
-    return y
-
-
-def decode_proj_supported(n_head, n_query_groups, head_size, n_splits, lin) -> bool:
-    """Whether lga_attention_decode_proj covers this decode step: a 4-bit ``QuantLinear`` out-projection of the
-    geometries the fused launch is built for (csrc/attention.hip proj_shape)."""
-    from lit_gpt.quantize import QuantLinear
-
-    if not isinstance(lin, QuantLinear) or lin.qweight.dtype != torch.uint8:
-        return False
-    return bool(load_library().lga_attention_decode_proj_supported(
-        n_head, n_query_groups, head_size, n_splits, lin.out_features, lin.in_features, lin.group, lin.fmt))
-
-
-def attention_decode_proj(qkv, k_cache, v_cache, cache_pos, rope_pos, cos, sin, n_head, n_query_groups, head_size,
-                          rope_n_elem, scale, n_splits, workspace: AttentionWorkspace, lin, residual, out=None,
-                          y=None):
-    """One decode token: RoPE + KV-append + attention + the 4-bit out-projection + residual in ONE launch (reference
-    model.py:656 and :591). Returns (out (1, N), y (1, H*hs)); out is bit-identical to
-    ``q4_gemv(y, ..., residual=residual)``."""
-    if qkv.shape[0] != 1:
-        raise ValueError("attention_decode_proj handles exactly one token (T = 1)")
-    if workspace is None or workspace.key != (1, n_head, n_query_groups, head_size, n_splits):
-        raise ValueError("attention_decode_proj needs the layer's AttentionWorkspace")
-    max_seq = k_cache.shape[-2]
-    N = lin.out_features
-    y = y if y is not None else torch.empty(1, n_head * head_size, dtype=torch.bfloat16, device=qkv.device)
-    out = out if out is not None else torch.empty(1, N, dtype=torch.bfloat16, device=qkv.device)
-    _check(load_library().lga_attention_decode_proj(
-        _dev(qkv, "qkv", torch.bfloat16), _dev(k_cache, "k_cache", torch.bfloat16),
-        _dev(v_cache, "v_cache", torch.bfloat16), _dev(cache_pos, "cache_pos", torch.int64),
-        _dev(rope_pos, "rope_pos", torch.int64), _dev(cos, "cos", torch.float32), _dev(sin, "sin", torch.float32),
-        cos.shape[0], _dev(y, "y", torch.bfloat16), _dev(workspace.partials, "workspace", torch.float32),
-        _dev(workspace.counters, "counters", torch.int32), _dev(workspace.sync, "sync", torch.int32), n_head,
-        n_query_groups, head_size, rope_n_elem, max_seq, n_splits, float(scale),
-        _dev(lin.qweight, "qweight", torch.uint8), _dev(lin.scales, "scales"), _opt(lin.bias, "bias", torch.bfloat16),
-        _dev(residual, "residual", torch.bfloat16), _dev(out, "out", torch.bfloat16), N, lin.group, lin.fmt,
-        _stream()))
-    return out, y
 
 
 class HeadWorkspace:
@@ -729,70 +642,6 @@ def moe_gate_route(x, qweight, scales, n_expert, K, group, fmt, k, *, norm_weigh
     return ids, probs
 
 
-def gemv_gate_route_supported(proj, gate, k: int) -> bool:
-    """Whether lga_q4_gemv_gate_route covers this (out-projection, router gate) pair: both bias-free 4-bit
-    QuantLinears of one kernel format, the projection's N a multiple of 16, K <= 6144, n_expert <= 8."""
-    from lit_gpt.quantize import QuantLinear
-
-    if not (isinstance(proj, QuantLinear) and isinstance(gate, QuantLinear) and proj.bias is None
-            and gate.bias is None and gate.in_features == proj.out_features):
-        return False
-    return bool(load_library().lga_q4_gemv_gate_route_supported(proj.out_features, proj.in_features, proj.group,
-                                                                 proj.fmt, gate.out_features, k, gate.group,
-                                                                 gate.fmt))
-
-
-class GateRouteWorkspace:
-    """Persistent outputs of lga_q4_gemv_gate_route for one MoE block (allocate before graph capture): the routing
-    (ids (1, k) int32, probs (1, k) bf16) and the launch's arrival counter (zeroed once, re-armed by the kernel)."""
-
-    def __init__(self, k: int, device) -> None:
-        self.ids = torch.zeros(1, k, dtype=torch.int32, device=device)
-        self.probs = torch.zeros(1, k, dtype=torch.bfloat16, device=device)
-        self.counter = torch.zeros(ATTN_COUNTER_STRIDE, dtype=torch.int32, device=device)
-
-
-def q4_gemv_gate_route(x, proj, residual, gate, norm_weight, eps, k, ws: GateRouteWorkspace, out=None):
-    """y = proj(x) + residual (bf16, as q4_gemv) and, on y, (ids, probs) = the routing of gate(rmsnorm(y)) (as
-    moe_gate_route) in ONE launch; the routing lands in ws.ids / ws.probs. Returns y."""
-    N, K = proj.out_features, proj.in_features
-    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
-    _check(load_library().lga_q4_gemv_gate_route(
-        _dev(x, "x", torch.bfloat16), _dev(proj.qweight, "qweight", torch.uint8), _dev(proj.scales, "scales"),
-        _dev(residual, "residual", torch.bfloat16), _dev(y, "y", torch.bfloat16), N, K, proj.group, proj.fmt,
-        _dev(gate.qweight, "gate_qweight", torch.uint8), _dev(gate.scales, "gate_scales"), gate.group, gate.fmt,
-        _dev(norm_weight, "norm_weight", torch.bfloat16), float(eps), gate.out_features, k,
-        _dev(ws.ids, "ids", torch.int32), _dev(ws.probs, "probs", torch.bfloat16),
-        _dev(ws.counter, "counter", torch.int32), _stream()))
-    return y
-
-
-def moe_gate_fc_supported(gate, fc_1, k: int) -> bool:
-    """Whether lga_moe_gate_fc covers this (router gate, stacked fc_1 expert) pair (K <= 4096, E <= 8)."""
-    return bool(load_library().lga_moe_gate_fc_supported(gate.out_features, k, fc_1.out_features, fc_1.in_features,
-                                                          fc_1.group, gate.group, fc_1.fmt, gate.fmt))
-
-
-def moe_gate_fc(x, norm_weight, eps, gate, qw1, sc1, qw2, sc2, N, K, group, fmt, k, *, ids=None, probs=None,
-                out=None):
-    """One token: (y (k, N), ids (1, k), probs (1, k)) = the routed fc_1 || fc_2 + SwiGLU GEMVs of the experts the
-    gate (RMSNorm fused) picks, routing and GEMVs in ONE launch — bit-identical to moe_gate_route +
-    q4_gemv_swiglu_experts."""
-    ws_, ss_ = _expert_strides(qw1, sc1)
-    if _expert_strides(qw2, sc2) != (ws_, ss_):
-        raise ValueError("fc_1 and fc_2 expert stacks must share one stride")
-    ids = ids if ids is not None else torch.empty(1, k, dtype=torch.int32, device=x.device)
-    probs = probs if probs is not None else torch.empty(1, k, dtype=torch.bfloat16, device=x.device)
-    y = out if out is not None else torch.empty(k, N, dtype=torch.bfloat16, device=x.device)
-    _check(load_library().lga_moe_gate_fc(
-        _dev(x, "x", torch.bfloat16), _dev(norm_weight, "norm_weight", torch.bfloat16), float(eps),
-        _dev(gate.qweight, "gate_qweight", torch.uint8), _dev(gate.scales, "gate_scales"), gate.group, gate.fmt,
-        gate.out_features, k, _dev(qw1, "qw1", torch.uint8), _dev(sc1, "sc1"), _dev(qw2, "qw2", torch.uint8),
-        _dev(sc2, "sc2"), ws_, ss_, qw1.size(0), _dev(y, "y", torch.bfloat16), N, K, group, fmt,
-        _dev(ids, "ids", torch.int32), _dev(probs, "probs", torch.bfloat16), _stream()))
-    return y, ids, probs
-
-
 def experts_pair_supported(N: int, K: int, group: int, fmt: int) -> bool:
     """Whether lga_q4_gemv_experts_pair_combine covers this routed proj shape."""
     return bool(load_library().lga_q4_gemv_experts_pair_supported(N, K, group, fmt))
@@ -838,26 +687,6 @@ def q4_gemv_experts(x, qweight, scales, ids, N, K, group, fmt, *, out=None, vari
                                               _dev(scales, "scales"), _dev(ids, "ids", torch.int32), k,
                                               qweight.size(0), ws, ss, K, _dev(y, "y", torch.bfloat16), N, K, group,
                                               fmt, variant, _stream()))
-    return y
-
-
-def q4_gemv_experts_combine_fits(k: int, N: int, K: int) -> bool:
-    """Whether lga_q4_gemv_experts_combine takes this routed proj (k = 2 slots, N < 24000, K <= 16384)."""
-    return k == 2 and 0 < N < 24000 and K % 32 == 0 and 0 < K <= 16384
-
-
-def q4_gemv_experts_combine(x, qweight, scales, ids, probs, residual, N, K, group, fmt, *, out=None):
-    """One token, k = 2: y (N,) = residual + the two routed experts' proj outputs weighted by ``probs`` and summed
-    in ascending expert id with the bf16 rounding points of lga_moe_combine — bit-identical to q4_gemv_experts +
-    moe_combine, in one launch. x (2, K): each slot's input; W stacked (E, N, K/2)."""
-    if ids.numel() != 2 or probs.numel() != 2 or x.numel() != 2 * K or residual.numel() != N:
-        raise ValueError("q4_gemv_experts_combine: needs 2 slots (ids, probs, x of 2 x K) and a residual of N")
-    ws, ss = _expert_strides(qweight, scales)
-    y = out if out is not None else torch.empty(N, dtype=torch.bfloat16, device=x.device)
-    _check(load_library().lga_q4_gemv_experts_combine(
-        _dev(x, "x", torch.bfloat16), _dev(qweight, "qweight", torch.uint8), _dev(scales, "scales"),
-        _dev(ids, "ids", torch.int32), _dev(probs, "probs", torch.bfloat16), _dev(residual, "residual", torch.bfloat16),
-        qweight.size(0), ws, ss, _dev(y, "y", torch.bfloat16), N, K, group, fmt, _stream()))
     return y
 
 

@@ -131,57 +131,13 @@ def test_decode_attention_32k_context_mixtral_tp2_rank_shape():
         assert torch.all(err <= ref.abs() * 2 ** -7 + 2e-3), float(err.max())
 
 
-@pytest.mark.parametrize("name,mode", [("Llama-2-7b-hf", "int4-g128"), ("Mixtral-8x7B-v0.1", "nf4")])
-@torch.inference_mode()
-def test_decode_out_projection_inside_attention_launch_bit_identical(name, mode):
-    """The decode step's out-projection + residual inside the attention launch (CausalSelfAttention.fuse_proj,
-    lga_attention_decode_proj) gives bit-identical logits to the separate proj GEMV launch, at full width (7B's
-    32 groups; Mixtral's GQA, whose q_per_kv 4 runs as 2 head slices of 2)."""
-    from generate.base import build_model
-    from lit_gpt import Config
-    from lit_gpt.model import CausalSelfAttention
-
-    from lit_gpt import ops
-
-    cfg = Config.from_name(name, n_layer=1)
-    T, N = 300, 5  # a cache of >= 256 rows: the production split count (8 / 16), so the fused launch covers it
-    model = build_model(cfg, quantize=mode, device=DEV, seed=3, max_seq_length=T + N + 1)
-    attn = model.transformer.h[0].attn
-    H, G, hs = cfg.n_head, cfg.n_query_groups, cfg.head_size
-    assert ops.decode_proj_supported(H, G, hs, ops.decode_splits(G, H // G, hs, T + N + 1), attn.proj)
-    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=3)).to(DEV)
-    from lit_gpt.quantize import QuantLinear
-
-    outs = {}
-    default = CausalSelfAttention.fuse_proj
-    QuantLinear.gemv_variant = 0  # the fused kernel reproduces the 4-rows-per-wave projection GEMV
-    try:
-        for fused in (False, True):
-            CausalSelfAttention.fuse_proj = fused
-            for b in model.transformer.h:
-                b.attn.kv_cache.reset_parameters()
-            lg = model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1]
-            tok, seq = int(torch.argmax(lg)), []
-            for i in range(N):
-                lg = model(torch.tensor([[tok]], device=DEV), torch.tensor([T + i], device=DEV),
-                           last_token_only=True)[0, -1]
-                seq.append(lg.clone())
-                tok = int(torch.argmax(lg))
-            outs[fused] = torch.stack(seq)
-    finally:
-        CausalSelfAttention.fuse_proj = default
-        QuantLinear.gemv_variant = -1
-    assert torch.equal(outs[False], outs[True])
-
-
 @pytest.mark.parametrize("mode", ["int4-g128", "nf4"])
 @torch.inference_mode()
-@pytest.mark.parametrize("flag", ["moe_pair_combine", "moe_gate_fc"])
+@pytest.mark.parametrize("flag", ["moe_pair_combine"])
 def test_mixtral_pair_combine_bit_identical(mode, flag):
     """Full-width Mixtral-8x7B (2 blocks): the decode step's routed proj GEMVs + combine + residual as one launch
-    (model.moe_pair_combine, lga_q4_gemv_experts_pair_combine), and the gate + routing folded into the routed fc launch
-    (model.moe_gate_fc, lga_moe_gate_fc), each give bit-identical logits and generated tokens to the launches they
-    replace, eager and through the HIP-graph generate path."""
+    (model.moe_pair_combine, lga_q4_gemv_experts_pair_combine) gives bit-identical logits and generated tokens to the
+    launches it replaces, eager and through the HIP-graph generate path."""
     from generate.base import build_model, generate
     from lit_gpt import Config
     from lit_gpt import model as M
@@ -214,90 +170,6 @@ def test_mixtral_pair_combine_bit_identical(mode, flag):
         setattr(M, flag, default)
     assert torch.equal(outs[False], outs[True])
     assert toks[False] == toks[True]
-
-
-@pytest.mark.parametrize("mode", ["int4-g128", "nf4"])
-@torch.inference_mode()
-def test_mixtral_gate_route_inside_out_projection_bit_identical(mode):
-    """Full-width Mixtral-8x7B block: the decode step's router gate + routing inside the attention's out-projection
-    launch (LLaMAMoE.fold_gate, ops.q4_gemv_gate_route) gives bit-identical logits to the separate
-    lga_moe_gate_route launch, eager and through the HIP-graph generate path."""
-    from generate.base import build_model, generate
-    from lit_gpt import Config
-    from lit_gpt.model import LLaMAMoE
-
-    cfg = Config.from_name("Mixtral-8x7B-v0.1", n_layer=2)
-    T, N = 300, 6
-    model = build_model(cfg, quantize=mode, device=DEV, seed=5, max_seq_length=T + N + 1)
-    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=5)).to(DEV)
-    from lit_gpt.quantize import QuantLinear
-
-    outs, toks = {}, {}
-    default = LLaMAMoE.fold_gate
-    QuantLinear.gemv_variant = 0  # the fused kernel reproduces the 4-rows-per-wave projection GEMV
-    try:
-        for fold in (False, True):
-            LLaMAMoE.fold_gate = fold
-            for b in model.transformer.h:
-                b.attn.kv_cache.reset_parameters()
-            lg = model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1]
-            tok, seq = int(torch.argmax(lg)), []
-            for i in range(N):
-                lg = model(torch.tensor([[tok]], device=DEV), torch.tensor([T + i], device=DEV),
-                           last_token_only=True)[0, -1]
-                seq.append(lg.clone())
-                tok = int(torch.argmax(lg))
-            outs[fold] = torch.stack(seq)
-            for b in model.transformer.h:
-                b.attn.kv_cache.reset_parameters()
-            toks[fold] = generate(model, prompt, T + N, temperature=0.0)[T:].tolist()
-        assert model.transformer.h[0].mlp._route_req.proj_ok  # the fold ran
-    finally:
-        LLaMAMoE.fold_gate = default
-        QuantLinear.gemv_variant = -1
-    assert torch.equal(outs[False], outs[True])
-    assert toks[False] == toks[True]
-
-
-@pytest.mark.parametrize("mode", ["int4-g128", "bnb.nf4"])
-@torch.inference_mode()
-def test_decode_qkv_inside_attention_launch(mode):
-    """The opt-in fused decode launch (CausalSelfAttention.fuse_qkv, lga_qkv_attention_decode: RMSNorm + qkv GEMV +
-    RoPE + KV append + attention in one launch) against the default two launches, Llama-2-7B width: the same KV cache
-    rows (q, k, v are bit-identical) and logits within the fp32 summation order of the attention's online softmax."""
-    from generate.base import build_model
-    from lit_gpt import Config
-    from lit_gpt.model import CausalSelfAttention
-
-    from lit_gpt import ops
-
-    cfg = Config.from_name("Llama-2-7b-hf", n_layer=1)
-    T, N = 300, 5
-    model = build_model(cfg, quantize=mode, device=DEV, seed=4, max_seq_length=T + N + 1)
-    attn = model.transformer.h[0].attn
-    H, G, hs = cfg.n_head, cfg.n_query_groups, cfg.head_size
-    assert ops.qkv_attention_supported(cfg.n_embd, H, G, hs, ops.decode_splits(G, 1, hs, T + N + 1), attn.attn)
-    prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=4)).to(DEV)
-    outs, caches = {}, {}
-    default = CausalSelfAttention.fuse_qkv
-    try:
-        for fused in (False, True):
-            CausalSelfAttention.fuse_qkv = fused
-            attn.kv_cache.reset_parameters()
-            lg = model(prompt.view(1, -1), torch.arange(T, device=DEV), last_token_only=True)[0, -1]
-            tok, seq = int(torch.argmax(lg)), []
-            for i in range(N):
-                lg = model(torch.tensor([[tok]], device=DEV), torch.tensor([T + i], device=DEV),
-                           last_token_only=True)[0, -1]
-                seq.append(lg.float().clone())
-                tok = int(torch.argmax(lg))
-            outs[fused] = torch.stack(seq)
-            caches[fused] = (attn.kv_cache.k[..., : T + N, :].clone(), attn.kv_cache.v[..., : T + N, :].clone())
-    finally:
-        CausalSelfAttention.fuse_qkv = default
-    assert torch.equal(caches[False][0], caches[True][0]) and torch.equal(caches[False][1], caches[True][1])
-    tol = 2e-2 * outs[False].abs().max().item()  # bf16 y rounding of a one-block model's logits
-    assert (outs[False] - outs[True]).abs().max().item() <= tol
 
 
 @pytest.mark.timeout(900)

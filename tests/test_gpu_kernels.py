@@ -623,84 +623,6 @@ def test_moe_gate_route_matches_gemv_then_route(ops, fmt, group, K):
 
 
 @pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (3, 64), (0, 32)])
-@pytest.mark.parametrize("N,K", [(4096, 14336), (512, 384), (1000, 2080), (768, 4096), (640, 6144), (512, 11008)])
-def test_experts_combine_matches_gemv_then_combine(ops, fmt, group, N, K):
-    """lga_q4_gemv_experts_combine (one launch) == lga_q4_gemv_experts + lga_moe_combine (+ residual), bit for bit:
-    both slot orders (the lower expert id added first), rows past a 16-row tile, every chunks-per-lane template."""
-    if K % group:
-        pytest.skip("K must be a multiple of the group")
-    g = torch.Generator().manual_seed(N + K + fmt)
-    E = 8
-    qw, sc = [], []
-    for e in range(E):
-        q, s_ = ops.quantize((torch.randn(N, K, generator=g) * 0.02).to(DEV), fmt, group)
-        qw.append(q)
-        sc.append(s_)
-    qw, sc = torch.stack(qw), torch.stack(sc)
-    for pair in ((1, 6), (6, 1), (0, 7)):
-        ids = torch.tensor(pair, dtype=torch.int32, device=DEV)
-        x = torch.randn(2, K, generator=g).bfloat16().to(DEV)
-        probs = torch.softmax(torch.randn(2, generator=g), 0).bfloat16().to(DEV)
-        res = (torch.randn(N, generator=g) * 2).bfloat16().to(DEV)
-        eout = ops.q4_gemv_experts(x, qw, sc, ids, N, K, group, fmt)
-        want = ops.moe_combine(eout.view(1, 2, N).contiguous(), probs.view(1, 2), ids.view(1, 2),
-                               residual=res.view(1, N)).view(-1)
-        got = ops.q4_gemv_experts_combine(x, qw, sc, ids, probs, res, N, K, group, fmt)
-        assert torch.equal(got.view(torch.int16), want.view(torch.int16)), (pair, (got.float() - want.float()).abs().max())
-
-
-@pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bnb.fp4", "int4-g32"])
-@pytest.mark.parametrize("N,K", [(4096, 4096), (1024, 2048), (768, 6144), (2048, 1024)])
-def test_gemv_gate_route_matches_gemv_then_gate_route(ops, mode, N, K):
-    """lga_q4_gemv_gate_route (out-projection + residual, then in its last-arriving workgroup the next MoE's gate +
-    routing on the projection's output) == lga_q4_gemv (variant 0: the 4-rows-per-wave form the fused kernel
-    reproduces) + lga_moe_gate_route, bit for bit: y, expert ids and
-    probabilities, 8 / 4 experts, k = 1 / 2, tied gate rows; repeated launches (the counter re-arms) and a graph
-    replay."""
-    from lit_gpt.quantize import QuantLinear
-
-    g = torch.Generator().manual_seed(N + K)
-    proj = QuantLinear.from_float((torch.randn(N, K, generator=g) * 0.02).to(DEV), None, mode, DEV)
-    for E, k in ((8, 2), (4, 1), (8, 1)):
-        wg = torch.randn(E, N, generator=g) * 0.02
-        if E == 8:
-            wg[5] = wg[2]  # tied logits: the CPU torch.topk tie order decides
-        gate = QuantLinear.from_float(wg.to(DEV), None, mode, DEV)
-        assert ops.gemv_gate_route_supported(proj, gate, k)
-        nw = (1.0 + 0.1 * torch.randn(N, generator=g)).bfloat16().to(DEV)
-        ws = ops.GateRouteWorkspace(k, DEV)
-        for rep in range(3):
-            x = torch.randn(K, generator=g).bfloat16().to(DEV)
-            res = (torch.randn(N, generator=g) * 2).bfloat16().to(DEV)
-            want = ops.q4_gemv(x, proj.qweight, proj.scales, N, K, proj.group, proj.fmt, residual=res, variant=0)
-            ids0, p0 = ops.moe_gate_route(want, gate.qweight, gate.scales, E, N, gate.group, gate.fmt, k,
-                                          norm_weight=nw, eps=1e-5)
-            got = ops.q4_gemv_gate_route(x, proj, res, gate, nw, 1e-5, k, ws)
-            assert torch.equal(got.view(torch.int16), want.view(torch.int16)), (mode, E, k, rep)
-            assert torch.equal(ws.ids, ids0) and torch.equal(ws.probs.view(torch.int16), p0.view(torch.int16)), \
-                (mode, E, k, rep, ws.ids, ids0)
-        assert int(ws.counter[0]) == 0  # re-armed
-    # graph replay: the captured launch recomputes from the buffers' current contents
-    x = torch.randn(K, generator=g).bfloat16().to(DEV)
-    res = torch.randn(N, generator=g).bfloat16().to(DEV)
-    out = torch.empty(N, dtype=torch.bfloat16, device=DEV)
-    ops.q4_gemv_gate_route(x, proj, res, gate, nw, 1e-5, k, ws, out=out)
-    torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        ops.q4_gemv_gate_route(x, proj, res, gate, nw, 1e-5, k, ws, out=out)
-    for _ in range(2):
-        x.copy_(torch.randn(K, generator=g).bfloat16())
-        graph.replay()
-        torch.cuda.synchronize()
-        want = ops.q4_gemv(x, proj.qweight, proj.scales, N, K, proj.group, proj.fmt, residual=res, variant=0)
-        ids0, p0 = ops.moe_gate_route(want, gate.qweight, gate.scales, gate.out_features, N, gate.group, gate.fmt,
-                                      k, norm_weight=nw, eps=1e-5)
-        assert torch.equal(out.view(torch.int16), want.view(torch.int16))
-        assert torch.equal(ws.ids, ids0) and torch.equal(ws.probs.view(torch.int16), p0.view(torch.int16))
-
-
-@pytest.mark.parametrize("fmt,group", [(0, 128), (1, 64), (3, 64), (0, 32)])
 @pytest.mark.parametrize("N,K", [(4096, 14336), (512, 384), (1024, 2080), (768, 4096), (640, 6144), (512, 11008)])
 def test_experts_pair_combine_matches_gemv_then_combine(ops, fmt, group, N, K):
     """lga_q4_gemv_experts_pair_combine (both slots' routed proj GEMVs, the second-arriving workgroup of each row block
@@ -744,54 +666,6 @@ def test_experts_pair_combine_matches_gemv_then_combine(ops, fmt, group, N, K):
         want = ops.moe_combine(eout.view(1, 2, N).contiguous(), probs.view(1, 2), ids.view(1, 2),
                                residual=res.view(1, N)).view(-1)
         assert torch.equal(out.view(torch.int16), want.view(torch.int16)), pair
-
-
-@pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bnb.fp4", "int4-g32"])
-@pytest.mark.parametrize("N,K", [(14336, 4096), (1024, 2048), (3000, 4096), (640, 1024)])
-def test_moe_gate_fc_matches_gate_route_then_experts(ops, mode, N, K):
-    """lga_moe_gate_fc (the gate + routing derived by every workgroup, then the routed fc_1 || fc_2 + SwiGLU rows) ==
-    lga_moe_gate_route + lga_q4_gemv_swiglu_experts, bit for bit: y, expert ids and probabilities, 8 / 4 experts,
-    k = 2 / 1, tied gate rows, both tile forms (2N >= 24000: 4 rows per wave, else 2) and a graph replay."""
-    from lit_gpt.quantize import QuantLinear
-
-    g = torch.Generator().manual_seed(N + K + 11)
-    for E, k in ((8, 2), (4, 1)):
-        fc1 = [QuantLinear.from_float((torch.randn(N, K, generator=g) * 0.02).to(DEV), None, mode, DEV) for _ in range(E)]
-        fc2 = [QuantLinear.from_float((torch.randn(N, K, generator=g) * 0.02).to(DEV), None, mode, DEV) for _ in range(E)]
-        q1, s1 = torch.stack([l.qweight for l in fc1]), torch.stack([l.scales for l in fc1])
-        q2, s2 = torch.stack([l.qweight for l in fc2]), torch.stack([l.scales for l in fc2])
-        wg = torch.randn(E, K, generator=g) * 0.02
-        if E == 8:
-            wg[5] = wg[2]  # tied logits: the CPU torch.topk tie order decides
-        gate = QuantLinear.from_float(wg.to(DEV), None, mode, DEV)
-        assert ops.moe_gate_fc_supported(gate, fc1[0], k)
-        nw = (1.0 + 0.1 * torch.randn(K, generator=g)).bfloat16().to(DEV)
-        grp, fmt = fc1[0].group, fc1[0].fmt
-        for rep in range(2):
-            x = torch.randn(K, generator=g).bfloat16().to(DEV)
-            ids0, p0 = ops.moe_gate_route(x, gate.qweight, gate.scales, E, K, gate.group, gate.fmt, k, norm_weight=nw,
-                                          eps=1e-5)
-            want = ops.q4_gemv_swiglu_experts(x, q1, s1, q2, s2, ids0.view(-1), N, K, grp, fmt, norm_weight=nw,
-                                              eps=1e-5)
-            got, ids1, p1 = ops.moe_gate_fc(x, nw, 1e-5, gate, q1, s1, q2, s2, N, K, grp, fmt, k)
-            assert torch.equal(ids1, ids0) and torch.equal(p1.view(torch.int16), p0.view(torch.int16)), (E, k, rep)
-            assert torch.equal(got.view(torch.int16), want.view(torch.int16)), (mode, E, k, rep)
-    out = torch.empty(k, N, dtype=torch.bfloat16, device=DEV)
-    ids_b = torch.empty(1, k, dtype=torch.int32, device=DEV)
-    pr_b = torch.empty(1, k, dtype=torch.bfloat16, device=DEV)
-    ops.moe_gate_fc(x, nw, 1e-5, gate, q1, s1, q2, s2, N, K, grp, fmt, k, ids=ids_b, probs=pr_b, out=out)
-    torch.cuda.synchronize()
-    graph = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(graph):
-        ops.moe_gate_fc(x, nw, 1e-5, gate, q1, s1, q2, s2, N, K, grp, fmt, k, ids=ids_b, probs=pr_b, out=out)
-    for _ in range(2):
-        x.copy_(torch.randn(K, generator=g).bfloat16())
-        graph.replay()
-        torch.cuda.synchronize()
-        ids0, p0 = ops.moe_gate_route(x, gate.qweight, gate.scales, gate.out_features, K, gate.group, gate.fmt, k,
-                                      norm_weight=nw, eps=1e-5)
-        want = ops.q4_gemv_swiglu_experts(x, q1, s1, q2, s2, ids0.view(-1), N, K, grp, fmt, norm_weight=nw, eps=1e-5)
-        assert torch.equal(ids_b, ids0) and torch.equal(out.view(torch.int16), want.view(torch.int16))
 
 
 def test_moe_gate_route_rejects_bad_shapes(ops):
@@ -877,90 +751,6 @@ def test_attention_decode_head_slices_agree(ops, H, G, splits, monkeypatch):
         assert torch.all((y - outs[0]).abs() <= outs[0].abs() * 2 ** -7 + 2e-3)
 
 
-@pytest.mark.parametrize("H,G", [(32, 32), (32, 8)])
-@pytest.mark.parametrize("mode,bias", [("int4-g128", False), ("nf4", False), ("int4-g128", True), ("bnb.fp4", False)])
-def test_attention_decode_proj_bit_identical_to_two_launches(ops, H, G, mode, bias):
-    """RoPE + KV append + attention + out-projection + residual in ONE launch (lga_attention_decode_proj) ==
-    lga_attention_decode_fused then lga_q4_gemv(residual): caches, the attention row and the projected row all
-    bit-identical, over positions that include a repeat (the hand-off words advance per launch) and p = 0."""
-    from lit_gpt.quantize import QuantLinear
-
-    hs, S = 128, 2304
-    C = H * hs
-    qkv = to_dev_bf16(synth.normal((1, (H + 2 * G) * hs), "pq", 9, 1.0))
-    k0 = to_dev_bf16(synth.normal((G, S, hs), "pk", 9, 1.0))
-    v0 = to_dev_bf16(synth.normal((G, S, hs), "pv", 9, 1.0))
-    cos, sin = om.build_rope_cache(S, hs, 10000)
-    cos, sin = cos.to(DEV), sin.to(DEV)
-    w = torch.from_numpy(synth.normal((C, C), "pw", 9, 0.02)).float()
-    b = torch.from_numpy(synth.normal((C,), "pb", 9, 0.5)).float() if bias else None
-    lin = QuantLinear.from_float(w, b, mode, torch.device(DEV))
-    res = to_dev_bf16(synth.normal((1, C), "pr", 9, 1.0))
-    splits = ops.decode_splits(G, H // G, hs, S)
-    assert ops.decode_proj_supported(H, G, hs, splits, lin)
-    ws_a = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
-    ws_b = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
-    ka, va, kb, vb = k0.clone(), v0.clone(), k0.clone(), v0.clone()
-    scale = 1.0 / math.sqrt(hs)
-    for p in (2047, 0, 1, 37, 2303, 2047, 1000):
-        pos = torch.tensor([p], device=DEV)
-        ya = ops.attention_decode_fused(qkv, ka, va, pos, pos, cos, sin, H, G, hs, hs, scale, splits, workspace=ws_a)
-        oa = ops.q4_gemv(ya.view(-1), lin.qweight, lin.scales, C, C, lin.group, lin.fmt, bias=lin.bias,
-                         residual=res.view(-1), variant=0)  # the 4-rows-per-wave form the fused kernel reproduces
-        ob, yb = ops.attention_decode_proj(qkv, kb, vb, pos, pos, cos, sin, H, G, hs, hs, scale, splits, ws_b, lin,
-                                           res)
-        assert torch.equal(ka, kb) and torch.equal(va, vb), p
-        assert torch.equal(ya, yb), p
-        assert torch.equal(oa.view(-1), ob.view(-1)), p
-    assert int(ws_b.counters.abs().sum()) == 0
-
-
-@torch.inference_mode()
-def test_attention_decode_proj_graph_replay(ops):
-    """The fused attention + projection captured in a HIP graph and replayed at advancing positions (the position
-    updated on the device between replays, as DecodeGraph does) equals the eager two-launch path step by step."""
-    from lit_gpt.quantize import QuantLinear
-
-    H = G = 32
-    hs, S = 128, 2304
-    C = H * hs
-    qkv = to_dev_bf16(synth.normal((1, (H + 2 * G) * hs), "gq", 9, 1.0))
-    k0 = to_dev_bf16(synth.normal((G, S, hs), "gk", 9, 1.0))
-    v0 = to_dev_bf16(synth.normal((G, S, hs), "gv", 9, 1.0))
-    cos, sin = om.build_rope_cache(S, hs, 10000)
-    cos, sin = cos.to(DEV), sin.to(DEV)
-    lin = QuantLinear.from_float(torch.from_numpy(synth.normal((C, C), "gw", 9, 0.02)).float(), None, "int4-g128",
-                                 torch.device(DEV))
-    res = to_dev_bf16(synth.normal((1, C), "gr", 9, 1.0))
-    splits = ops.decode_splits(G, H // G, hs, S)
-    ws_a = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
-    ws_b = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
-    ka, va, kb, vb = k0.clone(), v0.clone(), k0.clone(), v0.clone()
-    scale = 1.0 / math.sqrt(hs)
-    pos_g = torch.tensor([2040], device=DEV)
-    ob, yb = ops.attention_decode_proj(qkv, kb, vb, pos_g, pos_g, cos, sin, H, G, hs, hs, scale, splits, ws_b, lin,
-                                       res)  # warm-up launch (outside the graph)
-    g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
-        ops.attention_decode_proj(qkv, kb, vb, pos_g, pos_g, cos, sin, H, G, hs, hs, scale, splits, ws_b, lin, res,
-                                  out=ob, y=yb)
-        pos_g.add_(1)
-    pos_a = torch.tensor([2040], device=DEV)
-    ya = ops.attention_decode_fused(qkv, ka, va, pos_a, pos_a, cos, sin, H, G, hs, hs, scale, splits, workspace=ws_a)
-    pos_g.fill_(2041)
-    for step in range(6):
-        pos_a.fill_(2041 + step)
-        ya = ops.attention_decode_fused(qkv, ka, va, pos_a, pos_a, cos, sin, H, G, hs, hs, scale, splits,
-                                        workspace=ws_a)
-        oa = ops.q4_gemv(ya.view(-1), lin.qweight, lin.scales, C, C, lin.group, lin.fmt, residual=res.view(-1),
-                         variant=0)
-        g.replay()
-        torch.cuda.synchronize()
-        assert int(pos_g.item()) == 2042 + step
-        assert torch.equal(ya, yb) and torch.equal(oa.view(-1), ob.view(-1)), step
-    assert torch.equal(ka, kb) and torch.equal(va, vb)
-
-
 @pytest.mark.parametrize("mode,N,K", [("int4-g128", 32000, 4096), ("nf4", 32000, 4096), ("int4-g128", 50304, 2048),
                                       ("bnb.fp4", 1000, 256)])
 @pytest.mark.parametrize("tie", [False, True])
@@ -996,55 +786,3 @@ def test_fused_greedy_head_bit_identical(ops, mode, N, K, tie):
             assert int(ib) == 7 or float(la[int(ib)]) > float(la[7])
     assert int(work.buf[-(9 * 256) // 8:].abs().sum()) == 0  # counters re-armed
 
-
-@pytest.mark.parametrize("mode,bias", [("int4-g128", False), ("nf4", False), ("int4-g128", True)])
-@pytest.mark.parametrize("S,positions", [(2304, [2047, 0, 1, 37, 2303, 2047, 2100]), (4096, [3000, 4095, 2463, 2464])])
-def test_qkv_attention_decode_matches_two_launches(ops, mode, bias, S, positions):
-    """RMSNorm + qkv GEMV + RoPE + KV append + attention in ONE launch (lga_qkv_attention_decode, Llama-2-7B
-    geometry) == lga_q4_gemv(norm) then lga_attention_decode_fused: the qkv row and both caches bit-identical, y
-    within fp32 summation order (tolerance as the fused-vs-two-launch attention test) and within bf16 rounding of an
-    fp64 softmax. Positions past 308 keys per split (S 4096) run the streamed remainder; a repeated position checks
-    the per-group hand-off counters across launches."""
-    from lit_gpt.quantize import QuantLinear
-
-    H = G = 32
-    hs, C = 128, 4096
-    N = (H + 2 * G) * hs
-    g = torch.Generator().manual_seed(S + len(mode))
-    w = torch.randn(N, C, generator=g) * 0.02
-    b = torch.randn(N, generator=g) * 0.5 if bias else None
-    lin = QuantLinear.from_float(w, b, mode, torch.device(DEV))
-    nw = (1.0 + torch.randn(C, generator=g) * 0.1).bfloat16().to(DEV)
-    k0 = (torch.randn(G, S, hs, generator=g)).bfloat16().to(DEV)
-    v0 = (torch.randn(G, S, hs, generator=g)).bfloat16().to(DEV)
-    cos, sin = om.build_rope_cache(S, hs, 10000)
-    cos, sin = cos.to(DEV), sin.to(DEV)
-    splits = ops.decode_splits(G, 1, hs, S)
-    assert ops.qkv_attention_supported(C, H, G, hs, splits, lin)
-    ws_a = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
-    ws_b = ops.AttentionWorkspace(1, H, G, hs, splits, DEV)
-    scratch = torch.empty(N, dtype=torch.bfloat16, device=DEV)
-    ka, va, kb, vb = k0.clone(), v0.clone(), k0.clone(), v0.clone()
-    scale = 1.0 / math.sqrt(hs)
-    for p in positions:
-        x = (torch.randn(1, C, generator=g) * 2).bfloat16().to(DEV)
-        pos = torch.tensor([p], device=DEV)
-        qkv = ops.q4_gemv(x.view(-1), lin.qweight, lin.scales, N, C, lin.group, lin.fmt, bias=lin.bias,
-                          norm_weight=nw, eps=1e-5)
-        ya = ops.attention_decode_fused(qkv.view(1, -1), ka, va, pos, pos, cos, sin, H, G, hs, hs, scale, splits,
-                                        workspace=ws_a).float()
-        yb = ops.qkv_attention_decode(x, nw, 1e-5, lin, kb, vb, pos, pos, cos, sin, H, G, hs, scale, splits, ws_b,
-                                      scratch).float()
-        assert torch.equal(qkv, scratch), p
-        assert torch.equal(ka, kb) and torch.equal(va, vb), p
-        assert torch.all((ya - yb).abs() <= ya.abs() * 2 ** -7 + 2e-3), (p, float((ya - yb).abs().max()))
-        # fp64 softmax from the (bit-exact) cache contents and the roped q
-        q = qkv.view(G, 3, hs)[:, 0].double().cpu()
-        c64, s64 = cos[p].double().cpu(), sin[p].double().cpu()
-        qr = torch.from_numpy(quant.bf16_bits_to_f32(quant.f32_to_bf16_bits(
-            (q * c64 + torch.cat((-q[:, hs // 2:], q[:, : hs // 2]), -1) * s64).float().numpy()))).double()
-        kd, vd = kb[:, : p + 1].double().cpu(), vb[:, : p + 1].double().cpu()
-        ref = torch.softmax(torch.einsum("gd,gkd->gk", qr, kd) * scale, -1)
-        ref = torch.einsum("gk,gkd->gd", ref, vd).reshape(-1)
-        assert torch.max((yb.double().cpu().view(-1) - ref).abs() - ref.abs() * 2 ** -7) <= 1e-4 + 2e-3, p
-    assert int(ws_b.counters.abs().sum()) == 0

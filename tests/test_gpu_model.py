@@ -262,9 +262,9 @@ def test_kv_cache_matches_no_cache_forward():
 @torch.inference_mode()
 def test_moe_decode_fused_gate_route_bit_identical(mode, monkeypatch):
     """The sparse-MoE decode step with the gate GEMV and the routing in one launch (lga_moe_gate_route) and the
-    routed proj GEMVs with the combine in one launch (lga_q4_gemv_experts_combine) produces the same logits, bit for
-    bit, as the unfused form (lga_q4_gemv + lga_moe_route, lga_q4_gemv_experts + lga_moe_combine), and actually takes
-    both fused launches."""
+    routed proj GEMVs with the combine in one launch (lga_q4_gemv_experts_pair_combine) produces the same logits, bit
+    for bit, as the unfused form (lga_q4_gemv + lga_moe_route, lga_q4_gemv_experts + lga_moe_combine), and actually
+    takes both fused launches."""
     from lit_gpt import model as lm
     from lit_gpt import ops
 
@@ -274,7 +274,7 @@ def test_moe_decode_fused_gate_route_bit_identical(mode, monkeypatch):
     prompt = torch.from_numpy(synth.token_ids(T, cfg.vocab_size, seed=51)).to(DEV)
     stream = torch.from_numpy(synth.token_ids(N, cfg.vocab_size, seed=52)).to(DEV)
     calls = []
-    for name in ("moe_gate_route", "q4_gemv_experts_combine"):
+    for name in ("moe_gate_route", "q4_gemv_experts_pair_combine"):
         def counted(*a, _orig=getattr(ops, name), _name=name, **kw):
             calls.append(_name)
             return _orig(*a, **kw)
@@ -283,7 +283,7 @@ def test_moe_decode_fused_gate_route_bit_identical(mode, monkeypatch):
     outs = {}
     for fused in (True, False):
         monkeypatch.setattr(lm, "moe_gate_route", fused)
-        monkeypatch.setattr(lm, "moe_fused_combine", fused)
+        monkeypatch.setattr(lm, "moe_pair_combine", fused)
         model = build_gpu_model(cfg, sd, mode, T + N)
         got = [model(prompt.view(1, -1), torch.arange(T, device=DEV))[0, -1]]
         for i in range(N):
@@ -291,7 +291,7 @@ def test_moe_decode_fused_gate_route_bit_identical(mode, monkeypatch):
         outs[fused] = torch.stack(got).cpu()
         if fused:
             assert calls.count("moe_gate_route") == N * cfg.n_layer, "decode did not take lga_moe_gate_route"
-            assert calls.count("q4_gemv_experts_combine") == N * cfg.n_layer, "decode did not fuse the combine"
+            assert calls.count("q4_gemv_experts_pair_combine") == N * cfg.n_layer, "decode did not fuse the combine"
     assert torch.equal(outs[True].view(torch.int16), outs[False].view(torch.int16))
 
 

@@ -1,7 +1,7 @@
 """A/B of decode-attention builds in ONE process on one box (box-to-box spread is ~4 %, larger than the effects).
 
 usage: AB_LIBS=lit-gpt_amd/lit_gpt/_lib/liblitgpt_amd.so,tools/_lab5/attn_old.so python tools/attn_ab.py
-       (AB_HEADS=32 AB_GROUPS=AB_HEADS AB_CACHE=2304 AB_LAYERS=32 AB_SPLITS=product AB_POS=2063,2302 AB_PROJ=1)
+       (AB_HEADS=32 AB_GROUPS=AB_HEADS AB_CACHE=2304 AB_LAYERS=32 AB_SPLITS=product AB_POS=2063,2302)
 Per library: 32 fused decode-attention launches (Llama-2-7B geometry, one KV cache per block, 8 splits) captured in
 one HIP graph, replayed back to back — bench.py's time_attention — at several positions; rounds alternate the
 libraries so drift hits both. Prints us per launch (median over rounds).
@@ -70,8 +70,6 @@ def main():
                 e.record()
                 e.synchronize()
                 res.setdefault((p, i), []).append(s.elapsed_time(e) * 1e3 / (10 * layers))
-    if os.environ.get("AB_PROJ", "1") != "0":
-        proj_ab(loaded[0], caches, qkv, cos, sin, H, G, hs, S, splits, positions, rounds, dev)
     for p in positions:
         nbytes = 2 * G * hs * 2 * (p + 1) + (H + 2 * G) * hs * 2 + H * hs * 2
         for i, (li, sp) in enumerate(variants):
@@ -79,66 +77,6 @@ def main():
             med = float(np.median(v))
             print(f"p={p} {Path(libs[li]).name:28s} splits {sp:3d} {med:7.2f} us  (min {min(v):.2f} max {max(v):.2f})  "
                   f"{nbytes / med / 1e3:7.1f} GB/s = {nbytes / med / 1e3 / 8000:.3f} of 8 TB/s", flush=True)
-
-
-def proj_ab(lib, caches, qkv, cos, sin, H, G, hs, S, splits, positions, rounds, dev):
-    """The decode attention followed by the out-projection + residual: two launches (attention, lga_q4_gemv) vs the
-    fused lga_attention_decode_proj, 32 blocks with their own caches and proj weights, one graph each."""
-    from lit_gpt.quantize import QuantLinear
-
-    ops._lib = lib
-    C = H * hs
-    lins = [QuantLinear.from_float(torch.randn(C, C, device=dev) * 0.02, None, "int4-g128", dev) for _ in caches]
-    res = torch.randn(1, C, device=dev).bfloat16()
-    y = torch.empty(1, C, device=dev, dtype=torch.bfloat16)
-    o = torch.empty(1, C, device=dev, dtype=torch.bfloat16)
-    ws = ops.AttentionWorkspace(1, H, G, hs, splits, dev)
-    scale = 1.0 / math.sqrt(hs)
-    for p in positions:
-        pos = torch.tensor([p], device=dev)
-
-        def two():
-            for (kc, vc), lin in zip(caches, lins):
-                ops.attention_decode_fused(qkv, kc, vc, pos, pos, cos, sin, H, G, hs, hs, scale, splits,
-                                           workspace=ws, out=y)
-                ops.q4_gemv(y.view(-1), lin.qweight, lin.scales, C, C, 128, 0, residual=res.view(-1), out=o.view(-1))
-
-        def one():
-            for (kc, vc), lin in zip(caches, lins):
-                ops.attention_decode_proj(qkv, kc, vc, pos, pos, cos, sin, H, G, hs, hs, scale, splits, ws, lin, res,
-                                          out=o, y=y)
-
-        def attn_only():
-            for kc, vc in caches:
-                ops.attention_decode_fused(qkv, kc, vc, pos, pos, cos, sin, H, G, hs, hs, scale, splits,
-                                           workspace=ws, out=y)
-
-        def proj_only():
-            for lin in lins:
-                ops.q4_gemv(y.view(-1), lin.qweight, lin.scales, C, C, 128, 0, residual=res.view(-1), out=o.view(-1))
-
-        graphs = {}
-        for name, fn in (("attention", attn_only), ("proj", proj_only), ("attention + proj", two),
-                         ("fused attention+proj", one)):
-            fn()
-            torch.cuda.synchronize()
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                fn()
-            g.replay()
-            torch.cuda.synchronize()
-            graphs[name] = g
-        t = {}
-        for r in range(rounds):
-            for name, g in graphs.items():
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s.record()
-                for _ in range(10):
-                    g.replay()
-                e.record()
-                e.synchronize()
-                t.setdefault(name, []).append(s.elapsed_time(e) * 1e3 / (10 * len(caches)))
-        print(f"p={p}: " + "  ".join(f"{k} {np.median(v):6.2f}" for k, v in t.items()) + " us per block", flush=True)
 
 
 if __name__ == "__main__":
