@@ -149,6 +149,10 @@ class OracleGPT:
         self.rope_pos_dtype = rope_pos_dtype
         self.max_seq_length = cfg.block_size
         self.cache: Optional[Cache] = None
+        # tests only: route_override(router_logits (T, E), topk_idx (T, k)) -> idx (T, k). Random-init routers put
+        # experts within a bf16 ulp of each other; where the product broke such a near-tie the other way, a parity test
+        # lets the oracle take the product's expert set (both are valid evaluations) so the later steps stay comparable
+        self.route_override: Optional[Callable[[torch.Tensor, torch.Tensor], torch.Tensor]] = None
 
     # GPT.max_seq_length setter + rope cache (model.py:466-484, 525-532)
     def set_kv_cache(self, max_seq_length: int) -> None:
@@ -213,6 +217,9 @@ class OracleGPT:
         if c._mlp_class == "LLaMAMoE":  # model.py:727-743
             router = self._lin(f"{p}.gate", x)
             probs, idx = torch.topk(router, c.n_expert_per_token)
+            if self.route_override is not None:  # test hook: adopt another implementation's tie-break (see below)
+                idx = self.route_override(router, idx)
+                probs = torch.gather(router, 1, idx)
             probs = probs.softmax(dim=1, dtype=torch.float).to(x.dtype)
             y = torch.zeros_like(x)
             for e in range(c.n_expert):

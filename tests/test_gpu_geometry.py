@@ -252,3 +252,26 @@ def test_prefill_flash_attention_32k_sampled_rows_vs_fp64():
             err = (y[t, h].double() - ref).abs()
             # bf16 P entering P.V (as SDPA's bf16 math) + bf16 output; fp32 accumulation over up to 32k keys
             assert torch.all(err <= ref.abs() * 2 ** -6 + 5e-3), (t, h, float(err.max()))
+
+
+@pytest.mark.parametrize("name", ["Llama-2-7b-hf", "Mixtral-8x7B-v0.1"])
+@torch.inference_mode()
+def test_long_context_rope_tables_match_reference(name):
+    """The rope tables the product's decode / prefill kernels read (GPT.cos / sin, built on the GPU by
+    generate.base.build_model under rope_positions="reference", i.e. the reference's bf16 init_tensor context) at
+    4k-32k positions against the reference's own build_rope_cache output (tests/golden/g5_rope_long.npz; base 1e4 for
+    Llama-2, 1e6 for Mixtral, lit_gpt/config.py:1304). The position rounding is pinned exactly by the CPU tests; the
+    device's cos / sin may differ from the CPU's by an ulp, so the bound is 2e-7 (a wrong position is off by 1e-2+)."""
+    from generate.base import build_model
+    from lit_gpt import Config
+
+    g = np.load(__import__("pathlib").Path(__file__).parent / "golden" / "g5_rope_long.npz", allow_pickle=False)
+    cfg = Config.from_name(name, n_layer=1, n_embd=256, n_head=2, n_query_groups=2, intermediate_size=256,
+                           vocab_size=512, padding_multiple=64, block_size=32768)
+    assert cfg.rope_n_elem == 128
+    model = build_model(cfg, quantize="int4-g128", device=DEV, seed=1, max_seq_length=32768)
+    rows = torch.from_numpy(g["rows"]).to(DEV)
+    base = int(cfg.rope_base)
+    cos, sin = model.cos.index_select(0, rows).float().cpu().numpy(), model.sin.index_select(0, rows).float().cpu().numpy()
+    np.testing.assert_allclose(cos, g[f"cos_{base}_bf16"], rtol=0, atol=2e-7)
+    np.testing.assert_allclose(sin, g[f"sin_{base}_bf16"], rtol=0, atol=2e-7)

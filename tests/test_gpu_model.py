@@ -127,6 +127,37 @@ def _routing_ambiguous(margins, tol=2 ** -6):
     return amb
 
 
+class _AdoptGpuRoutes:
+    """``OracleGPT.route_override`` for teacher-forced MoE parity: router call n of the oracle takes the expert set the
+    product picked in its call n wherever that set is a near-tie for the oracle's own logits — its weakest logit within
+    ``rel`` (4 bf16 ulps) of the row's largest magnitude below the oracle's k-th best — and keeps its own choice
+    otherwise. A set the product picked OUTSIDE that band is a routing error and fails the test (no skip)."""
+
+    def __init__(self, gpu_calls, rel=2 ** -6):
+        self.gpu, self.rel, self.n, self.adopted = gpu_calls, rel, 0, 0
+
+    def __call__(self, router, idx):
+        k = idx.size(1)
+        g = self.gpu[self.n]
+        self.n += 1
+        assert g.numel() == idx.numel(), "router call sequences differ between the product and the oracle"
+        g = g.reshape(idx.shape).to(idx.device)
+        r = router.double()
+        kth = torch.sort(r, dim=-1, descending=True).values[:, k - 1]
+        tol = self.rel * r.abs().amax(dim=-1)
+        out = idx.clone()
+        for t in range(idx.size(0)):
+            if torch.equal(torch.sort(idx[t]).values, g[t]):
+                continue
+            weakest = r[t, g[t]].min()
+            assert weakest >= kth[t] - tol[t], (
+                f"router call {self.n - 1} token {t}: product experts {g[t].tolist()} vs oracle "
+                f"{torch.sort(idx[t]).values.tolist()}, gap {float(kth[t] - weakest):.3g} > tolerance {float(tol[t]):.3g}")
+            out[t] = g[t]
+            self.adopted += 1
+        return out
+
+
 @pytest.mark.parametrize("key", list(CFGS))
 @pytest.mark.parametrize("mode", ["int4-g128", "nf4", "bnb.nf4-dq", "bnb.fp4", "bnb.fp4-dq", "bf16"])
 @torch.inference_mode()
@@ -141,34 +172,24 @@ def test_teacher_forced_logits_match_oracle(key, mode):
     stream = torch.from_numpy(synth.token_ids(N, cfg.vocab_size, seed=22))  # forced continuation
     with _GpuRoutes() as routes:
         got = [model(prompt.view(1, -1).to(DEV), torch.arange(T, device=DEV))[0, -1].float().cpu()]
-        marks = [len(routes.calls)]
         for i in range(N - 1):
             got.append(model(stream[i:i + 1].view(1, 1).to(DEV), torch.tensor([T + i], device=DEV))[0, -1].float()
                        .cpu())
-            marks.append(len(routes.calls))
-    exp, diverged = {}, [False] * N
+    exp = {}
     for dt in (torch.bfloat16, torch.float64):
         ref = oracle_for(cfg, sd, mode, dt)
         ref.set_kv_cache(T + N)
-        choices = []
-        _watch_router_margins(ref, choices)
+        if routes.calls:
+            # a router near-tie the product broke the other way is not an error: the oracle adopts that expert set
+            # (bounded by _AdoptGpuRoutes' tolerance), so every step stays comparable and none is skipped
+            ref.route_override = adopt = _AdoptGpuRoutes(routes.calls)
         out = [ref.forward(prompt, torch.arange(T))[-1]]
         for i in range(N - 1):
             out.append(ref.forward(stream[i:i + 1], torch.tensor([T + i]))[-1])
         exp[dt] = out
-        # a router near-tie the two sides broke differently sends a token through another expert (not an error):
-        # from the first step whose expert sets differ on, the caches differ too and the steps are not comparable
-        same = [torch.equal(a, b) for a, b in zip(routes.calls, choices)] if choices else []
-        first_bad = next((j for j, ok in enumerate(same) if not ok), None)
-        if first_bad is not None:
-            step = next(s for s, m in enumerate(marks) if m > first_bad)
-            for s in range(step, N):
-                diverged[s] = True
-    if diverged[0]:
-        pytest.skip("a router near-tie inside the prompt: the two sides legitimately route a token differently")
-    for s, (g, div) in enumerate(zip(got, diverged)):
-        if div:
-            continue
+        if routes.calls:
+            assert adopt.n == len(routes.calls), "router call counts differ between the product and the oracle"
+    for s, g in enumerate(got):
         check_step(g, exp[torch.bfloat16][s], exp[torch.float64][s], f"{key} {mode} step {s}")
 
 

@@ -212,6 +212,25 @@ def test_rope_cache_follows_reference_default_dtype(golden):
     np.testing.assert_array_equal(cos.numpy(), g["rope_small_cos"])
 
 
+def test_product_rope_long_context_rows_match_reference(golden):
+    """The product's build_rope_cache at 4k-32k positions, base 1e4 and 1e6, fp32 and bf16 default dtype: bit-equal
+    to the reference's tables (tests/golden/g5_rope_long.npz, make_golden_rope.py)."""
+    from lit_gpt.model import build_rope_cache
+
+    g = golden("g5_rope_long.npz")
+    rows = g["rows"]
+    for base in (10000, 1000000):
+        for dt, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+            prev = torch.get_default_dtype()
+            torch.set_default_dtype(dt)
+            try:
+                cos, sin = build_rope_cache(32768, 128, base=base)
+            finally:
+                torch.set_default_dtype(prev)
+            np.testing.assert_array_equal(cos[rows].numpy(), g[f"cos_{base}_{tag}"])
+            np.testing.assert_array_equal(sin[rows].numpy(), g[f"sin_{base}_{tag}"])
+
+
 def test_topk_order_restatement_matches_cpu_torch_topk():
     """oracle.model.topk_order (the spec of lga_moe_route) == torch.topk on the CPU, ties included."""
     import random
@@ -290,3 +309,34 @@ def test_fp4_oracle_is_bitsandbytes_fp4():
     assert np.all(err <= nearest + 1e-6)
     np.testing.assert_array_equal(quant.dequantize_fp4(*quant.quantize_fp4(d, 64), 64), d)
     assert parse_mode("bnb.fp4") == (ops.FMT_FP4, 64) and parse_mode("bnb.fp4-dq") == (ops.FMT_FP4, 64)
+
+
+def test_oracle_route_override_hook():
+    """OracleGPT.route_override (the MoE parity tests' near-tie adoption): an override returning the oracle's own
+    expert sets leaves the logits bit-identical, and one that swaps a token's set changes only what it routes."""
+    from lit_gpt import Config
+
+    cfg = Config.from_name("Mixtral-8x7B-v0.1", n_layer=1, n_embd=128, n_head=4, n_query_groups=2,
+                           intermediate_size=96, vocab_size=200, padding_multiple=64, block_size=64)
+    sd = synth.state_dict(cfg, seed=3)
+    idx = torch.from_numpy(synth.token_ids(6, cfg.vocab_size, seed=3))
+    base = om.OracleGPT(cfg, sd, dtype=torch.float64)
+    base.set_kv_cache(16)
+    want = base.forward(idx, torch.arange(6))
+    same = om.OracleGPT(cfg, sd, dtype=torch.float64)
+    same.set_kv_cache(16)
+    seen = []
+    same.route_override = lambda router, i: (seen.append(i.clone()), i)[1]
+    assert torch.equal(same.forward(idx, torch.arange(6)), want)
+    assert len(seen) == cfg.n_layer and seen[0].shape == (6, cfg.n_expert_per_token)
+    other = om.OracleGPT(cfg, sd, dtype=torch.float64)
+    other.set_kv_cache(16)
+
+    def swap_last(router, i):
+        j = i.clone()
+        j[-1] = torch.topk(router[-1], cfg.n_expert_per_token + 1).indices[1:]  # 2nd and 3rd best
+        return j
+
+    other.route_override = swap_last
+    got = other.forward(idx, torch.arange(6))
+    assert torch.equal(got[:-1], want[:-1]) and not torch.equal(got[-1], want[-1])

@@ -132,6 +132,20 @@ def test_rope_cache_and_apply(golden):
     np.testing.assert_allclose(y.numpy(), g["rope_y"], rtol=0, atol=1e-5)
 
 
+def test_rope_long_context_rows_match_reference(golden):
+    """The oracle's rope tables at 4k-32k positions (config 5's 32k context, rope_base 1e6; Llama-2's 1e4) against the
+    reference's own build_rope_cache (tests/golden/make_golden_rope.py), under an fp32 and a bf16 default dtype — the
+    bf16 position rounding that the 8k / 32k Mixtral prefill tests depend on."""
+    g = golden("g5_rope_long.npz")
+    rows = g["rows"]
+    for base in (10000, 1000000):
+        for pos_dtype, tag in ((torch.float32, "f32"), (torch.bfloat16, "bf16")):
+            cos, sin = om.build_rope_cache(32768, 128, base, 1, pos_dtype)
+            np.testing.assert_allclose(cos[rows].numpy(), g[f"cos_{base}_{tag}"], rtol=0, atol=1e-6)
+            np.testing.assert_allclose(sin[rows].numpy(), g[f"sin_{base}_{tag}"], rtol=0, atol=1e-6)
+        assert not np.allclose(g[f"cos_{base}_f32"], g[f"cos_{base}_bf16"])
+
+
 def test_rmsnorm(golden):
     g = golden("g3_ops.npz")
     x, w = torch.from_numpy(g["rms_x"]), torch.from_numpy(g["rms_w"])
