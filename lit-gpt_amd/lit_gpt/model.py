@@ -624,12 +624,17 @@ def build_rope_cache(seq_len: int, n_elem: int, device: Optional[torch.device] =
     The positions are a true division of an integer range, so (as in the reference) they take the DEFAULT dtype:
     under a bf16 default — the reference's ``fabric.init_tensor()`` with bf16-true / bnb precision around
     ``model.max_seq_length = ...`` (generate/base.py:153-157, generate/tp.py) — positions above 256 round to bf16
-    before the fp32 outer product. ``generate.base.build_model(rope_positions=...)`` chooses that context."""
-    inv_freq = torch.arange(0, n_elem, 2, device=device).float().div(n_elem)
+    before the fp32 outer product. ``generate.base.build_model(rope_positions=...)`` chooses that context.
+
+    The tables are computed on the CPU (as the reference's CPU run computes them) and then moved to ``device``: the
+    GPU's fp32 cos / sin of angles in the thousands of radians differ from the CPU's by up to ~1.6e-3 (measured at
+    the 4k-32k rows of tests/golden/g5_rope_long.npz), the CPU's are the reference's values bit for bit."""
+    inv_freq = torch.arange(0, n_elem, 2).float().div(n_elem)
     theta = 1.0 / torch.pow(float(base), inv_freq)
-    positions = torch.arange(seq_len, device=device).div(condense_ratio)  # default dtype, see above
+    positions = torch.arange(seq_len).div(condense_ratio)  # default dtype, see above
     angles = torch.outer(positions, theta).repeat(1, 2)
-    return torch.cos(angles), torch.sin(angles)
+    cos, sin = torch.cos(angles), torch.sin(angles)
+    return (cos, sin) if device is None else (cos.to(device), sin.to(device))
 
 
 def apply_rope(x: torch.Tensor, cos: torch.Tensor, sin: torch.Tensor) -> torch.Tensor:

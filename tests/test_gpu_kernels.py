@@ -449,6 +449,37 @@ def test_attention_decode_fused_matches_two_launch_path(ops, H, G, p, splits):
     assert torch.max((yb - ref).abs() - ref.abs() * 2 ** -7) <= 1e-4
 
 
+@pytest.mark.parametrize("H,G", [(32, 32), (8, 1), (32, 8)])
+@pytest.mark.parametrize("p", [1726, 1727, 2000, 2047, 2302, 2303])
+@pytest.mark.parametrize("splits", [8, 16, 36])
+def test_attention_decode_fixed_splits_ignore_rows_past_p(ops, H, G, p, splits):
+    """Split ranges fixed by the cache length (csrc/attention.hip LGA_ATTN_FIXED: the first K/V batch leaves before
+    input_pos is read, and may cover rows past p) with every cache row past p set to NaN: the output is finite and
+    matches the fp64 softmax over keys 0..p; p = 1726 / 1727 sit on either side of the 3/4-of-the-cache switch to
+    live-position ranges (S = 2304)."""
+    hs, S = 128, 2304
+    qkv = to_dev_bf16(synth.normal((1, (H + 2 * G) * hs), "nq", 8, 1.0))
+    k0 = to_dev_bf16(synth.normal((G, S, hs), "nk", 8, 1.0))
+    v0 = to_dev_bf16(synth.normal((G, S, hs), "nv", 8, 1.0))
+    k0[:, p:] = float("nan")  # row p is appended by the launch itself
+    v0[:, p:] = float("nan")
+    cos, sin = om.build_rope_cache(S, hs, 10000)
+    cos, sin = cos.to(DEV), sin.to(DEV)
+    pos = torch.tensor([p], device=DEV)
+    scale = 1.0 / math.sqrt(hs)
+    y = ops.attention_decode_fused(qkv, k0, v0, pos, pos, cos, sin, H, G, hs, hs, scale, n_splits=splits)
+    y = y.double().cpu().view(H, hs)
+    assert torch.all(torch.isfinite(y))
+    qpk = H // G
+    kd, vd = k0[:, : p + 1].double().cpu(), v0[:, : p + 1].double().cpu()
+    q = ops.rope_kv_append(qkv, k0.clone(), v0.clone(), pos, pos, cos, sin, H, G, hs, hs).double().cpu()
+    ref = torch.empty(H, hs, dtype=torch.float64)
+    for h in range(H):
+        sc = kd[h // qpk] @ q[0, h] * scale
+        ref[h] = torch.softmax(sc, 0) @ vd[h // qpk]
+    assert torch.max((y - ref).abs() - ref.abs() * 2 ** -7) <= 1e-4
+
+
 def test_attention_decode_fused_rejects_unsupported_geometry(ops):
     qkv = torch.zeros(1, 3 * 64 * 4, dtype=torch.bfloat16, device=DEV)
     kc = torch.zeros(4, 16, 64, dtype=torch.bfloat16, device=DEV)
