@@ -543,7 +543,8 @@ def main():
                    "global_batch": 1, "seq_len": T, "parallelism": f"tp{world}",
                    "graph": use_graph, "steps_per_graph_launch": CHUNK if use_graph else 0,
                    **({"graph_note": graph_note} if graph_note else {}),
-                   **({"allreduce": ("xgmi one-shot" + ("" if gtp.comm.get_default().fused_ok else
+                   **({"allreduce": (f"xgmi one-shot, fused GEMV protocol {gtp.comm.get_default().protocol}" +
+                                     ("" if gtp.comm.get_default().fused_ok else
                                                         f" (fused GEMV form off: {gtp.comm.get_default().fused_fallback})"))
                        if gtp.comm.get_default() is not None else
                        f"rccl ({gtp.comm.fallback_reason or 'LGA_TP_ALLREDUCE=rccl'})"} if world > 1 else {})},

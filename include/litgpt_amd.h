@@ -238,11 +238,20 @@ int lga_comm_trace(void* buf, int n_records);
  * lga_q4_gemv(x, W, bias) over the ranks (+ residual), bit for bit — each workgroup pushes its partial rows into
  * every rank's mailbox, the last-arriving workgroup of the rank raises the flags, waits for the peers and sums in
  * rank order. Same mailboxes / sequence counter / error word as lga_allreduce_bf16 (calls of the two may be mixed);
- * arrive_counter: 576 uint32 (9 counters at a 256-B stride) zeroed once (re-armed by the kernel). N % 8 == 0, N <= cap. Graph-capturable. */
+ * arrive_counter: 576 uint32 (9 counters at a 256-B stride; 640 with the tagged form's) zeroed once (re-armed by the kernel). N % 8 == 0, N <= cap. Graph-capturable. */
 int lga_q4_gemv_allreduce(const void* x, const uint8_t* qweight, const void* scales, const void* bias,
                           const void* residual, void* y, int N, int K, int group, int fmt, void* const* mailboxes,
                           int rank, int world, int cap, unsigned* seq_counter, unsigned* arrive_counter,
                           unsigned* err, lga_stream_t stream);
+/* The same call in the tagged protocol (generate/tp.py:73-74 on multi-GPU ranks): every workgroup pushes its rows as
+ * 8-byte {bf16 pair, call sequence} granules into every rank's mailbox and polls its own rows from every rank — no
+ * arrival counters, flags or last-arriver sum; identical result bits. arrive_counter: 640 uint32 (word 576 is the
+ * monotonic launch counter the sequence derives from, zeroed once); seq_counter unused. The grid need not be
+ * co-resident (a workgroup waits only for other ranks). Same mailboxes: lga_comm_mailbox_bytes covers both regions. */
+int lga_q4_gemv_allreduce_tagged(const void* x, const uint8_t* qweight, const void* scales, const void* bias,
+                                 const void* residual, void* y, int N, int K, int group, int fmt,
+                                 void* const* mailboxes, int rank, int world, int cap, unsigned* seq_counter,
+                                 unsigned* arrive_counter, unsigned* err, lga_stream_t stream);
 
 /* -- greedy sampling (generate/base.py:30-47 at temperature 0): lowest index among the maxima; optionally
  *    writes the token (int32) and advances *pos_inout by one (generate/base.py:92) -------------------------- */

@@ -54,9 +54,6 @@ __device__ __forceinline__ uint4 ld_kv(const uint16_t* p) {
 // q heads itself, and the workgroup whose split owns the new position p ropes k, appends k and v to the cache
 // at p (KVCache.forward, lit_gpt/model.py:788-795) and scores that key from registers — replacing the separate
 // lga_rope_kv_append launch of the decode step.
-#ifndef LGA_ATTN_FIXED
-#define LGA_ATTN_FIXED 1  // lab A/B: 0 = split ranges always from the live position
-#endif
 #ifndef LGA_ATTN_SOLO
 #define LGA_ATTN_SOLO 1  // lab A/B: 0 = the workgroup-barrier publish for every slice width
 #endif
@@ -81,65 +78,25 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
   const int rg = wave * RGW + lane / LPR;
   const int sub = lane % LPR;
   LGA_TRACE(0);
-  // Split ranges (LGA_ATTN_FIXED): split s owns the contiguous rows [s * cs, (s + 1) * cs) of the CACHE (cs =
-  // ceil(max_seq / splits)), fixed at capture, so its first two K/V batches do not depend on input_pos: they are
-  // issued right behind q and the RoPE rows (whose addresses need only the scalar position loads), before any of
-  // those land, instead of after the RoPE. generate sizes the cache to prompt + new tokens, so the keys 0..p fill
-  // all but the tail of the splits; when they fill less than 3/4 of the cache the kernel falls back to ranges of
-  // ceil((p + 1) / splits) (the early batches are then re-issued and the first ones wasted)
-  const int cs_fix = (max_seq + n_splits - 1) / n_splits;
-  const int s_lo = min(split * cs_fix, max_seq), s_hi = min(s_lo + cs_fix, max_seq);
-  const uint16_t* kbase = kc + (size_t)g * max_seq * HS + sub * 8;
-  const uint16_t* vbase = vc + (size_t)g * max_seq * HS + sub * 8;
   // both positions in one scalar round trip (hipcc otherwise waits for input_pos before issuing rope_pos)
   const long p = input_pos[t];
   const long rp_raw = FUSED ? rope_pos[t] : 0;
-  // the q rows first: they are needed first and depend on nothing
-  uint4 qraw[QPK];
-#pragma unroll
-  for (int h = 0; h < QPK; ++h) {
-    if (FUSED)  // qkv row layout per group: [q_0 .. q_{QPK-1}, k, v] x HS (scripts/convert_hf_checkpoint.py:181-187)
-      qraw[h] = *(const uint4*)(q + ((size_t)g * (QPKT + 2) + hsi * QPK + h) * HS + sub * 8);
-    else
-      qraw[h] = *(const uint4*)(q + ((size_t)t * n_head + (size_t)g * QPKT + hsi * QPK + h) * HS + sub * 8);
-  }
-  float cs[FUSED ? 8 : 1], sn[FUSED ? 8 : 1];
-  if (FUSED) {
-    const long rp = min(max(rp_raw, 0L), (long)rope_rows - 1);
-    const float* cr = cos + (size_t)rp * HS + sub * 8;
-    const float* sr = sin + (size_t)rp * HS + sub * 8;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      cs[i] = cr[i];
-      sn[i] = sr[i];
-    }
-  }
-  constexpr int STP = RG * UNR;  // keys per step of the split (all row groups)
-  uint4 ka[UNR], va[UNR], kb[UNR], vb[UNR];
-  if (PIPE && LGA_ATTN_FIXED) {
-    __builtin_amdgcn_sched_barrier(0);  // the batches go out behind q and the RoPE rows (vmcnt retires in order)
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {  // rows past p are masked (and their values zeroed) before use
-      const int j = max(min(s_lo + rg + u * RG, s_hi - 1), 0);
-      ka[u] = ld_kv(kbase + (size_t)j * HS);
-      va[u] = ld_kv(vbase + (size_t)j * HS);
-    }
-#pragma unroll
-    for (int u = 0; u < UNR; ++u) {
-      const int j = max(min(s_lo + STP + rg + u * RG, s_hi - 1), 0);
-      kb[u] = ld_kv(kbase + (size_t)j * HS);
-      vb[u] = ld_kv(vbase + (size_t)j * HS);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-  }
   const int L = (int)min(p + 1, (long)max_seq);  // keys 0..p (never past the cache)
-  const bool fixed = LGA_ATTN_FIXED && 4 * (long)L >= 3 * (long)max_seq;  // uniform
-  const int chunk = fixed ? cs_fix : (L + n_splits - 1) / n_splits;
-  const int k_lo = fixed ? s_lo : split * chunk;
-  const int k_hi = min(fixed ? s_hi : k_lo + chunk, L);
+  const int chunk = (L + n_splits - 1) / n_splits;
+  const int k_lo = split * chunk;
+  const int k_hi = min(k_lo + chunk, L);
   LGA_TRACE(1);
   const bool owns_new = FUSED && p < max_seq && k_lo <= p && p < k_hi;
   const int k_end = FUSED ? min(k_hi, (int)p) : k_hi;  // fused: key p is scored from registers below
+  const float* cr = nullptr;
+  const float* sr = nullptr;
+  if (FUSED) {
+    const long rp = min(max(rp_raw, 0L), (long)rope_rows - 1);
+    cr = cos + (size_t)rp * HS + sub * 8;
+    sr = sin + (size_t)rp * HS + sub * 8;
+  }
+  const uint16_t* kbase = kc + (size_t)g * max_seq * HS + sub * 8;
+  const uint16_t* vbase = vc + (size_t)g * max_seq * HS + sub * 8;
   // clamped duplicate rows (past k_end) are masked in consume() and hit in cache
   auto fetch = [&](uint4 (&kv)[UNR], uint4 (&vv)[UNR], int j0) {
 #pragma unroll
@@ -150,6 +107,25 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
     }
   };
   const int j_first = k_lo + rg;
+
+  // the q rows and the RoPE tables, then the first K/V batch (an empty split's batch re-reads row 0 and is never
+  // consumed)
+  uint4 qraw[QPK];
+#pragma unroll
+  for (int h = 0; h < QPK; ++h) {
+    if (FUSED)  // qkv row layout per group: [q_0 .. q_{QPK-1}, k, v] x HS (scripts/convert_hf_checkpoint.py:181-187)
+      qraw[h] = *(const uint4*)(q + ((size_t)g * (QPKT + 2) + hsi * QPK + h) * HS + sub * 8);
+    else
+      qraw[h] = *(const uint4*)(q + ((size_t)t * n_head + (size_t)g * QPKT + hsi * QPK + h) * HS + sub * 8);
+  }
+  float cs[FUSED ? 8 : 1], sn[FUSED ? 8 : 1];
+  if (FUSED) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      cs[i] = cr[i];
+      sn[i] = sr[i];
+    }
+  }
   // q stays packed bf16 (as the reference's bf16 q): scores are v_dot2_f32_bf16 chains — two exact bf16 products
   // per instruction into an fp32 accumulator, half the VALU of unpack + fma. Interleaved A/B (tools/attn_ab.py,
   // round 5) at p = 32066, 32 splits: Mixtral 34.8 -> 33.8 us, its TP = 2 rank 24.8 -> 23.5; Llama-2-7B neutral
@@ -169,20 +145,10 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
     return __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(s2, a.w), __builtin_bit_cast(s2, b.w), d, false);
   };
   // the first K/V batch AFTER the RoPE: issued beside q (ahead of the RoPE's wait) every split's first loads leave
-  // in one burst at kernel start, measured 0.25-0.3 us slower per launch (tools/attn_ab.py, round 5) — unless the
-  // ranges are fixed (above), where two batches leave behind q and the RoPE rows
+  // in one burst at kernel start, measured 0.25-0.3 us slower per launch (tools/attn_ab.py, round 5)
   __builtin_amdgcn_sched_barrier(0);
-  if (PIPE) {
-    if (fixed) {  // the early batches: rows past k_end may be stale (or never written): their values must not reach o
-#pragma unroll
-      for (int u = 0; u < UNR; ++u) {
-        if (j_first + u * RG >= k_end) va[u] = make_uint4(0, 0, 0, 0);
-        if (j_first + STP + u * RG >= k_end) vb[u] = make_uint4(0, 0, 0, 0);
-      }
-    } else {
-      fetch(ka, va, j_first);
-    }
-  }
+  uint4 ka[UNR], va[UNR], kb[UNR], vb[UNR];
+  if (PIPE) fetch(ka, va, j_first);
   LGA_TRACE(2);
   // m starts at a finite floor, not -inf: every row group runs the split's step count, so one whose keys are all
   // past k_end sees only masked (-inf) scores, and exp(floor - floor) = 1 keeps its (l, o) = 0 instead of NaN; a
@@ -227,27 +193,17 @@ __device__ __forceinline__ void attn_body(const uint16_t* __restrict__ q, uint16
   if (PIPE) {
     // software pipeline: step i + 1's 2*UNR loads are issued before step i's math, so every row group keeps 2-4
     // steps of K/V in flight and a split costs one load round trip plus its streaming time (the first batch was
-    // issued above, next to q; with fixed ranges the second one too)
-    const int nst = k_end > k_lo ? (k_end - k_lo + STP - 1) / STP : 0;
+    // issued above, next to q)
+    const int stp = RG * UNR;
+    const int nst = k_end > k_lo ? (k_end - k_lo + stp - 1) / stp : 0;
     int i = 0;
-    if (fixed) {
-      for (; i < nst; i += 2) {
-        consume(ka, va, j_first + i * STP);
-        if (i + 2 < nst) fetch(ka, va, j_first + (i + 2) * STP);
-        if (i + 1 < nst) {
-          consume(kb, vb, j_first + (i + 1) * STP);
-          if (i + 3 < nst) fetch(kb, vb, j_first + (i + 3) * STP);
-        }
-      }
-    } else {
-      for (; i + 1 < nst; i += 2) {
-        fetch(kb, vb, j_first + (i + 1) * STP);
-        consume(ka, va, j_first + i * STP);
-        if (i + 2 < nst) fetch(ka, va, j_first + (i + 2) * STP);
-        consume(kb, vb, j_first + (i + 1) * STP);
-      }
-      if (i < nst) consume(ka, va, j_first + i * STP);
+    for (; i + 1 < nst; i += 2) {
+      fetch(kb, vb, j_first + (i + 1) * stp);
+      consume(ka, va, j_first + i * stp);
+      if (i + 2 < nst) fetch(ka, va, j_first + (i + 2) * stp);
+      consume(kb, vb, j_first + (i + 1) * stp);
     }
+    if (i < nst) consume(ka, va, j_first + i * stp);
   } else {
     for (int j0 = j_first; j0 < k_end; j0 += RG * UNR) {
       fetch(ka, va, j0);

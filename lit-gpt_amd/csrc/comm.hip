@@ -74,8 +74,11 @@ __global__ void __launch_bounds__(kCommThreads) allreduce_kernel(const uint16_t*
 
 }  // namespace lga
 
+// flags, the flag protocol's data [2][8][cap] bf16, then the tagged protocol's granules [2][8][cap / 2] x 8 B
+// (gemv_ar.hip granule_ptr)
 extern "C" size_t lga_comm_mailbox_bytes(int cap) {
-  return lga::kFlagBytes + (size_t)2 * lga::kMaxRanks * (size_t)cap * sizeof(uint16_t);
+  return lga::kFlagBytes + (size_t)2 * lga::kMaxRanks * (size_t)cap * sizeof(uint16_t) +
+         (size_t)2 * lga::kMaxRanks * (size_t)cap * 4;
 }
 
 // Uncached (coherent across devices) zeroed device allocation + its IPC handle (64 bytes, hipIpcMemHandle_t).

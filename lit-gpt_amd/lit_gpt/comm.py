@@ -16,6 +16,8 @@ One process per GPU, all ranks of the group on this node (xGMI / same-device IPC
 from __future__ import annotations
 
 import ctypes
+import os
+import socket
 from typing import List, Optional
 
 import torch
@@ -73,14 +75,28 @@ class XgmiAllReduce:
                 ptrs.append(p.value)
         self.seq = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
-        # lga_q4_gemv_allreduce's arrival counters (9 words at a 256-B stride)
-        self.arrive = torch.zeros(9 * 64, dtype=torch.int32, device=self.device)
+        # lga_q4_gemv_allreduce's arrival counters (9 words at a 256-B stride) + the tagged form's launch counter
+        self.arrive = torch.zeros(10 * 64, dtype=torch.int32, device=self.device)
+        # the fused row-parallel GEMV's protocol: "tagged" (granules; every workgroup waits only for other ranks)
+        # when every rank owns its GPU, "flags" (last arriver, one workgroup waits) when ranks share a device — the
+        # one-GPU tests and rehearsals, where the tagged form's waiting workgroups of one rank could occupy the CUs
+        # the others' kernels need. LGA_AR_PROTOCOL=flags|tagged overrides.
+        self.protocol = self._choose_protocol(group)
         self._agree(failure, "mailbox mapping")
         self._mailboxes = (ctypes.c_void_p * self.world)(*ptrs)
         self._self_test()
         self.fused_ok = True  # lga_q4_gemv_allreduce passed its own self-test (else linear_reduce uses two launches)
         self.fused_fallback: Optional[str] = None
         self._self_test_fused()
+
+    def _choose_protocol(self, group) -> str:
+        env = os.environ.get("LGA_AR_PROTOCOL", "auto")
+        if env in ("flags", "tagged"):
+            return env
+        ident = str(getattr(torch.cuda.get_device_properties(self.device), "uuid", self.device.index))
+        ids: List[Optional[str]] = [None] * self.world
+        dist.all_gather_object(ids, (socket.gethostname(), ident), group=group)
+        return "tagged" if len(set(ids)) == self.world else "flags"
 
     def _agree(self, failure: Optional[str], what: str) -> None:
         """All ranks learn whether any rank failed (MIN over a flag); on failure every rank raises."""
@@ -193,7 +209,9 @@ class XgmiAllReduce:
             if residual.numel() != N:
                 raise ValueError("XgmiAllReduce.gemv_all_reduce: residual shape differs from the output")
             res = ops._dev(residual.contiguous(), "residual", torch.bfloat16)
-        ops._check(ops.load_library().lga_q4_gemv_allreduce(
+        lib = ops.load_library()
+        fn = lib.lga_q4_gemv_allreduce_tagged if self.protocol == "tagged" else lib.lga_q4_gemv_allreduce
+        ops._check(fn(
             ops._dev(x.contiguous(), "x", torch.bfloat16), ops._dev(lin.qweight, "qweight", torch.uint8),
             ops._dev(lin.scales, "scales"), ops._opt(lin.bias, "bias", torch.bfloat16), res,
             ops._dev(y, "y", torch.bfloat16), N, K, lin.group, lin.fmt, self._mailboxes, self.rank, self.world,

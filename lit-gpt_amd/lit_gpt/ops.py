@@ -100,6 +100,8 @@ SIGNATURES = {
     "lga_sample_topk": [_P, _I, _I, _F, _P, ctypes.c_ulonglong, _P, _P, _P, _P, _P, _I, _I, _P, _P, _P, _P],
     "lga_q4_gemv_allreduce": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P, _P,
                               _P],
+    "lga_q4_gemv_allreduce_tagged": [_P, _P, _P, _P, _P, _P, _I, _I, _I, _I, ctypes.POINTER(_P), _I, _I, _I, _P, _P,
+                                     _P, _P],
 }
 _RESTYPES = {"lga_q4_gemv_experts_pair_counters": ctypes.c_size_t, "lga_q4f_workspace_bytes": ctypes.c_size_t, "lga_last_error_string": ctypes.c_char_p, "lga_attention_workspace_bytes": ctypes.c_size_t,
              "lga_comm_mailbox_bytes": ctypes.c_size_t, "lga_q4_gemv_argmax_work_bytes": ctypes.c_size_t}

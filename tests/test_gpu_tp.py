@@ -28,7 +28,7 @@ WORKERS = Path(__file__).parent / "workers"
 MOE_GAP = 2 ** -6  # router top-k / next gap below which a step may route differently on the two sides
 
 
-def _launch(worker, nproc, args, timeout=540):
+def _launch(worker, nproc, args, timeout=540, env_extra=None):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -38,7 +38,7 @@ def _launch(worker, nproc, args, timeout=540):
     # hardware queue slots, so the ranks' flag-waiting kernels run together instead of being time-sliced by the
     # scheduler (a time-sliced peer looks like a lost one: the 5 s bound and stale-looking bursts). One process per
     # GPU, the deployment the kernels are built for, never shares the queues.
-    env = dict(os.environ, OMP_NUM_THREADS="2", GPU_MAX_HW_QUEUES="1")
+    env = dict(os.environ, OMP_NUM_THREADS="2", GPU_MAX_HW_QUEUES="1", **(env_extra or {}))
     if os.environ.get("LGA_TP_TEST_HW_QUEUES"):  # diagnostics: the queue count under which the bursts once timed out
         env["GPU_MAX_HW_QUEUES"] = os.environ["LGA_TP_TEST_HW_QUEUES"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
@@ -77,21 +77,25 @@ def test_xgmi_allreduce_late_peer_raises_on_every_rank(tmp_path):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("nproc", [2, 4, 8])
-def test_fused_gemv_allreduce_bit_exact_vs_two_launches(nproc, tmp_path):
-    """lga_q4_gemv_allreduce (row-parallel GEMV with the all-reduce in its epilogue, one launch) == lga_q4_gemv +
-    lga_allreduce_bf16 bit for bit at 2, 4 and 8 ranks: 7B / 70B-like shard shapes, int4 / nf4 / fp4, bias and
-    residual, graph-captured (mixed with plain all-reduce calls in one sequence) and back-to-back eager calls."""
+@pytest.mark.parametrize("protocol,nproc", [("flags", 2), ("flags", 4), ("flags", 8), ("tagged", 2), ("tagged", 4)])
+def test_fused_gemv_allreduce_bit_exact_vs_two_launches(protocol, nproc, tmp_path):
+    """lga_q4_gemv_allreduce (row-parallel GEMV with the all-reduce in its epilogue, one launch; "flags": the last
+    arriver sums) and lga_q4_gemv_allreduce_tagged ("tagged": every workgroup pushes granules and polls its own rows)
+    == lga_q4_gemv + lga_allreduce_bf16 bit for bit: 7B / 70B-like shard shapes, int4 / nf4 / fp4, bias and residual,
+    graph-captured (mixed with plain all-reduce calls in one sequence) and back-to-back eager calls. The tagged form
+    runs at 2 and 4 ranks here: its waiting workgroups hold CUs, and 8 ranks sharing ONE GPU can fill it with them
+    (on the deployment every rank owns its GPU; comm.XgmiAllReduce picks "flags" when ranks share a device)."""
     out = tmp_path / "status.txt"
-    _launch("gemv_allreduce_worker.py", nproc, [out], timeout=280)
+    _launch("gemv_allreduce_worker.py", nproc, [out], timeout=280, env_extra={"LGA_AR_PROTOCOL": protocol})
     print(Path(str(out) + ".trace.txt").read_text())
     assert out.read_text() == "ok", out.read_text()
 
 
 @pytest.mark.timeout(120)
-def test_fused_gemv_allreduce_late_peer_raises_on_every_rank(tmp_path):
+@pytest.mark.parametrize("protocol", ["flags", "tagged"])
+def test_fused_gemv_allreduce_late_peer_raises_on_every_rank(protocol, tmp_path):
     out = tmp_path / "status.txt"
-    _launch("gemv_allreduce_worker.py", 2, [out, "--late-peer"], timeout=100)
+    _launch("gemv_allreduce_worker.py", 2, [out, "--late-peer"], timeout=100, env_extra={"LGA_AR_PROTOCOL": protocol})
     assert out.read_text() == "ok", out.read_text()
 
 

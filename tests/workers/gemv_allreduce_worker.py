@@ -37,6 +37,9 @@ def main():
     if "--time" in sys.argv:
         return timing(c, out, world, rank)
     bad = [] if c.fused_ok else [f"start-up self-test: {c.fused_fallback}"]
+    want = os.environ.get("LGA_AR_PROTOCOL")
+    if want in ("flags", "tagged") and c.protocol != want:
+        bad.append(f"protocol {c.protocol}, asked for {want}")
     c.enable_trace(512)  # every call's protocol record, per rank (allreduce_worker.trace_report)
     # (N, K per rank, mode, bias): 7B attn.proj / mlp.proj shards at this world size, 70B-like widths, fp4 / nf4
     cases = [(4096, 4096 // world, "int4-g128", False), (4096, 11008 // world, "int4-g128", False),

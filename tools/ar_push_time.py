@@ -48,11 +48,19 @@ def main():
         flags[r * 64] = 0x7FFFFFFF
     rc = hip.hipMemcpy(ctypes.c_void_p(mbs[0]), flags.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(flags.nbytes), 1)
     assert rc == 0, rc
+    # the tagged protocol's granules from peers 1..7 in rank 0's own mailbox (both slots), tags far ahead as well
+    gran_off = 8 * 64 * 4 + 2 * 8 * cap * 2
+    gran = np.zeros((2, 8, cap // 2, 2), dtype=np.uint32)
+    gran[:, 1:, :, 1] = 0x7FFFFFFF
+    rc = hip.hipMemcpy(ctypes.c_void_p(mbs[0] + gran_off), gran.ctypes.data_as(ctypes.c_void_p),
+                       ctypes.c_size_t(gran.nbytes), 1)
+    assert rc == 0, rc
+    tagged = hasattr(lib, "lga_q4_gemv_allreduce_tagged")
     torch.cuda.synchronize()
     mb_arr = (ctypes.c_void_p * world)(*mbs)
     seq = torch.zeros(1, dtype=torch.int32, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    arrive = torch.zeros(576, dtype=torch.int32, device=dev)
+    arrive = torch.zeros(640, dtype=torch.int32, device=dev)
     n_rec = 4 * args.calls + 16
     trace = torch.zeros(n_rec, 16, dtype=torch.int64, device=dev)
     ops._check(lib.lga_comm_trace(ctypes.c_void_p(trace.data_ptr()), n_rec))
@@ -108,6 +116,12 @@ def main():
             ctypes.c_void_p(res.data_ptr()), ctypes.c_void_p(y.data_ptr()), N, K, g, 0, mb_arr, 0, world, cap,
             ctypes.c_void_p(seq.data_ptr()), ctypes.c_void_p(arrive.data_ptr()), ctypes.c_void_p(err.data_ptr()),
             st())))
+        if tagged:
+            measure(f"lga_q4_gemv_allreduce_tagged {label}", lambda: ops._check(lib.lga_q4_gemv_allreduce_tagged(
+                ctypes.c_void_p(x.data_ptr()), ctypes.c_void_p(qw.data_ptr()), ctypes.c_void_p(sc.data_ptr()), None,
+                ctypes.c_void_p(res.data_ptr()), ctypes.c_void_p(y.data_ptr()), N, K, g, 0, mb_arr, 0, world, cap,
+                ctypes.c_void_p(seq.data_ptr()), ctypes.c_void_p(arrive.data_ptr()), ctypes.c_void_p(err.data_ptr()),
+                st())))
         # the same GEMV alone (no all-reduce) for the difference
         ops.q4_gemv(x, qw, sc, N, K, g, 0, residual=res, out=y)
         torch.cuda.synchronize()

@@ -129,8 +129,9 @@ def main():
     act = torch.zeros(L * stride, device=dev, dtype=torch.bfloat16)
     ews = torch.zeros(L * Hr * splits * (hs + 4), device=dev, dtype=torch.float32)
     ctr = torch.zeros(lib.lga_e3_counter_words(L, Gr), device=dev, dtype=torch.int32)
-    err = torch.zeros(1, device=dev, dtype=torch.int32)
+    err = torch.zeros(64 + 256 * 8 * 48, device=dev, dtype=torch.int32)  # word 0: error bits; then per-wave records
     n_cu = ops.num_cus()
+    assert Hr == Gr, "the lab engine covers one query head per group"
     print(f"{args.geom}: rank H={Hr} G={Gr} I={Ir} Kp={Kp} splits={splits} rows/unit {ru} units {units} "
           f"LDS {lib.lga_e3_lds_bytes()} B, {n_cu} CUs", flush=True)
 
@@ -142,14 +143,15 @@ def main():
                              ctypes.c_void_p(act.data_ptr()), ctypes.c_longlong(stride), IA(*offs),
                              ctypes.c_void_p(ews.data_ptr()), ctypes.c_void_p(ctr.data_ptr()),
                              ctypes.c_void_p(err.data_ptr()), ctypes.c_float(1e-5), ctypes.c_float(scale), compute)
-        return buf
+        return torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).to(dev)  # the kernel reads Args from HBM
 
     bufs = {1: make_args(1), 0: make_args(0)}
 
     def f_engine(compute=1):
         def run():
             ctr.zero_()
-            rc = lib.lga_e3_launch(bufs[compute], n_cu, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+            rc = lib.lga_e3_launch(ctypes.c_void_p(bufs[compute].data_ptr()), n_cu,
+                                   ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
             assert rc == 0, rc
         return run
 
@@ -162,11 +164,34 @@ def main():
         if args.floor:
             t.setdefault("engine floor", []).append(time_graph(f_engine(0), L))
         torch.cuda.synchronize()
-        assert int(err.item()) == 0, f"engine error word {int(err.item()):#x}"
+        if int(err[0].item()) != 0:
+            dump(err)
     for k, v in t.items():
         print(f"{args.geom} {k:14s} " + " ".join(f"{x:6.2f}" for x in v) + f"  us/layer (best {min(v):.2f})",
               flush=True)
     print(f"{args.geom} engine / per-op = {min(t['engine']) / min(t['per-op']):.3f}", flush=True)
+
+
+def dump(err):
+    """Print the engine's timeout records (engine3.hip dbg) and stop."""
+    e = err.cpu().numpy().astype("int64")
+    recs = e[64:].reshape(256, 8, 48)
+    names = {1: "claimer queue", 2: "loader queue", 4: "loader FREE", 8: "wait_done", 16: "staged", 32: "wait_full",
+             64: "desc"}
+    shown = 0
+    from collections import Counter
+    print(f"engine error bits {int(e[0]):#x}; timeouts by kind:",
+          dict(Counter(names.get(int(c), c) for c in recs[:, :, 0].ravel() if c)), flush=True)
+    for cu in range(256):
+        for w in range(8):
+            r = recs[cu, w]
+            if r[0] and shown < 12:
+                shown += 1
+                print(f"cu {cu} wave {w} {names.get(int(r[0]), r[0])}: ctx {r[1]} {r[2]} {r[3]} | staged {r[4]} "
+                      f"gather {r[5]} edge {r[6]} desc_seq {r[7]} cq {r[8]}/{r[9]} gathering {r[10]} | "
+                      f"full {r[12:20].tolist()} freed {r[20:28].tolist()} acc_w {[hex(x) for x in r[28:36]]} "
+                      f"acc_n {r[36:44].tolist()}", flush=True)
+    raise SystemExit(1)
 
 
 def check(run, W, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, err):
@@ -175,7 +200,8 @@ def check(run, W, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, 
     kc0, vc0 = w["kc"].clone(), w["vc"].clone()
     run()
     torch.cuda.synchronize()
-    assert int(err.item()) == 0, f"engine error word {int(err.item()):#x}"
+    if int(err[0].item()) != 0:
+        dump(err)
     a = act[:stride]
     e_qkv, e_y, e_xp, e_g, e_xo = (a[offs[i]:offs[i] + n] for i, n in enumerate((Nq, Kp, C, Ir, C)))
 

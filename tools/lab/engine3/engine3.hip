@@ -26,6 +26,8 @@
 
 namespace e3 {
 
+extern __shared__ __attribute__((aligned(16))) unsigned char e3_smem[];
+
 constexpr int NS = 8;             // ring slots
 constexpr int SLOT = 17408;       // bytes per slot
 constexpr int NCONS = 3;          // consumer waves
@@ -116,7 +118,13 @@ __device__ __forceinline__ u32x4 ld128_wt(const void* p, unsigned off) {
   return __builtin_amdgcn_raw_buffer_load_b128(rsrc(p, 0x7FFFFFFF), off, 0, 16);
 }
 __device__ __forceinline__ unsigned ld_ctr(const unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// the chip-wide completion counts: returning system-scope adds (polled from every XCD by ld_ctr); a no-return
+// agent-scope add polled this way lost counts (round 6 lab: 477-492 of 512 seen, flushes all made)
+__device__ __forceinline__ void add_done(unsigned* p, unsigned v) {
+  const unsigned old = __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("" ::"v"(old));
 }
 __device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -158,17 +166,44 @@ struct Ctl {
   int gather_op;             // op a consumer is gathering (lock)
   int gathering;             // the loader thins its stream while set
   int edge_ok;               // last op known complete chip-wide
+  int ru[5], units[5];       // Args::ru / Args::units (indexed at run time)
 };
 constexpr int LDS_RING = 0;
 constexpr int LDS_XIN = NS * SLOT;
 constexpr int LDS_CTL = LDS_XIN + MAXK * 2;
 constexpr int LDS_TOTAL = LDS_CTL + (int)sizeof(Ctl);
 static_assert(LDS_TOTAL <= 163840, "LDS budget");
+// diagnostics on a timeout: the wave's record in err[64 + (cu * 8 + wave) * 32 ...]: code, three context values, then
+// a snapshot of the CU's control words
+__device__ __forceinline__ void dbg(const Args& a, const Ctl* c, unsigned code, int v0, int v1, int v2) {
+  if ((threadIdx.x & 63) != 0) return;
+  unsigned* r = a.err + 64 + ((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 48;
+  const volatile Ctl* v = (const volatile Ctl*)c;
+  r[0] = code; r[1] = (unsigned)v0; r[2] = (unsigned)v1; r[3] = (unsigned)v2;
+  r[4] = (unsigned)v->staged_op; r[5] = (unsigned)v->gather_op; r[6] = (unsigned)v->edge_ok; r[7] = v->desc_seq;
+  r[8] = v->cq_push; r[9] = v->cq_pop; r[10] = (unsigned)v->gathering;
+  for (int i = 0; i < NS; ++i) { r[12 + i] = v->full[i]; r[20 + i] = v->freed[i]; }
+  for (int i = 0; i < NACC; ++i) { r[28 + i] = v->acc_w[i]; r[36 + i] = v->acc_n[i]; }
+}
+__device__ __forceinline__ int ru_of(const Args&, int k) {
+  return __builtin_amdgcn_readfirstlane(((volatile Ctl*)(e3_smem + LDS_CTL))->ru[k]);
+}
+__device__ __forceinline__ int units_of(const Args&, int k) {
+  return __builtin_amdgcn_readfirstlane(((volatile Ctl*)(e3_smem + LDS_CTL))->units[k]);
+}
 
-__device__ __forceinline__ unsigned vload(const unsigned* p) { return *(const volatile unsigned*)p; }
-__device__ __forceinline__ int vloadi(const int* p) { return *(const volatile int*)p; }
+// LDS control words are the same for every lane: read once, made wave-uniform (scalar registers), so control flow on
+// them is scalar and nothing derived from them (layer pointers, offsets) turns into per-lane vector loads
+__device__ __forceinline__ unsigned vload(const unsigned* p) {
+  return __builtin_amdgcn_readfirstlane(*(const volatile unsigned*)p);
+}
+__device__ __forceinline__ int vloadi(const int* p) { return (int)__builtin_amdgcn_readfirstlane((unsigned)*(const volatile int*)p); }
 
 __device__ __forceinline__ int op_kind(int op) { return op % 5; }
+// per-kind fields from an LDS copy (a runtime index into the kernel-argument struct would copy the whole struct to
+// scratch and turn every field read into a vector memory load)
+__device__ __forceinline__ int ru_of(const Args&, int k);
+__device__ __forceinline__ int units_of(const Args&, int k);
 
 // units of op in shard sh: [U sh / NSH, U (sh + 1) / NSH)
 __device__ __forceinline__ void shard_range(int U, int sh, int& b, int& e) {
@@ -198,13 +233,13 @@ __device__ __forceinline__ int unit_fills(const Args& a, int op, int u, long p) 
 
 // ---------------------------------------------------------------------------------------------------------------
 // claimer (wave 0): walks the ops in order, claims units from its XCD's head, queues them for the loader
-__device__ void claimer(const Args& a, Ctl* c, int lane) {
+__device__ __forceinline__ void claimer(const Args& a, Ctl* c, int lane) {
   const int sh = blockIdx.x % NSH;
   const int nops = 5 * a.L;
   unsigned push = 0;
   for (int op = 0; op < nops; ++op) {
     int b, e;
-    shard_range(a.units[op_kind(op)], sh, b, e);
+    shard_range(units_of(a, op_kind(op)), sh, b, e);
     while (true) {
       unsigned v = 0;
       if (lane == 0 && b < e) v = __hip_atomic_fetch_add(claim_ctr(a, op, sh), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -215,7 +250,7 @@ __device__ void claimer(const Args& a, Ctl* c, int lane) {
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
       while ((int)(push - vload(&c->cq_pop)) >= NCQ) {
         __builtin_amdgcn_s_sleep(1);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) { if (lane == 0) atomicOr(a.err, 1u); return; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) { if (lane == 0) atomicOr(a.err, 1u); dbg(a, c, 1, op, push, u); return; }
       }
       if (lane == 0) {
         int* q = c->cq[push % NCQ];
@@ -247,10 +282,6 @@ __device__ void claimer(const Args& a, Ctl* c, int lane) {
 
 // ---------------------------------------------------------------------------------------------------------------
 // loader (wave 1): for every claimed unit, a descriptor, then its fills by LDS-DMA
-struct Fill {  // issue bookkeeping of the fills in flight
-  int idx[4];
-  int ins[4];
-};
 
 // DMA the bytes of one fill: chunk range A (16-B chunks) then dword range B, into slot base `lds`; returns
 // the number of DMA instructions issued
@@ -268,33 +299,30 @@ __device__ __forceinline__ int dma_fill(const uint8_t* A, int nA16, const uint8_
   return ins;
 }
 
-__device__ void loader(const Args& a, Ctl* c, unsigned char* smem, int lane) {
+__device__ __forceinline__ void loader(const Args& a, Ctl* c, unsigned char* smem, int lane) {
   const long p = a.pos[0];
   const unsigned ring = (unsigned)(uintptr_t)(smem + LDS_RING);
   unsigned pop = 0, dseq = 0;
   int fill = 0;
-  int nin = 0;  // fills in flight (issued, not yet published)
-  Fill fl;
+  int nin = 0;  // fills in flight (issued, not yet published): their indices f0 < f1 < f2, DMA instruction counts n0..n2
+  int f0 = 0, f1 = 0, f2 = 0, n1 = 0, n2 = 0;
   int cur_op = -1, claimed = 0;
-  auto publish_oldest = [&](int keep_ins) {
-    // the oldest fill in flight lands once vmcnt <= instructions issued after it
-    wait_vm(keep_ins);
-    if (lane == 0) __hip_atomic_store(&c->full[fl.idx[0] % NS], (unsigned)fl.idx[0] + 1u, __ATOMIC_RELAXED,
+  // the oldest fill in flight has landed once vmcnt <= the instructions issued after it (vmcnt retires in order)
+  auto publish_oldest = [&]() {
+    wait_vm(nin == 3 ? n1 + n2 : (nin == 2 ? n1 : 0));
+    if (lane == 0) __hip_atomic_store(&c->full[f0 % NS], (unsigned)f0 + 1u, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_WORKGROUP);
-    for (int k = 0; k < 3; ++k) { fl.idx[k] = fl.idx[k + 1]; fl.ins[k] = fl.ins[k + 1]; }
+    f0 = f1;
+    f1 = f2;
+    n1 = n2;
     --nin;
-  };
-  auto ins_after_oldest = [&]() {
-    int s = 0;
-    for (int k = 1; k < nin; ++k) s += fl.ins[k];
-    return s;
   };
   while (true) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (vload(&c->cq_push) == pop) {
-      if (nin > 0) publish_oldest(ins_after_oldest());  // nothing to issue: publish what landed
+      if (nin > 0) publish_oldest();  // nothing to issue: publish what landed
       else __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) { if (lane == 0) atomicOr(a.err, 2u); return; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) { if (lane == 0) atomicOr(a.err, 2u); dbg(a, c, 2, pop, fill, dseq); return; }
     }
     const int* q = c->cq[pop % NCQ];
     const int op = vloadi(&q[0]), u0 = vloadi(&q[1]), n = vloadi(&q[2]);
@@ -307,18 +335,20 @@ __device__ void loader(const Args& a, Ctl* c, unsigned char* smem, int lane) {
         c->acc_w[op % NACC] = 0;
         c->acc_n[op % NACC] = 0;
       }
+      asm volatile("" ::: "memory");
     }
     if (op < 0 || n == 0) {  // op exhausted (or the end): close its accounting
       if (op >= 0 && op_kind(op) != OA) {
         unsigned old = 0;
         if (lane == 0) {
           c->acc_n[op % NACC] = (unsigned)claimed;
+          // hipcc may sink a plain store below a relaxed atomic: a consumer seeing FLAG would read a stale count
+          asm volatile("" ::: "memory");
           old = atomicAdd(&c->acc_w[op % NACC], FLAG);
         }
         old = __builtin_amdgcn_readfirstlane(old);
         if (old == (unsigned)claimed && claimed > 0 && lane == 0)  // every claimed unit already finished
-          __hip_atomic_fetch_add(done_ctr(a, op, blockIdx.x % NSH), (unsigned)claimed, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+          add_done(done_ctr(a, op, blockIdx.x % NSH), (unsigned)claimed);
       }
       if (op < 0) break;
       continue;
@@ -343,13 +373,13 @@ __device__ void loader(const Args& a, Ctl* c, unsigned char* smem, int lane) {
         const unsigned need = (unsigned)max(fill - NS + 1, 0);
         const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
         while (vload(&c->freed[fill % NS]) < need) {
-          if (nin > 0) publish_oldest(ins_after_oldest());
+          if (nin > 0) publish_oldest();
           else __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_s_memrealtime() - t1 > TMO) { if (lane == 0) atomicOr(a.err, 4u); return; }
+          if (__builtin_amdgcn_s_memrealtime() - t1 > TMO) { if (lane == 0) atomicOr(a.err, 4u); dbg(a, c, 4, fill, op, u); return; }
         }
         // keep at most 3 fills in flight (1 while a consumer of this CU gathers an op input)
         const int maxin = vloadi(&c->gathering) ? 1 : 3;
-        while (nin >= maxin) publish_oldest(ins_after_oldest());
+        while (nin >= maxin) publish_oldest();
         const unsigned slot = ring + (unsigned)((fill % NS) * SLOT);
         const Layer& ly = a.layers[op / 5];
         int ins;
@@ -363,7 +393,7 @@ __device__ void loader(const Args& a, Ctl* c, unsigned char* smem, int lane) {
           ins = dma_fill(kr, nk * HS * 2 / 16, nullptr, 0, slot, lane);
           ins += dma_fill(vr, nk * HS * 2 / 16, nullptr, 0, slot + KEYS * HS * 2, lane);
         } else {
-          const int N = gemv_rows(a, kind), K = gemv_k(a, kind), G = gemv_g(a, kind), R = a.ru[kind];
+          const int N = gemv_rows(a, kind), K = gemv_k(a, kind), G = gemv_g(a, kind), R = ru_of(a, kind);
           const int r0 = u * R, nr = min(R, N - r0);
           const uint8_t* W = kind == OQ ? ly.wq : kind == OP ? ly.wp : kind == OF ? ly.wf1 : ly.wd;
           const uint16_t* Sc = kind == OQ ? ly.sq : kind == OP ? ly.sp : kind == OF ? ly.sf1 : ly.sd;
@@ -381,14 +411,16 @@ __device__ void loader(const Args& a, Ctl* c, unsigned char* smem, int lane) {
                             slot + (unsigned)(R * K / 2), lane);
           }
         }
-        fl.idx[nin] = fill;
-        fl.ins[nin] = ins;
+        ins = __builtin_amdgcn_readfirstlane(ins);
+        if (nin == 0) f0 = fill;
+        else if (nin == 1) { f1 = fill; n1 = ins; }
+        else { f2 = fill; n2 = ins; }
         ++nin;
         ++fill;
       }
     }
   }
-  while (nin > 0) publish_oldest(ins_after_oldest());
+  while (nin > 0) publish_oldest();
   // one end descriptor per consumer
   for (int k = 0; k < NCONS; ++k) {
     if (lane == 0) {
@@ -406,9 +438,9 @@ __device__ void loader(const Args& a, Ctl* c, unsigned char* smem, int lane) {
 // consumers (waves 2..4)
 
 // chip-wide completion of op (its done counters reach the op's total)
-__device__ bool wait_done(const Args& a, Ctl* c, int op, int lane) {
+__device__ __forceinline__ bool wait_done(const Args& a, Ctl* c, int op, int lane) {
   if (op < 0 || vloadi(&c->edge_ok) >= op) return true;
-  const unsigned total = op_kind(op) == OA ? (unsigned)a.G : (unsigned)a.units[op_kind(op)];
+  const unsigned total = op_kind(op) == OA ? (unsigned)a.G : (unsigned)units_of(a, op_kind(op));
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (true) {
     unsigned v = lane < NSH ? ld_ctr(done_ctr(a, op, lane)) : 0u;
@@ -419,6 +451,7 @@ __device__ bool wait_done(const Args& a, Ctl* c, int op, int lane) {
     __builtin_amdgcn_s_sleep(2);
     if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) {
       if (lane == 0) atomicOr(a.err, 8u);
+      dbg(a, c, 8, op, (int)v, (int)total);
       return false;
     }
   }
@@ -427,7 +460,7 @@ __device__ bool wait_done(const Args& a, Ctl* c, int op, int lane) {
 }
 
 // the input vector of a GEMV op into LDS (bf16), RMS-normalised for the qkv and fc ops
-__device__ void gather(const Args& a, Ctl* c, unsigned char* smem, int op, int lane) {
+__device__ __forceinline__ void gather(const Args& a, Ctl* c, unsigned char* smem, int op, int lane) {
   const int kind = op_kind(op), layer = op / 5;
   const uint16_t* src;
   const uint16_t* nw = nullptr;
@@ -488,7 +521,7 @@ __device__ void gather(const Args& a, Ctl* c, unsigned char* smem, int op, int l
 }
 
 // make the input of op available in LDS (returns false on a timeout)
-__device__ bool ensure_input(const Args& a, Ctl* c, unsigned char* smem, int op, int lane) {
+__device__ __forceinline__ bool ensure_input(const Args& a, Ctl* c, unsigned char* smem, int op, int lane) {
   const int kind = op_kind(op);
   if (kind == OA) return wait_done(a, c, op - 1, lane);  // q / k / v rows: read per unit
   if (vloadi(&c->staged_op) == op) return true;
@@ -516,6 +549,7 @@ __device__ bool ensure_input(const Args& a, Ctl* c, unsigned char* smem, int op,
     __builtin_amdgcn_s_sleep(1);
     if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) {
       if (lane == 0) atomicOr(a.err, 16u);
+      dbg(a, c, 16, op, vloadi(&c->staged_op), 0);
       return false;
     }
   }
@@ -523,12 +557,13 @@ __device__ bool ensure_input(const Args& a, Ctl* c, unsigned char* smem, int op,
   return true;
 }
 
-__device__ bool wait_full(const Ctl* c, int fill, const Args& a, int lane) {
+__device__ __forceinline__ bool wait_full(const Ctl* c, int fill, const Args& a, int lane) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (vload(&c->full[fill % NS]) < (unsigned)fill + 1u) {
     __builtin_amdgcn_s_sleep(0);
     if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) {
       if (lane == 0) atomicOr(a.err, 32u);
+      dbg(a, (const Ctl*)c, 32, fill, (int)vload(&c->full[fill % NS]), 0);
       return false;
     }
   }
@@ -542,13 +577,12 @@ __device__ __forceinline__ void release(Ctl* c, int fill, int lane) {
 }
 
 // one finished unit of a GEMV op: this CU's count; the last of the CU's claimed units adds them chip-wide
-__device__ void account(const Args& a, Ctl* c, int op, int lane) {
+__device__ __forceinline__ void account(const Args& a, Ctl* c, int op, int lane) {
   unsigned old = 0;
   if (lane == 0) old = atomicAdd(&c->acc_w[op % NACC], 1u);
   old = __builtin_amdgcn_readfirstlane(old);
   if ((old & FLAG) && (old & (FLAG - 1)) + 1u == vload(&c->acc_n[op % NACC]) && lane == 0)
-    __hip_atomic_fetch_add(done_ctr(a, op, blockIdx.x % NSH), vload(&c->acc_n[op % NACC]), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    add_done(done_ctr(a, op, blockIdx.x % NSH), vload(&c->acc_n[op % NACC]));
 }
 
 // 32 weights (16 B, byte j = elements 2j | 2j+1 << 4) . 32 x (bf16 in LDS) with the nibble offset 8 folded in
@@ -570,9 +604,9 @@ __device__ __forceinline__ float chunk_dot(const u32x4 w, const float (&xf)[32],
   return fmaf(-8.0f, xsum, d);
 }
 
-__device__ void gemv_unit(const Args& a, unsigned char* smem, int op, int u, int fill, int lane) {
+__device__ __forceinline__ void gemv_unit(const Args& a, unsigned char* smem, int op, int u, int fill, int lane) {
   const int kind = op_kind(op), layer = op / 5;
-  const int N = gemv_rows(a, kind), K = gemv_k(a, kind), G = gemv_g(a, kind), R = a.ru[kind];
+  const int N = gemv_rows(a, kind), K = gemv_k(a, kind), G = gemv_g(a, kind), R = ru_of(a, kind);
   const int r0 = u * R, nr = min(R, N - r0);
   const int NC = K / 32, gpr = K / G;
   const unsigned char* slot = smem + LDS_RING + (fill % NS) * SLOT;
@@ -642,8 +676,9 @@ __device__ void gemv_unit(const Args& a, unsigned char* smem, int op, int u, int
 
 // attention unit (query group g, split s): online softmax over the split's cache keys in the ring, the new key p
 // from the qkv row, then the publish / last-arriver combine of the per-op kernel
-__device__ void attn_unit(const Args& a, unsigned char* smem, int op, int u, int fill0, int nf, int lane) {
-  const int layer = op / 5, g = u / a.splits, s = u % a.splits, QPK = a.H / a.G;
+__device__ __forceinline__ void attn_unit(const Args& a, unsigned char* smem, int op, int u, int fill0, int nf, int lane) {
+  const int layer = op / 5, g = u / a.splits, s = u % a.splits;
+  constexpr int QPK = 1;  // lab build: one query head per group (Llama-2-7B and its TP ranks); the host checks
   const long p = a.pos[0];
   int lo, hi;
   split_range(a, p, s, lo, hi);
@@ -654,7 +689,7 @@ __device__ void attn_unit(const Args& a, unsigned char* smem, int op, int u, int
   const int key = lane >> 1, half = lane & 1;
   float m[4], l[4], o0[4], o1[4];
   uint32_t q[4][32];  // this lane's half (64 dims) of each head's q, bf16 pairs
-  for (int h = 0; h < QPK && h < 4; ++h) {
+  for (int h = 0; h < QPK; ++h) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const u32x4 v = ld128_wt(qkv, (unsigned)((h * HS + half * 64 + k * 8) * 2));
@@ -669,7 +704,7 @@ __device__ void attn_unit(const Args& a, unsigned char* smem, int op, int u, int
   }
   typedef short s2 __attribute__((ext_vector_type(2)));
   auto step = [&](const unsigned char* kb, const unsigned char* vb, int nk) {
-    for (int h = 0; h < QPK && h < 4; ++h) {
+    for (int h = 0; h < QPK; ++h) {
       float d = 0.0f;
       const unsigned char* kr = kb + (size_t)key * HS * 2 + half * 128;
 #pragma unroll
@@ -715,7 +750,7 @@ __device__ void attn_unit(const Args& a, unsigned char* smem, int op, int u, int
       *(u32x4*)(ly.vc + ((size_t)g * a.S + p) * HS + lane * 8) = vv;
     }
     if (a.compute) {
-      for (int h = 0; h < QPK && h < 4; ++h) {
+      for (int h = 0; h < QPK; ++h) {
         float d = 0.0f;
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
@@ -739,7 +774,7 @@ __device__ void attn_unit(const Args& a, unsigned char* smem, int op, int u, int
   }
   // publish this split's (m, l, o) per head: [layer][head][split][HS + 4]
   float* wsl = a.ws + (size_t)layer * a.H * a.splits * (HS + 4);
-  for (int h = 0; h < QPK && h < 4; ++h) {
+  for (int h = 0; h < QPK; ++h) {
     float* pr = wsl + ((size_t)(g * QPK + h) * a.splits + s) * (HS + 4);
     const uint32_t oo[2] = {__float_as_uint(o0[h]), __float_as_uint(o1[h])};
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, oo),
@@ -755,7 +790,7 @@ __device__ void attn_unit(const Args& a, unsigned char* smem, int op, int u, int
   t = __builtin_amdgcn_readfirstlane(t);
   if (t != (unsigned)(a.splits - 1)) return;
   // the last split of the group: merge every split (lane owns dims 2 lane, 2 lane + 1) and hand y over
-  for (int h = 0; h < QPK && h < 4; ++h) {
+  for (int h = 0; h < QPK; ++h) {
     const float* base = wsl + (size_t)(g * QPK + h) * a.splits * (HS + 4);
     float mx = -INFINITY;
     for (int k = 0; k < a.splits; ++k) {
@@ -777,16 +812,17 @@ __device__ void attn_unit(const Args& a, unsigned char* smem, int op, int u, int
                                           (unsigned)(((g * QPK + h) * HS + 2 * lane) * 2), 0, 16);
   }
   drain();
-  if (lane == 0) __hip_atomic_fetch_add(done_ctr(a, op, 0), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0) add_done(done_ctr(a, op, 0), 1u);
 }
 
-__device__ void consumer(const Args& a, Ctl* c, unsigned char* smem, int ci, int lane) {
+__device__ __forceinline__ void consumer(const Args& a, Ctl* c, unsigned char* smem, int ci, int lane) {
   for (unsigned d = (unsigned)ci;; d += NCONS) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (vload(&c->desc_seq) <= d) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) {
         if (lane == 0) atomicOr(a.err, 64u);
+        dbg(a, c, 64, (int)d, (int)vload(&c->desc_seq), 0);
         return;
       }
     }
@@ -807,15 +843,20 @@ __device__ void consumer(const Args& a, Ctl* c, unsigned char* smem, int ci, int
   }
 }
 
-__global__ void __launch_bounds__(NT) engine3_kernel(Args a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+__global__ void __launch_bounds__(NT) engine3_kernel(const Args* __restrict__ ap) {
+  const Args& a = *ap;  // read through the scalar cache (a by-value struct argument would be copied to scratch)
+  unsigned char* smem = e3_smem;
   Ctl* c = (Ctl*)(smem + LDS_CTL);
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += NT) ((unsigned*)c)[i] = 0u;
+  __syncthreads();
   if (threadIdx.x == 0) {
     c->staged_op = -1;
     c->gather_op = -1;
     c->edge_ok = -1;
+    c->ru[0] = a.ru[0]; c->ru[1] = a.ru[1]; c->ru[2] = a.ru[2]; c->ru[3] = a.ru[3]; c->ru[4] = a.ru[4];
+    c->units[0] = a.units[0]; c->units[1] = a.units[1]; c->units[2] = a.units[2]; c->units[3] = a.units[3];
+    c->units[4] = a.units[4];
   }
   __syncthreads();
   const int w = __builtin_amdgcn_readfirstlane(wave);
@@ -831,16 +872,14 @@ extern "C" int lga_e3_counter_words(int L, int G) { return (10 * L * e3::NSH + L
 extern "C" int lga_e3_args_bytes() { return (int)sizeof(e3::Args); }
 extern "C" int lga_e3_layer_bytes() { return (int)sizeof(e3::Layer); }
 
-// args: a host copy of e3::Args (the caller fills it through lga_e3_fill_args); grid = the CU count
-extern "C" int lga_e3_launch(const void* args_host, int n_cu, hipStream_t stream) {
+// args_dev: a device copy of e3::Args (the caller fills it through lga_e3_fill_args and copies it); grid = the CU count
+extern "C" int lga_e3_launch(const void* args_dev, int n_cu, hipStream_t stream) {
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)e3::engine3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, e3::LDS_TOTAL);
     attr = true;
   }
-  e3::Args a;
-  memcpy(&a, args_host, sizeof(a));
-  e3::engine3_kernel<<<n_cu, e3::NT, e3::LDS_TOTAL, stream>>>(a);
+  e3::engine3_kernel<<<n_cu, e3::NT, e3::LDS_TOTAL, stream>>>((const e3::Args*)args_dev);
   return (int)hipGetLastError();
 }
 
