@@ -245,8 +245,8 @@ int lga_q4_gemv_allreduce(const void* x, const uint8_t* qweight, const void* sca
                           unsigned* err, lga_stream_t stream);
 /* The same call in the tagged protocol (generate/tp.py:73-74 on multi-GPU ranks): every workgroup pushes its rows as
  * 8-byte {bf16 pair, call sequence} granules into every rank's mailbox and polls its own rows from every rank — no
- * arrival counters, flags or last-arriver sum; identical result bits. arrive_counter: 640 uint32 (word 576 is the
- * monotonic launch counter the sequence derives from, zeroed once); seq_counter unused. The grid need not be
+ * arrival counters, flags or last-arriver sum; identical result bits. arrive_counter: 640 uint32 (words 576 / 608:
+ * the launch's arrivals and the rank's call count the sequence derives from, zeroed once); seq_counter unused. The grid need not be
  * co-resident (a workgroup waits only for other ranks). Same mailboxes: lga_comm_mailbox_bytes covers both regions. */
 int lga_q4_gemv_allreduce_tagged(const void* x, const uint8_t* qweight, const void* scales, const void* bias,
                                  const void* residual, void* y, int N, int K, int group, int fmt,

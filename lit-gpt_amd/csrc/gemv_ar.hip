@@ -112,9 +112,11 @@ __global__ void __launch_bounds__(256) gemv_q4_ar_kernel(GemvArgs a, ArArgs c) {
 // instead of the drain + arrival chain + system-scope fences + one workgroup summing all N rows (measured in one
 // process with the peers' flags pre-set: 10.9-11.0 us per call at the 7B TP = 8 rank's shapes against 2.6 us for the
 // GEMV alone, profiles/r06_allreduce_push_single_process.txt).
-// The call sequence is derived without a shared counter: every workgroup adds 1 to a monotonic launch counter and
-// takes old / grid + 1 (launches on one stream do not overlap, so every workgroup of a launch gets the same value;
-// graph replays keep counting). A granule slot is the sequence's parity, as in the flag protocol: a rank is at most
+// The call sequence: every workgroup reads the rank's launch index at its start (+ 1 = this call's sequence) and,
+// once its pushes are out, arrives on a counter; the last arriver re-arms that counter and advances the index. Every
+// workgroup of the launch has started (and read the index) before the last one arrives, and launches on one stream
+// do not overlap, so all of a launch's workgroups agree on the sequence and graph replays keep counting. (An
+// old / grid division of one shared counter breaks as soon as two calls have different grids.) A granule slot is the sequence's parity, as in the flag protocol: a rank is at most
 // one call ahead of a peer, because its call s + 1 needed the peer's call-s granules, which the peer pushed only
 // after its call s - 1 had finished reading that slot. Every workgroup waits only for OTHER ranks, never for a
 // workgroup of its own launch, so the grid need not be co-resident; the poll is bounded (5 s, then the error word).
@@ -126,7 +128,8 @@ __device__ __forceinline__ unsigned char* granule_ptr(unsigned char* mb, int slo
 struct ArtArgs {
   unsigned char* mb[kMaxRanks];
   int rank, world, cap;
-  unsigned* launch_ctr;
+  unsigned* arrive;      // arrivals of this launch (re-armed by the last arriver)
+  unsigned* launch_idx;  // calls completed by this rank (monotonic)
   unsigned* err;
   const uint16_t* residual;
   uint16_t* y;
@@ -140,8 +143,8 @@ __global__ void __launch_bounds__(256) gemv_q4_art_kernel(GemvArgs a, ArtArgs c)
   __shared__ unsigned s_seq;
   __shared__ __attribute__((aligned(16))) uint4 s_in[kMaxRanks][NP];
   const int t = threadIdx.x;
-  if (t == 0) s_seq = __hip_atomic_fetch_add(c.launch_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) /
-                      gridDim.x + 1u;  // lands while the weights stream
+  if (t == 0)  // lands while the weights stream
+    s_seq = __hip_atomic_fetch_add(c.launch_idx, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   gemv_q4_body<RPR, CPT, FMT, false, false, false, NW, true>(a, blockIdx.x, smem);
   __syncthreads();
   const unsigned seq = __builtin_amdgcn_readfirstlane(s_seq);
@@ -156,6 +159,13 @@ __global__ void __launch_bounds__(256) gemv_q4_art_kernel(GemvArgs a, ArtArgs c)
     for (int r = 0; r < c.world; ++r) {  // one peer per iteration: the resource stays wave-uniform
       const __amdgpu_buffer_rsrc_t dst = mb_rsrc(granule_ptr(c.mb[r], slot, c.rank, c.cap), c.cap * 4);
       st_sys16(dst, (row0 / 4 + t) * 16, piece);
+    }
+  }
+  // the launch bookkeeping (off the data path: its latency overlaps the poll below)
+  if (t == 64) {
+    if (__hip_atomic_fetch_add(c.arrive, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1) {
+      __hip_atomic_store(c.arrive, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(c.launch_idx, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   // 2. poll this workgroup's pieces from every rank in the own mailbox (lane t: rank t / NP, piece t % NP)
@@ -305,8 +315,8 @@ extern "C" int lga_q4_gemv_allreduce(const void* x, const uint8_t* qweight, cons
   LGA_LAUNCH_RETURN();
 }
 
-// The tagged form of lga_q4_gemv_allreduce (same arguments and result bits): arrive_counter's word 9 * 64 is the
-// monotonic launch counter the call sequence derives from (zeroed once, never re-armed); seq_counter is not used
+// The tagged form of lga_q4_gemv_allreduce (same arguments and result bits): arrive_counter's words 9 * 64 (this
+// launch's arrivals, re-armed) and 9 * 64 + 32 (calls completed, monotonic; zeroed once); seq_counter is not used
 // (the tagged protocol has its own mailbox region, so its calls and the flag protocol's may be mixed).
 extern "C" int lga_q4_gemv_allreduce_tagged(const void* x, const uint8_t* qweight, const void* scales,
                                             const void* bias, const void* residual, void* y, int N, int K, int group,
@@ -333,7 +343,8 @@ extern "C" int lga_q4_gemv_allreduce_tagged(const void* x, const uint8_t* qweigh
   c.rank = rank;
   c.world = world;
   c.cap = cap;
-  c.launch_ctr = arrive_counter + 9 * lga::kArriveStride;
+  c.arrive = arrive_counter + 9 * lga::kArriveStride;
+  c.launch_idx = arrive_counter + 9 * lga::kArriveStride + 32;
   c.err = err;
   c.residual = (const uint16_t*)residual;
   c.y = (uint16_t*)y;

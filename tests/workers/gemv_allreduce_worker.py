@@ -40,6 +40,14 @@ def main():
     want = os.environ.get("LGA_AR_PROTOCOL")
     if want in ("flags", "tagged") and c.protocol != want:
         bad.append(f"protocol {c.protocol}, asked for {want}")
+    if bad:  # a broken protocol would make every later call wait out its 5 s bound: report and stop here
+        dist.barrier()
+        c.close()
+        if rank == 0:
+            Path(out).write_text(f"FAIL {bad}")
+            Path(out + ".trace.txt").write_text("")
+        dist.destroy_process_group()
+        return
     c.enable_trace(512)  # every call's protocol record, per rank (allreduce_worker.trace_report)
     # (N, K per rank, mode, bias): 7B attn.proj / mlp.proj shards at this world size, 70B-like widths, fp4 / nf4
     cases = [(4096, 4096 // world, "int4-g128", False), (4096, 11008 // world, "int4-g128", False),

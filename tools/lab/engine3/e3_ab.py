@@ -191,6 +191,20 @@ def dump(err):
                       f"gather {r[5]} edge {r[6]} desc_seq {r[7]} cq {r[8]}/{r[9]} gathering {r[10]} | "
                       f"full {r[12:20].tolist()} freed {r[20:28].tolist()} acc_w {[hex(x) for x in r[28:36]]} "
                       f"acc_n {r[36:44].tolist()}", flush=True)
+    # per-op accounting across CUs (any wave's snapshot of the CU): claimed units, finished units, closed or not
+    for slot in range(8):
+        n_sum = fin = closed = incons = 0
+        for cu in range(256):
+            r = next((recs[cu, w] for w in range(8) if recs[cu, w, 0]), None)
+            if r is None:
+                continue
+            w_, n_ = int(r[28 + slot]), int(r[36 + slot])
+            n_sum += n_
+            fin += w_ & 0xFFFFFF
+            closed += bool(w_ & 0x1000000)
+            incons += bool(w_ & 0x1000000) and (w_ & 0xFFFFFF) != n_
+        print(f"acc slot {slot}: claimed {n_sum}, finished {fin}, closed on {closed} CUs, count != claimed on {incons}",
+              flush=True)
     raise SystemExit(1)
 
 
