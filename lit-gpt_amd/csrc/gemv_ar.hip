@@ -104,7 +104,7 @@ __global__ void __launch_bounds__(256) gemv_q4_ar_kernel(GemvArgs a, ArArgs c) {
 
 // ---------------------------------------------------------------------------------------------------------------
 // Tagged form (lga_q4_gemv_allreduce_tagged): no arrival counters, no flags, no last-arriver sum. Every workgroup
-// pushes its rows into every rank's mailbox as 8-byte granules {bf16 pair, call sequence} (one 16-B system-coherent
+// pushes its rows into every peer's mailbox as 8-byte granules {bf16 pair, call sequence} (one 16-B system-coherent
 // store carries two; MI355X_MICROARCH.md "handoff-1to1": the data is its own flag), then polls its OWN rows'
 // granules from every rank in its own mailbox and writes those rows of y — the ordered fp32 sum over ranks 0..W-1,
 // bf16 once, + residual: ordered_sum8's arithmetic, so the bits equal lga_q4_gemv + lga_allreduce_bf16. The
@@ -157,9 +157,11 @@ __global__ void __launch_bounds__(256) gemv_q4_art_kernel(GemvArgs a, ArtArgs c)
     const uint2 rv = ((const uint2*)rows)[t];
     const uint4 piece = make_uint4(rv.x, seq, rv.y, seq);
     for (int r = 0; r < c.world; ++r) {  // one peer per iteration: the resource stays wave-uniform
+      if (r == c.rank) continue;           // the own rows stay in LDS (no round trip through the own mailbox)
       const __amdgpu_buffer_rsrc_t dst = mb_rsrc(granule_ptr(c.mb[r], slot, c.rank, c.cap), c.cap * 4);
       st_sys16(dst, (row0 / 4 + t) * 16, piece);
     }
+    s_in[c.rank][t] = piece;
   }
   // the launch bookkeeping (off the data path: its latency overlaps the poll below)
   if (t == 64) {
@@ -171,7 +173,7 @@ __global__ void __launch_bounds__(256) gemv_q4_art_kernel(GemvArgs a, ArtArgs c)
   // 2. poll this workgroup's pieces from every rank in the own mailbox (lane t: rank t / NP, piece t % NP)
   if (t < 64) {
     const int r = t / NP, p = t % NP;
-    const bool mine = r < c.world && p < np;
+    const bool mine = r < c.world && r != c.rank && p < np;
     __amdgpu_buffer_rsrc_t src[kMaxRanks];
 #pragma unroll
     for (int k = 0; k < kMaxRanks; ++k)

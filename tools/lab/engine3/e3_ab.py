@@ -129,7 +129,7 @@ def main():
     act = torch.zeros(L * stride, device=dev, dtype=torch.bfloat16)
     ews = torch.zeros(L * Hr * splits * (hs + 4), device=dev, dtype=torch.float32)
     ctr = torch.zeros(lib.lga_e3_counter_words(L, Gr), device=dev, dtype=torch.int32)
-    err = torch.zeros(64 + 256 * 8 * 48, device=dev, dtype=torch.int32)  # word 0: error bits; then per-wave records
+    err = torch.zeros(64 + 256 * 8 * 128, device=dev, dtype=torch.int32)  # word 0: error bits; then per-wave records
     n_cu = ops.num_cus()
     assert Hr == Gr, "the lab engine covers one query head per group"
     print(f"{args.geom}: rank H={Hr} G={Gr} I={Ir} Kp={Kp} splits={splits} rows/unit {ru} units {units} "
@@ -175,7 +175,7 @@ def main():
 def dump(err):
     """Print the engine's timeout records (engine3.hip dbg) and stop."""
     e = err.cpu().numpy().astype("int64")
-    recs = e[64:].reshape(256, 8, 48)
+    recs = e[64:].reshape(256, 8, 128)
     names = {1: "claimer queue", 2: "loader queue", 4: "loader FREE", 8: "wait_done", 16: "staged", 32: "wait_full",
              64: "desc"}
     shown = 0
@@ -205,6 +205,22 @@ def dump(err):
             incons += bool(w_ & 0x1000000) and (w_ & 0xFFFFFF) != n_
         print(f"acc slot {slot}: claimed {n_sum}, finished {fin}, closed on {closed} CUs, count != claimed on {incons}",
               flush=True)
+        if incons and slot == 7:
+            shown = 0
+            for cu in range(256):
+                r = next((recs[cu, w] for w in range(8) if recs[cu, w, 0]), None)
+                if r is None or not (int(r[28 + slot]) & 0x1000000) or (int(r[28 + slot]) & 0xFFFFFF) == int(r[36 + slot]):
+                    continue
+                if shown < 4:
+                    shown += 1
+                    ds = int(r[7])
+                    print(f"  cu {cu}: desc_seq {ds}, consumers at descs {r[44:47].tolist()}; ring (desc: op/unit) " +
+                          " ".join(f"{d}:{int(r[48 + d % 32])}/{int(r[80 + d % 32])}" for d in range(max(0, ds - 32), ds)),
+                          flush=True)
+                    for w in range(8):
+                        rw = recs[cu, w]
+                        if rw[0]:
+                            print(f"    wave {w} {names.get(int(rw[0]), rw[0])} ctx {rw[1]} {rw[2]} {rw[3]}", flush=True)
     raise SystemExit(1)
 
 

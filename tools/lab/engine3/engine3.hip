@@ -167,37 +167,51 @@ struct Ctl {
   int gathering;             // the loader thins its stream while set
   int edge_ok;               // last op known complete chip-wide
   int ru[5], units[5];       // Args::ru / Args::units (indexed at run time)
+  int cur_d[NCONS];          // diagnostics: the descriptor each consumer is on
 };
 constexpr int LDS_RING = 0;
 constexpr int LDS_XIN = NS * SLOT;
-constexpr int LDS_CTL = LDS_XIN + MAXK * 2;
-constexpr int LDS_TOTAL = LDS_CTL + (int)sizeof(Ctl);
-static_assert(LDS_TOTAL <= 163840, "LDS budget");
+constexpr int LDS_TOTAL = LDS_XIN + MAXK * 2;  // dynamic LDS: the ring and the staged input (Ctl is static LDS)
+// Ctl as a static __shared__ object: every access to it is a DS instruction. Reached through a pointer into the
+// dynamic area, hipcc emitted FLAT loads / stores for the volatile control words, which do not complete in order with
+// the DS ones — a descriptor's fields could land after its sequence word (round 6 lab: units lost on 8 CUs).
+__shared__ Ctl e3_ctl;
+typedef __attribute__((address_space(3))) Ctl CtlL;
+typedef __attribute__((address_space(3))) unsigned lu32;
+typedef __attribute__((address_space(3))) int li32;
+static_assert(LDS_TOTAL + sizeof(Ctl) <= 163840, "LDS budget");
 // diagnostics on a timeout: the wave's record in err[64 + (cu * 8 + wave) * 32 ...]: code, three context values, then
 // a snapshot of the CU's control words
-__device__ __forceinline__ void dbg(const Args& a, const Ctl* c, unsigned code, int v0, int v1, int v2) {
+__device__ __forceinline__ void dbg(const Args& a, const CtlL* c, unsigned code, int v0, int v1, int v2) {
   if ((threadIdx.x & 63) != 0) return;
-  unsigned* r = a.err + 64 + ((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 48;
-  const volatile Ctl* v = (const volatile Ctl*)c;
+  unsigned* r = a.err + 64 + ((size_t)blockIdx.x * 8 + (threadIdx.x >> 6)) * 128;
+  const volatile CtlL* v = (const volatile CtlL*)c;
   r[0] = code; r[1] = (unsigned)v0; r[2] = (unsigned)v1; r[3] = (unsigned)v2;
   r[4] = (unsigned)v->staged_op; r[5] = (unsigned)v->gather_op; r[6] = (unsigned)v->edge_ok; r[7] = v->desc_seq;
   r[8] = v->cq_push; r[9] = v->cq_pop; r[10] = (unsigned)v->gathering;
   for (int i = 0; i < NS; ++i) { r[12 + i] = v->full[i]; r[20 + i] = v->freed[i]; }
   for (int i = 0; i < NACC; ++i) { r[28 + i] = v->acc_w[i]; r[36 + i] = v->acc_n[i]; }
+  for (int i = 0; i < NCONS; ++i) r[44 + i] = (unsigned)v->cur_d[i];
+  for (int i = 0; i < NDESC; ++i) { r[48 + i] = (unsigned)v->desc[i][0]; r[80 + i] = (unsigned)v->desc[i][1]; }
 }
+__device__ __forceinline__ unsigned vload(const lu32* p) {
+  return __builtin_amdgcn_readfirstlane(*(const volatile lu32*)p);
+}
+__device__ __forceinline__ int vloadi(const li32* p) {
+  return (int)__builtin_amdgcn_readfirstlane((unsigned)*(const volatile li32*)p);
+}
+__device__ __forceinline__ void lst(lu32* p, unsigned v) { *(volatile lu32*)p = v; }
+__device__ __forceinline__ void lsti(li32* p, int v) { *(volatile li32*)p = v; }
 __device__ __forceinline__ int ru_of(const Args&, int k) {
-  return __builtin_amdgcn_readfirstlane(((volatile Ctl*)(e3_smem + LDS_CTL))->ru[k]);
+  return vloadi(&((CtlL*)&e3_ctl)->ru[k]);
 }
 __device__ __forceinline__ int units_of(const Args&, int k) {
-  return __builtin_amdgcn_readfirstlane(((volatile Ctl*)(e3_smem + LDS_CTL))->units[k]);
+  return vloadi(&((CtlL*)&e3_ctl)->units[k]);
 }
 
 // LDS control words are the same for every lane: read once, made wave-uniform (scalar registers), so control flow on
 // them is scalar and nothing derived from them (layer pointers, offsets) turns into per-lane vector loads
-__device__ __forceinline__ unsigned vload(const unsigned* p) {
-  return __builtin_amdgcn_readfirstlane(*(const volatile unsigned*)p);
-}
-__device__ __forceinline__ int vloadi(const int* p) { return (int)__builtin_amdgcn_readfirstlane((unsigned)*(const volatile int*)p); }
+
 
 __device__ __forceinline__ int op_kind(int op) { return op % 5; }
 // per-kind fields from an LDS copy (a runtime index into the kernel-argument struct would copy the whole struct to
@@ -233,7 +247,7 @@ __device__ __forceinline__ int unit_fills(const Args& a, int op, int u, long p) 
 
 // ---------------------------------------------------------------------------------------------------------------
 // claimer (wave 0): walks the ops in order, claims units from its XCD's head, queues them for the loader
-__device__ __forceinline__ void claimer(const Args& a, Ctl* c, int lane) {
+__device__ __forceinline__ void claimer(const Args& a, CtlL* c, int lane) {
   const int sh = blockIdx.x % NSH;
   const int nops = 5 * a.L;
   unsigned push = 0;
@@ -253,7 +267,7 @@ __device__ __forceinline__ void claimer(const Args& a, Ctl* c, int lane) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) { if (lane == 0) atomicOr(a.err, 1u); dbg(a, c, 1, op, push, u); return; }
       }
       if (lane == 0) {
-        int* q = c->cq[push % NCQ];
+        li32* q = c->cq[push % NCQ];
         q[0] = op;
         q[1] = last ? -1 : u;
         q[2] = last ? 0 : 1;
@@ -270,7 +284,7 @@ __device__ __forceinline__ void claimer(const Args& a, Ctl* c, int lane) {
     if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) { if (lane == 0) atomicOr(a.err, 1u); return; }
   }
   if (lane == 0) {
-    int* q = c->cq[push % NCQ];
+    li32* q = c->cq[push % NCQ];
     q[0] = -1;
     q[1] = -1;
     q[2] = 0;
@@ -299,7 +313,7 @@ __device__ __forceinline__ int dma_fill(const uint8_t* A, int nA16, const uint8_
   return ins;
 }
 
-__device__ __forceinline__ void loader(const Args& a, Ctl* c, unsigned char* smem, int lane) {
+__device__ __forceinline__ void loader(const Args& a, CtlL* c, unsigned char* smem, int lane) {
   const long p = a.pos[0];
   const unsigned ring = (unsigned)(uintptr_t)(smem + LDS_RING);
   unsigned pop = 0, dseq = 0;
@@ -324,7 +338,7 @@ __device__ __forceinline__ void loader(const Args& a, Ctl* c, unsigned char* sme
       else __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) { if (lane == 0) atomicOr(a.err, 2u); dbg(a, c, 2, pop, fill, dseq); return; }
     }
-    const int* q = c->cq[pop % NCQ];
+    const li32* q = c->cq[pop % NCQ];
     const int op = vloadi(&q[0]), u0 = vloadi(&q[1]), n = vloadi(&q[2]);
     ++pop;
     if (lane == 0) __hip_atomic_store(&c->cq_pop, pop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -344,7 +358,7 @@ __device__ __forceinline__ void loader(const Args& a, Ctl* c, unsigned char* sme
           c->acc_n[op % NACC] = (unsigned)claimed;
           // hipcc may sink a plain store below a relaxed atomic: a consumer seeing FLAG would read a stale count
           asm volatile("" ::: "memory");
-          old = atomicAdd(&c->acc_w[op % NACC], FLAG);
+          old = __hip_atomic_fetch_add(&c->acc_w[op % NACC], FLAG, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         old = __builtin_amdgcn_readfirstlane(old);
         if (old == (unsigned)claimed && claimed > 0 && lane == 0)  // every claimed unit already finished
@@ -358,7 +372,7 @@ __device__ __forceinline__ void loader(const Args& a, Ctl* c, unsigned char* sme
       const int nf = unit_fills(a, op, u, p);
       // descriptor (the consumer of dseq % NCONS); the slot ring bounds how far ahead descriptors can get
       if (lane == 0) {
-        int* d = c->desc[dseq % NDESC];
+        li32* d = c->desc[dseq % NDESC];
         d[0] = op;
         d[1] = u;
         d[2] = fill;
@@ -424,7 +438,7 @@ __device__ __forceinline__ void loader(const Args& a, Ctl* c, unsigned char* sme
   // one end descriptor per consumer
   for (int k = 0; k < NCONS; ++k) {
     if (lane == 0) {
-      int* d = c->desc[dseq % NDESC];
+      li32* d = c->desc[dseq % NDESC];
       d[0] = -1;
       d[1] = d[2] = d[3] = 0;
     }
@@ -438,7 +452,7 @@ __device__ __forceinline__ void loader(const Args& a, Ctl* c, unsigned char* sme
 // consumers (waves 2..4)
 
 // chip-wide completion of op (its done counters reach the op's total)
-__device__ __forceinline__ bool wait_done(const Args& a, Ctl* c, int op, int lane) {
+__device__ __forceinline__ bool wait_done(const Args& a, CtlL* c, int op, int lane) {
   if (op < 0 || vloadi(&c->edge_ok) >= op) return true;
   const unsigned total = op_kind(op) == OA ? (unsigned)a.G : (unsigned)units_of(a, op_kind(op));
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -455,12 +469,12 @@ __device__ __forceinline__ bool wait_done(const Args& a, Ctl* c, int op, int lan
       return false;
     }
   }
-  if (lane == 0) atomicMax(&c->edge_ok, op);
+  if (lane == 0) __hip_atomic_fetch_max(&c->edge_ok, op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   return true;
 }
 
 // the input vector of a GEMV op into LDS (bf16), RMS-normalised for the qkv and fc ops
-__device__ __forceinline__ void gather(const Args& a, Ctl* c, unsigned char* smem, int op, int lane) {
+__device__ __forceinline__ void gather(const Args& a, CtlL* c, unsigned char* smem, int op, int lane) {
   const int kind = op_kind(op), layer = op / 5;
   const uint16_t* src;
   const uint16_t* nw = nullptr;
@@ -521,7 +535,7 @@ __device__ __forceinline__ void gather(const Args& a, Ctl* c, unsigned char* sme
 }
 
 // make the input of op available in LDS (returns false on a timeout)
-__device__ __forceinline__ bool ensure_input(const Args& a, Ctl* c, unsigned char* smem, int op, int lane) {
+__device__ __forceinline__ bool ensure_input(const Args& a, CtlL* c, unsigned char* smem, int op, int lane) {
   const int kind = op_kind(op);
   if (kind == OA) return wait_done(a, c, op - 1, lane);  // q / k / v rows: read per unit
   if (vloadi(&c->staged_op) == op) return true;
@@ -529,7 +543,9 @@ __device__ __forceinline__ bool ensure_input(const Args& a, Ctl* c, unsigned cha
   int got = 0;
   if (lane == 0) {
     const int prev = vloadi(&c->gather_op);
-    got = prev < op && atomicCAS(&c->gather_op, prev, op) == prev;
+    int expect = prev;
+    got = prev < op && __hip_atomic_compare_exchange_strong(&c->gather_op, &expect, op, __ATOMIC_RELAXED,
+                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   got = __builtin_amdgcn_readfirstlane(got);
   if (got) {
@@ -557,29 +573,29 @@ __device__ __forceinline__ bool ensure_input(const Args& a, Ctl* c, unsigned cha
   return true;
 }
 
-__device__ __forceinline__ bool wait_full(const Ctl* c, int fill, const Args& a, int lane) {
+__device__ __forceinline__ bool wait_full(const CtlL* c, int fill, const Args& a, int lane) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
   while (vload(&c->full[fill % NS]) < (unsigned)fill + 1u) {
     __builtin_amdgcn_s_sleep(0);
     if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) {
       if (lane == 0) atomicOr(a.err, 32u);
-      dbg(a, (const Ctl*)c, 32, fill, (int)vload(&c->full[fill % NS]), 0);
+      dbg(a, c, 32, fill, (int)vload(&c->full[fill % NS]), 0);
       return false;
     }
   }
   asm volatile("" ::: "memory");  // no slot read may move above the poll
   return true;
 }
-__device__ __forceinline__ void release(Ctl* c, int fill, int lane) {
+__device__ __forceinline__ void release(CtlL* c, int fill, int lane) {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of the slot has returned
   if (lane == 0) __hip_atomic_store(&c->freed[fill % NS], (unsigned)fill + 1u, __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // one finished unit of a GEMV op: this CU's count; the last of the CU's claimed units adds them chip-wide
-__device__ __forceinline__ void account(const Args& a, Ctl* c, int op, int lane) {
+__device__ __forceinline__ void account(const Args& a, CtlL* c, int op, int lane) {
   unsigned old = 0;
-  if (lane == 0) old = atomicAdd(&c->acc_w[op % NACC], 1u);
+  if (lane == 0) old = __hip_atomic_fetch_add(&c->acc_w[op % NACC], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   old = __builtin_amdgcn_readfirstlane(old);
   if ((old & FLAG) && (old & (FLAG - 1)) + 1u == vload(&c->acc_n[op % NACC]) && lane == 0)
     add_done(done_ctr(a, op, blockIdx.x % NSH), vload(&c->acc_n[op % NACC]));
@@ -734,12 +750,12 @@ __device__ __forceinline__ void attn_unit(const Args& a, unsigned char* smem, in
   };
   for (int f = 0; f < nf; ++f) {
     const int fill = fill0 + f;
-    const Ctl* c = (const Ctl*)(smem + LDS_CTL);
+    CtlL* c = (CtlL*)&e3_ctl;
     if (!wait_full(c, fill, a, lane)) return;
     const unsigned char* slot = smem + LDS_RING + (fill % NS) * SLOT;
     const int nk = min(KEYS, min(hi, (int)p) - (lo + f * KEYS));
     if (a.compute) step(slot, slot + KEYS * HS * 2, nk);
-    release((Ctl*)(smem + LDS_CTL), fill, lane);
+    release(c, fill, lane);
   }
   if (lo <= p && p < hi) {  // the new key: appended to the cache (un-rotated in this lab build) and scored
     const uint16_t* kn = qkv + QPK * HS;
@@ -815,7 +831,7 @@ __device__ __forceinline__ void attn_unit(const Args& a, unsigned char* smem, in
   if (lane == 0) add_done(done_ctr(a, op, 0), 1u);
 }
 
-__device__ __forceinline__ void consumer(const Args& a, Ctl* c, unsigned char* smem, int ci, int lane) {
+__device__ __forceinline__ void consumer(const Args& a, CtlL* c, unsigned char* smem, int ci, int lane) {
   for (unsigned d = (unsigned)ci;; d += NCONS) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (vload(&c->desc_seq) <= d) {
@@ -827,7 +843,8 @@ __device__ __forceinline__ void consumer(const Args& a, Ctl* c, unsigned char* s
       }
     }
     asm volatile("" ::: "memory");
-    const int* ds = c->desc[d % NDESC];
+    if (lane == 0) lsti(&c->cur_d[ci], (int)d);
+    const li32* ds = c->desc[d % NDESC];
     const int op = vloadi(&ds[0]), u = vloadi(&ds[1]), fill = vloadi(&ds[2]), nf = vloadi(&ds[3]);
     if (op < 0) return;
     if (!ensure_input(a, c, smem, op, lane)) return;
@@ -846,7 +863,7 @@ __device__ __forceinline__ void consumer(const Args& a, Ctl* c, unsigned char* s
 __global__ void __launch_bounds__(NT) engine3_kernel(const Args* __restrict__ ap) {
   const Args& a = *ap;  // read through the scalar cache (a by-value struct argument would be copied to scratch)
   unsigned char* smem = e3_smem;
-  Ctl* c = (Ctl*)(smem + LDS_CTL);
+  CtlL* c = (CtlL*)&e3_ctl;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (int i = threadIdx.x; i < (int)(sizeof(Ctl) / 4); i += NT) ((unsigned*)c)[i] = 0u;
   __syncthreads();
