@@ -539,7 +539,10 @@ __device__ __forceinline__ bool ensure_input(const Args& a, CtlL* c, unsigned ch
   const int kind = op_kind(op);
   if (kind == OA) return wait_done(a, c, op - 1, lane);  // q / k / v rows: read per unit
   if (vloadi(&c->staged_op) == op) return true;
-  // a lock word: the consumer that moves gather_op to op gathers; the others wait for staged_op
+  // every consumer that needs op waits for the previous op chip-wide BEFORE it competes for the gather lock: a
+  // consumer that took the lock for op + 1 and then waited would block this CU's consumer of op, whose input then is
+  // never staged (round 6 lab: the lock went 5 -> 8 past a CU's only P unit, and op 7 never completed)
+  if (!wait_done(a, c, op - 1, lane)) return false;
   int got = 0;
   if (lane == 0) {
     const int prev = vloadi(&c->gather_op);
@@ -549,13 +552,12 @@ __device__ __forceinline__ bool ensure_input(const Args& a, CtlL* c, unsigned ch
   }
   got = __builtin_amdgcn_readfirstlane(got);
   if (got) {
-    if (!wait_done(a, c, op - 1, lane)) return false;
-    if (lane == 0) c->gathering = 1;
+    if (lane == 0) lsti(&c->gathering, 1);
     gather(a, c, smem, op, lane);
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (lane == 0) {
-      c->gathering = 0;
+      lsti(&c->gathering, 0);
       __hip_atomic_store(&c->staged_op, op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     return true;
