@@ -17,6 +17,7 @@ import math
 import sys
 from pathlib import Path
 
+import numpy as np
 import torch
 
 REPO = Path(__file__).resolve().parents[3]
@@ -72,6 +73,9 @@ def main():
     ap.add_argument("--pos", type=int, default=2200)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--floor", action="store_true")
+    ap.add_argument("--trace", action="store_true", help="per-op event times of one launch (static ranges)")
+    ap.add_argument("--lib", default="liblga_engine3.so", help="engine build under tools/_ab (slot / consumer count)")
+    ap.add_argument("--esplits", type=int, default=1, help="the engine's attention splits = this x the product's")
     args = ap.parse_args()
     dev = torch.device("cuda")
     C, H, G, I, tp = GEOMS[args.geom]
@@ -108,7 +112,11 @@ def main():
             ops.q4_gemv(g, *w["down"][:2], C, Ir, w["down"][2], 0, residual=o, out=x)
 
     # ---- the engine ----
-    lib = ctypes.CDLL(str(REPO / "tools" / "_ab" / "liblga_engine3.so"))
+    lib = ctypes.CDLL(str(REPO / "tools" / "_ab" / args.lib))
+    global SLOT
+    SLOT = lib.lga_e3_slot_bytes()
+    ncons = lib.lga_e3_consumers()
+    esplits = splits * args.esplits
     lib.lga_e3_launch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
     assert lib.lga_e3_layer_bytes() == 14 * 8
     ptrs = []
@@ -121,31 +129,39 @@ def main():
     gq, gp, gi = W[0]["qkv"][2], W[0]["proj"][2], W[0]["down"][2]
     ru = [rows_per_unit(C, gq, False), 0, rows_per_unit(Kp, gp, False), rows_per_unit(C, gq, True),
           rows_per_unit(Ir, gi, False)]
-    units = [-(-Nq // ru[0]), Gr * splits, -(-C // ru[2]), -(-Ir // ru[3]), -(-C // ru[4])]
+    units = [-(-Nq // ru[0]), Gr * esplits, -(-C // ru[2]), -(-Ir // ru[3]), -(-C // ru[4])]
     offs = [0]
     for n in (Nq, Kp, C, Ir):
         offs.append(offs[-1] + ((n + 63) // 64) * 64)
     stride = offs[-1] + ((C + 63) // 64) * 64
     act = torch.zeros(L * stride, device=dev, dtype=torch.bfloat16)
-    ews = torch.zeros(L * Hr * splits * (hs + 4), device=dev, dtype=torch.float32)
+    ews = torch.zeros(L * Hr * esplits * (hs + 4), device=dev, dtype=torch.float32)
     ctr = torch.zeros(lib.lga_e3_counter_words(L, Gr), device=dev, dtype=torch.int32)
     err = torch.zeros(64 + 256 * 8 * 128, device=dev, dtype=torch.int32)  # word 0: error bits; then per-wave records
     n_cu = ops.num_cus()
     assert Hr == Gr, "the lab engine covers one query head per group"
     print(f"{args.geom}: rank H={Hr} G={Gr} I={Ir} Kp={Kp} splits={splits} rows/unit {ru} units {units} "
-          f"LDS {lib.lga_e3_lds_bytes()} B, {n_cu} CUs", flush=True)
+          f"LDS {lib.lga_e3_lds_bytes()} B, {n_cu} CUs; engine: {args.lib} slot {SLOT} B, {ncons} consumers, "
+          f"{esplits} splits", flush=True)
 
-    def make_args(compute):
+    trace = torch.zeros(256 + 5 * L * n_cu * 32, device=dev, dtype=torch.int64)
+
+    def make_args(compute, traced=False):
         buf = ctypes.create_string_buffer(lib.lga_e3_args_bytes())
         IA = ctypes.c_int * 5
-        lib.lga_e3_fill_args(buf, ctypes.c_void_p(layers_dev.data_ptr()), L, C, Hr, Gr, Ir, Kp, S, splits, gq, gp, gi,
+        lib.lga_e3_fill_args(buf, ctypes.c_void_p(layers_dev.data_ptr()), L, C, Hr, Gr, Ir, Kp, S, esplits, gq, gp, gi,
                              IA(*ru), IA(*units), Nq, ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(x0.data_ptr()),
                              ctypes.c_void_p(act.data_ptr()), ctypes.c_longlong(stride), IA(*offs),
                              ctypes.c_void_p(ews.data_ptr()), ctypes.c_void_p(ctr.data_ptr()),
-                             ctypes.c_void_p(err.data_ptr()), ctypes.c_float(1e-5), ctypes.c_float(scale), compute)
+                             ctypes.c_void_p(err.data_ptr()), ctypes.c_float(1e-5), ctypes.c_float(scale), compute,
+                             ctypes.c_void_p(trace.data_ptr() if traced else 0))
         return torch.frombuffer(bytearray(buf.raw), dtype=torch.uint8).to(dev)  # the kernel reads Args from HBM
 
-    bufs = {1: make_args(1), 0: make_args(0)}
+    # compute bit 0: consumers compute; bit 1: static unit ranges (no claim atomics); 4 + bits: the same, traced
+    bufs = {m: make_args(m) for m in (0, 1, 2, 3)}
+    bufs[7] = make_args(3, traced=True)
+    bufs[5] = make_args(1, traced=True)
+    bufs[6] = make_args(2, traced=True)
 
     def f_engine(compute=1):
         def run():
@@ -156,20 +172,64 @@ def main():
         return run
 
     if args.check:
-        check(f_engine(1), W, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, err)
+        for m in (1, 3):
+            print(f"-- check, {'static ranges' if m & 2 else 'dynamic claims'}", flush=True)
+            try:
+                check(f_engine(m), W, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, err, ews, L)
+            except AssertionError as e:
+                print(f"check FAILED at {e}", flush=True)
+    if args.trace:
+        for m, name in ((7, "static ranges"), (6, "static ranges, consumers computing nothing (floor)"),
+                        (5, "dynamic claims")):
+            for _ in range(3):  # warm
+                f_engine(m)()
+            torch.cuda.synchronize()
+            trace.zero_()
+            f_engine(m)()
+            torch.cuda.synchronize()
+            if int(err[0].item()) != 0:
+                dump(err)
+            show_trace(trace.cpu().numpy(), L, n_cu, name, ncons)
     t = {}
     for r in range(3):
         t.setdefault("per-op", []).append(time_graph(f_layer, L))
         t.setdefault("engine", []).append(time_graph(f_engine(1), L))
+        t.setdefault("engine static", []).append(time_graph(f_engine(3), L))
         if args.floor:
             t.setdefault("engine floor", []).append(time_graph(f_engine(0), L))
+            t.setdefault("static floor", []).append(time_graph(f_engine(2), L))
         torch.cuda.synchronize()
         if int(err[0].item()) != 0:
             dump(err)
     for k, v in t.items():
         print(f"{args.geom} {k:14s} " + " ".join(f"{x:6.2f}" for x in v) + f"  us/layer (best {min(v):.2f})",
               flush=True)
-    print(f"{args.geom} engine / per-op = {min(t['engine']) / min(t['per-op']):.3f}", flush=True)
+    print(f"{args.geom} engine / per-op = {min(t['engine']) / min(t['per-op']):.3f}, "
+          f"static {min(t['engine static']) / min(t['per-op']):.3f}", flush=True)
+
+
+def show_trace(tr, L, n_cu, name, ncons):
+    """Per op of the middle layers, times (us) relative to the op's edge E = the last consumer end of the previous
+    op on any CU: median / max over CUs of each event, and the op's span E(op + 1) - E(op)."""
+    ev = tr[256:].reshape(5 * L, n_cu, 32).astype(np.float64) / 100.0  # 100 MHz -> us
+    t0 = tr[:n_cu].astype(np.float64).min() / 100.0
+    S0, E0 = 6, 6 + ncons
+    ends = np.where(ev[:, :, E0:E0 + ncons] > 0, ev[:, :, E0:E0 + ncons], 0).max(axis=2)  # [op][cu] last end
+    E = ends.max(axis=1)  # op complete (approx.: last consumer end)
+    kinds = "QAPFD"
+    print(f"trace ({name}): launch span {E[-1] - t0:.1f} us for {L} layers; per op of layers {L // 2 - 1}-{L // 2}, "
+          f"us relative to the previous op's completion (median / max over CUs; '-' no CU recorded it)", flush=True)
+    cols = ["claim0", "claim1", "load0", "load1", "edge", "staged", "start", "end"]
+    print("op      span  " + "  ".join(f"{c:>13s}" for c in cols), flush=True)
+    for op in range(5 * (L // 2 - 1), 5 * (L // 2 + 1)):
+        Eprev = E[op - 1]
+        starts = np.where(ev[op, :, S0:E0] > 0, ev[op, :, S0:E0], np.inf).min(axis=1)
+        vals = [ev[op, :, 0], ev[op, :, 1], ev[op, :, 2], ev[op, :, 3], ev[op, :, 4], ev[op, :, 5], starts, ends[op]]
+        cells = []
+        for v in vals:
+            v = v[(v > 0) & np.isfinite(v)]
+            cells.append("-" if v.size == 0 else f"{np.median(v) - Eprev:6.2f}/{v.max() - Eprev:6.2f}")
+        print(f"{op // 5:2d}{kinds[op % 5]}  {E[op] - Eprev:7.2f}  " + "  ".join(f"{c:>13s}" for c in cells), flush=True)
 
 
 def dump(err):
@@ -224,10 +284,19 @@ def dump(err):
     raise SystemExit(1)
 
 
-def check(run, W, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, err):
+def check(run, W, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, err, ews, L_):
     """Layer 0 of the engine against references of the same math."""
     w = W[0]
     kc0, vc0 = w["kc"].clone(), w["vc"].clone()
+    try:
+        _check(run, w, kc0, vc0, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, err, ews, L_)
+    finally:
+        w["kc"].copy_(kc0)
+        w["vc"].copy_(vc0)
+
+
+def _check(run, w, kc0, vc0, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, err, ews, L_):
+    failed = []
     run()
     torch.cuda.synchronize()
     if int(err[0].item()) != 0:
@@ -237,8 +306,9 @@ def check(run, W, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, 
 
     def rel(got, want, name, tol):
         d = (got.float() - want.float()).abs().max().item() / max(want.float().abs().max().item(), 1e-6)
-        print(f"check {name:5s}: max rel err {d:.2e}", flush=True)
-        assert d <= tol, name
+        print(f"check {name:5s}: max rel err {d:.2e}" + ("" if d <= tol else "  FAILED"), flush=True)
+        if d > tol:
+            failed.append(name)
 
     r_qkv = ops.q4_gemv(x0, *w["qkv"][:2], Nq, C, w["qkv"][2], 0, norm_weight=w["n1"])
     rel(e_qkv, r_qkv, "qkv", 2e-2)
@@ -253,6 +323,54 @@ def check(run, W, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, 
         gi = h // qpk
         s = kc[gi, :pos + 1] @ t[gi, h % qpk] * scale
         yr[h] = torch.softmax(s, 0) @ vc[gi, :pos + 1]
+    d = (e_y.float().view(Hr, hs) - yr).abs().amax(1) / yr.abs().amax(1).clamp_min(1e-6)
+    ratio = e_y.float().view(Hr, hs).norm(dim=1) / yr.norm(dim=1)
+    print(f"attn per head rel err {[round(x, 3) for x in d.tolist()[:8]]} ... norm ratio "
+          f"{[round(x, 3) for x in ratio.tolist()[:8]]}", flush=True)
+    # which wrong computation does the engine's y match? (diagnostics for a failing attention check)
+    if (e_y.float().view(Hr, hs) - yr).abs().max() > 2e-2 * yr.abs().max():
+        ey = e_y.float().view(Hr, hs)
+
+        def variant(fn):
+            out = torch.empty(Hr, hs, device=act.device)
+            for h in range(Hr):
+                out[h] = fn(h // qpk, t[h // qpk, h % qpk])
+            return ((ey - out).abs().amax(1) / out.abs().amax(1).clamp_min(1e-6)).median().item()
+        n = pos + 1
+        cand = {
+            "V rows shifted +1": lambda gi, q: torch.softmax(kc[gi, :n] @ q * scale, 0)[:-1] @ vc[gi, 1:n],
+            "V rows shifted -1": lambda gi, q: torch.softmax(kc[gi, :n] @ q * scale, 0)[1:] @ vc[gi, :n - 1],
+            "no new key": lambda gi, q: torch.softmax(kc[gi, :pos] @ q * scale, 0) @ vc[gi, :pos],
+            "scale 1": lambda gi, q: torch.softmax(kc[gi, :n] @ q, 0) @ vc[gi, :n],
+            "uniform": lambda gi, q: vc[gi, :n].mean(0),
+            "scale x2": lambda gi, q: torch.softmax(kc[gi, :n] @ q * scale * 2, 0) @ vc[gi, :n],
+            "scale /2": lambda gi, q: torch.softmax(kc[gi, :n] @ q * scale / 2, 0) @ vc[gi, :n],
+            "K of group g+1": lambda gi, q: torch.softmax(kc[(gi + 1) % Gr, :n] @ q * scale, 0) @ vc[gi, :n],
+            "V of group g+1": lambda gi, q: torch.softmax(kc[gi, :n] @ q * scale, 0) @ vc[(gi + 1) % Gr, :n],
+        }
+        for k, fn in cand.items():
+            print(f"  attn vs '{k}': median per-head rel err {variant(fn):.3f}", flush=True)
+        print(f"  reference per-head rel err median {d.median().item():.3f}", flush=True)
+        # per split: the engine's published (m, l, o) of layer 0 against the split's own attention
+        nsp = ews.numel() // (L_ * Hr * (hs + 4))
+        part = ews[:Hr * nsp * (hs + 4)].view(Hr, nsp, hs + 4)
+        L1 = pos + 1
+        chunk = -(-L1 // nsp)
+        l2e = 1.4426950408889634
+        for h in range(min(Hr, 2)):
+            gi = h // qpk
+            for sp in range(nsp):
+                lo, hi = min(sp * chunk, L1), min(sp * chunk + chunk, L1)
+                if hi <= lo:
+                    continue
+                sc = (kc[gi, lo:hi] @ t[gi, h % qpk]) * scale * l2e
+                m_r = sc.max()
+                e_r = torch.exp2(sc - m_r)
+                l_r, o_r = e_r.sum(), e_r @ vc[gi, lo:hi]
+                m_e, l_e, o_e = part[h, sp, 0], part[h, sp, 1], part[h, sp, 4:]
+                print(f"  head {h} split {sp} keys [{lo},{hi}): m {m_e.item():.4f}/{m_r.item():.4f} "
+                      f"l {l_e.item():.3f}/{l_r.item():.3f} o rel err "
+                      f"{((o_e - o_r).abs().max() / o_r.abs().max()).item():.3f}", flush=True)
     rel(e_y, yr.view(-1), "attn", 2e-2)
     r_xp = ops.q4_gemv(e_y.contiguous(), *w["proj"][:2], C, Kp, w["proj"][2], 0, residual=x0)
     rel(e_xp, r_xp, "proj", 2e-2)
@@ -261,8 +379,7 @@ def check(run, W, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, pos, scale, 
     rel(e_g, r_g, "fc", 3e-2)
     r_xo = ops.q4_gemv(e_g.contiguous(), *w["down"][:2], C, Ir, w["down"][2], 0, residual=e_xp.contiguous())
     rel(e_xo, r_xo, "down", 2e-2)
-    w["kc"].copy_(kc0)
-    w["vc"].copy_(vc0)
+    assert not failed, failed
 
 
 if __name__ == "__main__":

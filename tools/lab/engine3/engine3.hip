@@ -28,19 +28,26 @@ namespace e3 {
 
 extern __shared__ __attribute__((aligned(16))) unsigned char e3_smem[];
 
-constexpr int NS = 8;             // ring slots
-constexpr int SLOT = 17408;       // bytes per slot
-constexpr int NCONS = 3;          // consumer waves
+#ifndef E3_NS
+#define E3_NS 8
+#define E3_SLOT 17408
+#endif
+#ifndef E3_NCONS
+#define E3_NCONS 3
+#endif
+constexpr int NS = E3_NS;         // ring slots
+constexpr int SLOT = E3_SLOT;     // bytes per slot
+constexpr int NCONS = E3_NCONS;   // consumer waves
 constexpr int NWAVE = 2 + NCONS;  // claimer, loader, consumers
 constexpr int NT = NWAVE * 64;
 constexpr int NDESC = 32;         // descriptor ring
 constexpr int NCQ = 4;            // claim queue (entries the claimer may run ahead of the loader)
 constexpr int NSH = 8;            // claim / done shards (one per XCD under round-robin placement)
-constexpr int KEYS = 32;          // attention keys per slot (K rows, then V rows)
+constexpr int KEYS = SLOT >= 16384 ? 32 : 16;  // attention keys per slot (K rows, then V rows)
 constexpr int HS = 128;
 constexpr int MAXK = 11008;       // largest GEMV K: the input vector staged in LDS as bf16
 constexpr int CW = 16;            // uint32 words per counter (64 B)
-constexpr int NACC = 8;           // per-op accounting ring in LDS
+constexpr int NACC = 64;          // per-op accounting ring in LDS (the loader can run many small ops ahead)
 constexpr unsigned FLAG = 1u << 24;
 constexpr unsigned long long TMO = 200000000ull;  // 2 s of the 100 MHz clock: every wait is bounded
 
@@ -72,8 +79,20 @@ struct Args {
   unsigned* ctr;       // counters, zeroed before every launch
   unsigned* err;
   float eps, scale;
-  int compute;         // 0: consumers only wait / release (the transport floor)
+  int compute;         // bit 0: consumers compute (0: they only wait / release: the transport floor);
+                       // bit 1: static unit ranges (each CU its contiguous 1/n of every op, no claim atomics)
+  unsigned long long* trace;  // optional per-(op, CU) event times (TR_* below), 16 words each, after 256 start words
 };
+
+// trace events (s_memrealtime, 100 MHz), per (op, CU): claimer first claim / op exhausted, loader first / last fill
+// issued, edge seen (previous op complete chip-wide), input staged, then per consumer its first unit start and its
+// last unit end
+enum { TR_CLAIM0 = 0, TR_CLAIM1, TR_LOAD0, TR_LOAD1, TR_EDGE, TR_STAGED, TR_START = 6, TR_END = 6 + NCONS, TR_N = 32 };
+static_assert(TR_END + NCONS <= TR_N, "trace record");
+__device__ __forceinline__ void tr(const Args& a, int op, int ev, int lane) {
+  if (a.trace && lane == 0)
+    a.trace[256 + ((size_t)op * gridDim.x + blockIdx.x) * TR_N + ev] = __builtin_amdgcn_s_memrealtime();
+}
 
 // counter layout (words of CW uint32): claim heads [5L][NSH], done [5L][NSH], attention arrivals [L][G]
 __device__ __forceinline__ unsigned* claim_ctr(const Args& a, int op, int sh) { return a.ctr + ((size_t)op * NSH + sh) * CW; }
@@ -190,8 +209,8 @@ __device__ __forceinline__ void dbg(const Args& a, const CtlL* c, unsigned code,
   r[4] = (unsigned)v->staged_op; r[5] = (unsigned)v->gather_op; r[6] = (unsigned)v->edge_ok; r[7] = v->desc_seq;
   r[8] = v->cq_push; r[9] = v->cq_pop; r[10] = (unsigned)v->gathering;
   for (int i = 0; i < NS; ++i) { r[12 + i] = v->full[i]; r[20 + i] = v->freed[i]; }
-  for (int i = 0; i < NACC; ++i) { r[28 + i] = v->acc_w[i]; r[36 + i] = v->acc_n[i]; }
-  for (int i = 0; i < NCONS; ++i) r[44 + i] = (unsigned)v->cur_d[i];
+  for (int i = 0; i < 8; ++i) { r[28 + i] = v->acc_w[i]; r[36 + i] = v->acc_n[i]; }
+  for (int i = 0; i < NCONS && i < 4; ++i) r[44 + i] = (unsigned)v->cur_d[i];
   for (int i = 0; i < NDESC; ++i) { r[48 + i] = (unsigned)v->desc[i][0]; r[80 + i] = (unsigned)v->desc[i][1]; }
 }
 __device__ __forceinline__ unsigned vload(const lu32* p) {
@@ -251,13 +270,27 @@ __device__ __forceinline__ void claimer(const Args& a, CtlL* c, int lane) {
   const int sh = blockIdx.x % NSH;
   const int nops = 5 * a.L;
   unsigned push = 0;
+  const bool stat = (a.compute & 2) != 0;
   for (int op = 0; op < nops; ++op) {
     int b, e;
-    shard_range(units_of(a, op_kind(op)), sh, b, e);
+    tr(a, op, TR_CLAIM0, lane);
+    if (stat) {
+      const int U = units_of(a, op_kind(op));
+      b = (int)((long)U * blockIdx.x / gridDim.x);
+      e = (int)((long)U * (blockIdx.x + 1) / gridDim.x);
+    } else {
+      shard_range(units_of(a, op_kind(op)), sh, b, e);
+    }
+    bool once = false;
     while (true) {
       unsigned v = 0;
-      if (lane == 0 && b < e) v = __hip_atomic_fetch_add(claim_ctr(a, op, sh), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      v = __builtin_amdgcn_readfirstlane(v);
+      if (stat) {
+        v = once ? (unsigned)(e - b) : 0u;  // one record with the whole range, then the exhausted record
+        once = true;
+      } else {
+        if (lane == 0 && b < e) v = __hip_atomic_fetch_add(claim_ctr(a, op, sh), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v = __builtin_amdgcn_readfirstlane(v);
+      }
       const int u = b + (int)v;
       const bool last = b >= e || u >= e;
       // wait for a free queue entry
@@ -270,12 +303,15 @@ __device__ __forceinline__ void claimer(const Args& a, CtlL* c, int lane) {
         li32* q = c->cq[push % NCQ];
         q[0] = op;
         q[1] = last ? -1 : u;
-        q[2] = last ? 0 : 1;
+        q[2] = last ? 0 : (stat ? e - b : 1);
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       ++push;
       if (lane == 0) __hip_atomic_store(&c->cq_push, push, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (last) break;
+      if (last) {
+        tr(a, op, TR_CLAIM1, lane);
+        break;
+      }
     }
   }
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -396,6 +432,7 @@ __device__ __forceinline__ void loader(const Args& a, CtlL* c, unsigned char* sm
         while (nin >= maxin) publish_oldest();
         const unsigned slot = ring + (unsigned)((fill % NS) * SLOT);
         const Layer& ly = a.layers[op / 5];
+        if (u == u0 && f == 0 && claimed == 1) tr(a, op, TR_LOAD0, lane);
         int ins;
         if (kind == OA) {
           const int g = u / a.splits;
@@ -431,6 +468,7 @@ __device__ __forceinline__ void loader(const Args& a, CtlL* c, unsigned char* sm
         else { f2 = fill; n2 = ins; }
         ++nin;
         ++fill;
+        tr(a, op, TR_LOAD1, lane);
       }
     }
   }
@@ -469,7 +507,10 @@ __device__ __forceinline__ bool wait_done(const Args& a, CtlL* c, int op, int la
       return false;
     }
   }
-  if (lane == 0) __hip_atomic_fetch_max(&c->edge_ok, op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  int was = 0;
+  if (lane == 0) was = __hip_atomic_fetch_max(&c->edge_ok, op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  was = __builtin_amdgcn_readfirstlane(was);
+  if (was < op && op + 1 < 5 * a.L) tr(a, op + 1, TR_EDGE, lane);
   return true;
 }
 
@@ -560,6 +601,7 @@ __device__ __forceinline__ bool ensure_input(const Args& a, CtlL* c, unsigned ch
       lsti(&c->gathering, 0);
       __hip_atomic_store(&c->staged_op, op, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
+    tr(a, op, TR_STAGED, lane);
     return true;
   }
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -594,12 +636,13 @@ __device__ __forceinline__ void release(CtlL* c, int fill, int lane) {
                                     __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// one finished unit of a GEMV op: this CU's count; the last of the CU's claimed units adds them chip-wide
-__device__ __forceinline__ void account(const Args& a, CtlL* c, int op, int lane) {
+// n finished units of a GEMV op (their stores drained): this CU's count; the last of the CU's claimed units adds
+// them chip-wide
+__device__ __forceinline__ void account(const Args& a, CtlL* c, int op, int lane, unsigned n = 1) {
   unsigned old = 0;
-  if (lane == 0) old = __hip_atomic_fetch_add(&c->acc_w[op % NACC], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (lane == 0) old = __hip_atomic_fetch_add(&c->acc_w[op % NACC], n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   old = __builtin_amdgcn_readfirstlane(old);
-  if ((old & FLAG) && (old & (FLAG - 1)) + 1u == vload(&c->acc_n[op % NACC]) && lane == 0)
+  if ((old & FLAG) && (old & (FLAG - 1)) + n == vload(&c->acc_n[op % NACC]) && lane == 0)
     add_done(done_ctr(a, op, blockIdx.x % NSH), vload(&c->acc_n[op % NACC]));
 }
 
@@ -632,6 +675,14 @@ __device__ __forceinline__ void gemv_unit(const Args& a, unsigned char* smem, in
   const bool dual = kind == OF;
   const int nv = dual ? 2 * R : R;  // values: rows (dual: fc_1 rows, then fc_2 rows)
   const unsigned char* sc0 = slot + (dual ? 2 : 1) * R * K / 2;
+  uint16_t* act = a.act + (size_t)layer * a.act_stride;
+  uint16_t* out = kind == OQ ? act + a.a_qkv : kind == OP ? act + a.a_xp : kind == OF ? act + a.a_g : act + a.a_xo;
+  const uint16_t* res = kind == OP ? (layer == 0 ? a.x0 : a.act + (size_t)(layer - 1) * a.act_stride + a.a_xo)
+                                   : (kind == OD ? act + a.a_xp : nullptr);
+  // the residual row is issued before the dot loop so its latency hides under the arithmetic
+  u32x4 rv = {0u, 0u, 0u, 0u};
+  if (res && lane < nr) rv = ld128_wt(res, (unsigned)((r0 + lane) & ~7) * 2);
+  const int gsh = __builtin_ctz((unsigned)G);
   float part[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) part[i] = 0.0f;
@@ -649,20 +700,16 @@ __device__ __forceinline__ void gemv_unit(const Args& a, unsigned char* smem, in
         xs += xf[8 * k + 2 * q] + xf[8 * k + 2 * q + 1];
       }
     }
-    const int g = (cc * 32) / G;
+    const int g = (cc * 32) >> gsh;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
-      if (i < nv && (i % R) < nr) {
+      if (i < nv && (i >= R ? i - R : i) < nr) {
         const u32x4 w = *(const u32x4*)(slot + (size_t)i * (K / 2) + cc * 16);
         const uint16_t sb = *(const uint16_t*)(sc0 + ((size_t)i * gpr + g) * 2);
         part[i] = fmaf(bf(sb), chunk_dot(w, xf, xs), part[i]);
       }
     }
   }
-  uint16_t* act = a.act + (size_t)layer * a.act_stride;
-  uint16_t* out = kind == OQ ? act + a.a_qkv : kind == OP ? act + a.a_xp : kind == OF ? act + a.a_g : act + a.a_xo;
-  const uint16_t* res = kind == OP ? (layer == 0 ? a.x0 : a.act + (size_t)(layer - 1) * a.act_stride + a.a_xo)
-                                   : (kind == OD ? act + a.a_xp : nullptr);
   float tot[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) tot[i] = i < nv ? wave_sum(part[i]) : 0.0f;
@@ -681,7 +728,6 @@ __device__ __forceinline__ void gemv_unit(const Args& a, unsigned char* smem, in
     } else {
       o = v;
       if (res) {
-        const u32x4 rv = ld128_wt(res, (unsigned)((r0 + lane) & ~7) * 2);
         const uint32_t rw[4] = {rv.x, rv.y, rv.z, rv.w};
         const int e = (r0 + lane) & 7;
         const uint32_t h = (e & 1) ? (rw[e >> 1] >> 16) : (rw[e >> 1] & 0xFFFFu);
@@ -756,7 +802,7 @@ __device__ __forceinline__ void attn_unit(const Args& a, unsigned char* smem, in
     if (!wait_full(c, fill, a, lane)) return;
     const unsigned char* slot = smem + LDS_RING + (fill % NS) * SLOT;
     const int nk = min(KEYS, min(hi, (int)p) - (lo + f * KEYS));
-    if (a.compute) step(slot, slot + KEYS * HS * 2, nk);
+    if (a.compute & 1) step(slot, slot + KEYS * HS * 2, nk);
     release(c, fill, lane);
   }
   if (lo <= p && p < hi) {  // the new key: appended to the cache (un-rotated in this lab build) and scored
@@ -767,7 +813,7 @@ __device__ __forceinline__ void attn_unit(const Args& a, unsigned char* smem, in
       *(u32x4*)(ly.kc + ((size_t)g * a.S + p) * HS + lane * 8) = kv;
       *(u32x4*)(ly.vc + ((size_t)g * a.S + p) * HS + lane * 8) = vv;
     }
-    if (a.compute) {
+    if (a.compute & 1) {
       for (int h = 0; h < QPK; ++h) {
         float d = 0.0f;
 #pragma unroll
@@ -834,8 +880,24 @@ __device__ __forceinline__ void attn_unit(const Args& a, unsigned char* smem, in
 }
 
 __device__ __forceinline__ void consumer(const Args& a, CtlL* c, unsigned char* smem, int ci, int lane) {
+  int last_op = -1;
+  // units whose output stores are issued but not yet drained / counted (all of op pend): counted in one drain when
+  // the consumer moves to another op or would wait for a descriptor (a wait with uncounted units could deadlock:
+  // the loader may need the op complete before it can issue the next descriptor)
+  int pend = -1;
+  unsigned npend = 0;
+  auto flush = [&]() {
+    if (pend >= 0) {
+      drain();
+      account(a, c, pend, lane, npend);
+      tr(a, pend, TR_END + ci, lane);
+      pend = -1;
+      npend = 0;
+    }
+  };
   for (unsigned d = (unsigned)ci;; d += NCONS) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    if (vload(&c->desc_seq) <= d) flush();
     while (vload(&c->desc_seq) <= d) {
       __builtin_amdgcn_s_sleep(1);
       if (__builtin_amdgcn_s_memrealtime() - t0 > TMO) {
@@ -848,17 +910,21 @@ __device__ __forceinline__ void consumer(const Args& a, CtlL* c, unsigned char* 
     if (lane == 0) lsti(&c->cur_d[ci], (int)d);
     const li32* ds = c->desc[d % NDESC];
     const int op = vloadi(&ds[0]), u = vloadi(&ds[1]), fill = vloadi(&ds[2]), nf = vloadi(&ds[3]);
+    if (op != pend) flush();
     if (op < 0) return;
     if (!ensure_input(a, c, smem, op, lane)) return;
+    if (op != last_op) tr(a, op, TR_START + ci, lane);
+    last_op = op;
     if (op_kind(op) == OA) {
       attn_unit(a, smem, op, u, fill, nf, lane);
     } else {
       if (!wait_full(c, fill, a, lane)) return;
-      if (a.compute) gemv_unit(a, smem, op, u, fill, lane);
+      if (a.compute & 1) gemv_unit(a, smem, op, u, fill, lane);
       release(c, fill, lane);
-      drain();
-      account(a, c, op, lane);
+      pend = op;
+      ++npend;
     }
+    if (op_kind(op) == OA) tr(a, op, TR_END + ci, lane);
   }
 }
 
@@ -879,6 +945,7 @@ __global__ void __launch_bounds__(NT) engine3_kernel(const Args* __restrict__ ap
   }
   __syncthreads();
   const int w = __builtin_amdgcn_readfirstlane(wave);
+  if (a.trace && threadIdx.x == 0) a.trace[blockIdx.x] = __builtin_amdgcn_s_memrealtime();
   if (w == 0) claimer(a, c, lane);
   else if (w == 1) loader(a, c, smem, lane);
   else consumer(a, c, smem, w - 2, lane);
@@ -887,6 +954,8 @@ __global__ void __launch_bounds__(NT) engine3_kernel(const Args* __restrict__ ap
 }  // namespace e3
 
 extern "C" int lga_e3_lds_bytes() { return e3::LDS_TOTAL; }
+extern "C" int lga_e3_slot_bytes() { return e3::SLOT; }
+extern "C" int lga_e3_consumers() { return e3::NCONS; }
 extern "C" int lga_e3_counter_words(int L, int G) { return (10 * L * e3::NSH + L * G) * e3::CW; }
 extern "C" int lga_e3_args_bytes() { return (int)sizeof(e3::Args); }
 extern "C" int lga_e3_layer_bytes() { return (int)sizeof(e3::Layer); }
@@ -906,7 +975,8 @@ extern "C" int lga_e3_launch(const void* args_dev, int n_cu, hipStream_t stream)
 extern "C" int lga_e3_fill_args(void* out, const void* layers_dev, int L, int C, int H, int G, int I, int Kp, int S,
                                 int splits, int gq, int gp, int gi, const int* ru, const int* units, int Nq,
                                 const int64_t* pos, const void* x0, void* act, long long act_stride, const int* aoff,
-                                float* ws, unsigned* ctr, unsigned* err, float eps, float scale, int compute) {
+                                float* ws, unsigned* ctr, unsigned* err, float eps, float scale, int compute,
+                                unsigned long long* trace) {
   e3::Args a{};
   a.layers = (const e3::Layer*)layers_dev;
   a.L = L; a.C = C; a.H = H; a.G = G; a.I = I; a.Kp = Kp; a.S = S; a.splits = splits;
@@ -915,6 +985,7 @@ extern "C" int lga_e3_fill_args(void* out, const void* layers_dev, int L, int C,
   a.Nq = Nq; a.pos = pos; a.x0 = (const uint16_t*)x0; a.act = (uint16_t*)act; a.act_stride = act_stride;
   a.a_qkv = aoff[0]; a.a_y = aoff[1]; a.a_xp = aoff[2]; a.a_g = aoff[3]; a.a_xo = aoff[4];
   a.ws = ws; a.ctr = ctr; a.err = err; a.eps = eps; a.scale = scale; a.compute = compute;
+  a.trace = trace;
   memcpy(out, &a, sizeof(a));
   return 0;
 }
