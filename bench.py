@@ -31,6 +31,7 @@ import sys
 import time
 from pathlib import Path
 
+import numpy as np
 import torch
 
 REPO = Path(__file__).resolve().parent
@@ -463,22 +464,28 @@ def main():
                 nonlocal tok
                 tok = next_token(model, pos, tok.view(1, 1), temperature=0.0)
                 pos.add_(1)
-        def run(n):  # n decode steps: whole CHUNK-step graph launches, then single steps
+        def run(n, marks=None):  # n decode steps: whole CHUNK-step graph launches, then single steps
             done = 0
             while use_graph and n - done >= CHUNK > 1:
                 dg.steps()
                 done += CHUNK
+                if marks is not None:  # GPU-side marks between launches (the step-time spread; no host sync)
+                    ev = torch.cuda.Event(enable_timing=True)
+                    ev.record()
+                    marks.append(ev)
             for _ in range(n - done):
                 step()
 
         run(args.warmup)
         torch.cuda.synchronize()
         barrier()
+        marks = []
         t0 = time.perf_counter()
-        run(args.steps)
+        run(args.steps, marks)
         torch.cuda.synchronize()
         barrier()
         elapsed = time.perf_counter() - t0
+        launch_ms = [a.elapsed_time(b) / CHUNK for a, b in zip(marks, marks[1:])]
         gtp.comm.check_errors()  # TP: a timed-out xGMI all-reduce voids the run (raises on every rank)
         if world > 1:
             t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -565,6 +572,10 @@ def main():
                              "note": "seconds / frac: the FIRST (cold) prefill of the process, wall clock, the one "
                                      "reference-style tok/s counts; warm_*: the same prompt run a second time; every "
                                      "Linear's int4 weights dequantized inside the GEMM, flash attention, norms"},
+        "step_time_ms": None if len(launch_ms) < 2 else {
+            "p50": round(float(np.percentile(launch_ms, 50)), 4), "p95": round(float(np.percentile(launch_ms, 95)), 4),
+            "max": round(max(launch_ms), 4), "launches": len(launch_ms),
+            "note": f"per {CHUNK}-step graph launch / {CHUNK}, GPU events between the timed launches"},
         "reference_style_tokens_per_s": round((args.steps + args.warmup + 1) / (prefill_s + elapsed * (
             args.steps + args.warmup + 1) / args.steps), 2),
         "load_s": round(load_s, 2),

@@ -347,6 +347,15 @@ def _check(run, w, kc0, vc0, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, p
             "scale /2": lambda gi, q: torch.softmax(kc[gi, :n] @ q * scale / 2, 0) @ vc[gi, :n],
             "K of group g+1": lambda gi, q: torch.softmax(kc[(gi + 1) % Gr, :n] @ q * scale, 0) @ vc[gi, :n],
             "V of group g+1": lambda gi, q: torch.softmax(kc[gi, :n] @ q * scale, 0) @ vc[(gi + 1) % Gr, :n],
+            "q dims 0-63 only": lambda gi, q: torch.softmax(kc[gi, :n, :64] @ q[:64] * scale, 0) @ vc[gi, :n],
+            "q dims 64-127 only": lambda gi, q: torch.softmax(kc[gi, :n, 64:] @ q[64:] * scale, 0) @ vc[gi, :n],
+            "q dims 0-63 twice": lambda gi, q: torch.softmax(kc[gi, :n, :64] @ q[:64] * 2 * scale, 0) @ vc[gi, :n],
+            "q of group g+1": lambda gi, q: torch.softmax(kc[gi, :n] @ t[(gi + 1) % Gr, 0] * scale, 0) @ vc[gi, :n],
+            "k row as q": lambda gi, q: torch.softmax(kc[gi, :n] @ t[gi, qpk] * scale, 0) @ vc[gi, :n],
+            "q halves swapped": lambda gi, q: torch.softmax(kc[gi, :n] @ torch.cat([q[64:], q[:64]]) * scale, 0)
+            @ vc[gi, :n],
+            "q pairs swapped": lambda gi, q: torch.softmax(kc[gi, :n] @ q.view(-1, 2).flip(1).reshape(-1) * scale, 0)
+            @ vc[gi, :n],
         }
         for k, fn in cand.items():
             print(f"  attn vs '{k}': median per-head rel err {variant(fn):.3f}", flush=True)
