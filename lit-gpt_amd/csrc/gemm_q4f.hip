@@ -58,20 +58,26 @@ __device__ unsigned long long g_q4f_trace[8192 * 4];
 #endif
 constexpr int MAX_SPLITS = 8;  // K-slices per tile (split-K for short prompts)
 
-template <int BM_, int BN_>
+// NW_ waves per workgroup: 8 (one workgroup per CU; the product's tiles), or 4 with a 128 x 128 tile in <= 80 KB of
+// LDS so two independent workgroups share a CU (one's MFMAs under the other's DMA waits). The 4-wave tile is a lab
+// build only (-DLGA_Q4F_W4_LAB, then LGA_Q4F_W4=1; tools/q4f_tile_ab.py): bit-identical, measured slower
+template <int BM_, int BN_, int NW_ = 8>
 struct Tile {
-  static constexpr int BM = BM_, BN = BN_;
-  static constexpr int WM = BM / 64, WN = 8 / WM;  // wave grid
+  static constexpr int BM = BM_, BN = BN_, NW = NW_, NTH = NW * 64;
+  static constexpr int WM = BM / 64, WN = NW / WM;  // wave grid
   static constexpr int WC = BN / WN;               // weight rows (output columns) per wave
   static constexpr int FJ = WC / 16;               // 16-row weight fragments per wave
   static constexpr int A_BYTES = BM * BK * 2;      // one X tile (BM rows x 128 B)
   static constexpr int B_BYTES = BN * BK * 2;      // one bf16 weight tile
   static constexpr int RAW_BYTES = BN * BK / 2;    // one packed weight tile (BN rows x 32 B)
-  static constexpr int SC_BYTES = (BN == 256 ? 8 : 4) * 256;  // one scale stage: a 256-B slot per scale DMA wave
+  // packed weights move 32 rows per DMA: with BN / 32 == NW every wave issues one packed-weight DMA and one scale
+  // DMA; otherwise (8 waves, BN = 128) waves 4-7 the packed rows and waves 0-3 the scales
+  static constexpr bool RAW_ALL = BN / 32 == NW;
+  static constexpr int SC_BYTES = (RAW_ALL ? NW : 4) * 256;  // one scale stage: a 256-B slot per scale DMA wave
   // prefetch depth: X (and bf16 weight) tiles D K-steps ahead, packed weights D + 1 ahead. The 64-row tiles of
   // short prompts do little MFMA work per K-step, so they hide the DMA latency with depth instead (D = 4; the
   // 64 x 256 SwiGLU tile has no LDS for it)
-  static constexpr int D = BM == 64 && BN == 128 ? 4 : (BM == 256 && BN == 256 ? 1 : 2);
+  static constexpr int D = NW == 4 ? 1 : (BM == 64 && BN == 128 ? 4 : (BM == 256 && BN == 256 ? 1 : 2));
   static constexpr int NA = D + 1, NRAW = D + 2, NWB = 2;
   // LDS, 4-bit weights: A[NA] | RAW[NRAW] | SC[NRAW] | WB[2] | misc ; bf16 weights: A[NA] | B[NA] | misc
   static constexpr int OFF_RAW = NA * A_BYTES;
@@ -81,12 +87,13 @@ struct Tile {
   static constexpr int END_BF16 = NA * A_BYTES + NA * B_BYTES;
   static constexpr int OFF_MISC = END_Q4 > END_BF16 ? END_Q4 : END_BF16;  // nf4 table (64 B), last-arriver flag
   static constexpr int LDS_BYTES = OFF_MISC + 128;
-  static constexpr int RPT = BN * BK / 2 / NT;     // packed bytes each thread dequantizes (8 or 16)
+  static constexpr int RPT = BN * BK / 2 / NTH;    // packed bytes each thread dequantizes (8 or 16)
   static constexpr int TPR = 32 / RPT;             // dequant threads per weight row
   // DMAs per wave per stage: X pieces (8 rows x 128 B); bf16 weight pieces; packed weight + scale DMAs
-  static constexpr int APW = BM / 64, BPW = BN / 64, RAWPW = BN == 256 ? 2 : 1;
-  static_assert(WM * WN == 8 && FJ >= 1 && RPT >= 8, "tile shape");
-  static_assert(LDS_BYTES <= 163840, "LDS budget");
+  static constexpr int APW = BM / (8 * NW), BPW = BN / (8 * NW), RAWPW = RAW_ALL ? 2 : 1;
+  static_assert(WM * WN == NW && FJ >= 1 && RPT >= 8 && APW >= 1, "tile shape");
+  static_assert(RAW_ALL || (NW == 8 && BN == 128), "packed-weight DMA roles");
+  static_assert(LDS_BYTES <= (NW == 4 ? 81920 : 163840), "LDS budget (4 waves: two workgroups per CU)");
 };
 
 struct Args {
@@ -173,8 +180,8 @@ __device__ __forceinline__ void glds_rows8(const uint16_t* src, int ld, int row,
 
 // FMT 0 int4-g (bf16 scales), 1 nf4 (fp32 absmax), 2 bf16 weights. DUAL: fc_1 || fc_2 + SwiGLU (tile = BN / 2
 // columns of each; the weight tile's rows [0, BN/2) are fc_1's, [BN/2, BN) fc_2's).
-template <int FMT, bool DUAL, int BM_, int BN_>
-__global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
+template <int FMT, bool DUAL, int BM_, int BN_, int NW_ = 8>
+__global__ void __launch_bounds__(NW_ * 64, NW_ == 4 ? 2 : 1) gemm_q4f_kernel(Args a) {
   if (a.grp) {  // grouped: this m-tile's expert and row range (surplus tiles of the launch's upper bound exit here)
     const int mi = (blockIdx.x / a.splits) % a.mt;
     if (mi >= a.grp[0]) return;
@@ -186,7 +193,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
       if (a.sc2) a.sc2 = (const unsigned char*)a.sc2 + e * a.es;
     }
   }
-  using T = Tile<BM_, BN_>;
+  using T = Tile<BM_, BN_, NW_>;
   constexpr int BM = T::BM, BN = T::BN, NA = T::NA, NRAW = T::NRAW, FJ = T::FJ, WC = T::WC;
   constexpr int A_BYTES = T::A_BYTES, B_BYTES = T::B_BYTES, RAW_BYTES = T::RAW_BYTES, SC_BYTES = T::SC_BYTES;
   constexpr int OFF_RAW = T::OFF_RAW, OFF_SC = T::OFF_SC, OFF_WB = T::OFF_WB, OFF_MISC = T::OFF_MISC;
@@ -264,9 +271,9 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
     for (int i = 0; i < T::BPW; ++i) glds<16>(bsrc[i] + (size_t)lk * BK * 2, B + (wave * T::BPW + i) * 8 * 128);
   };
   // packed weight tile (1 KB = 32 rows x 32 B per DMA) and its scales (256 B = 64 rows x 4 B per DMA).
-  // BN = 256: every wave one of each (waves 4-7 repeat the scales of 0-3 into their own slots);
-  // BN = 128: waves 4-7 the packed rows, waves 0-3 the scales (2, 3 repeat 0, 1): one DMA per wave.
-  const int raw_wave = BN == 256 ? wave : wave - 4;
+  // RAW_ALL (BN = 32 NW): every wave one of each (waves past BN / 64 repeat earlier scale blocks into their own
+  // slots); 8 waves, BN = 128: waves 4-7 the packed rows, waves 0-3 the scales (2, 3 repeat 0, 1): one DMA per wave.
+  const int raw_wave = T::RAW_ALL ? wave : wave - 4;
   const unsigned char* rsrc =
       wrow_ptr(max(raw_wave, 0) * 32 + (lane >> 1)) + (size_t)kt0 * (BK / 2) + (lane & 1) * 16;
   const int sw = wave & (BN / 64 - 1);  // the 64-row scale block this wave fetches
@@ -278,7 +285,7 @@ __global__ void __launch_bounds__(NT, 1) gemm_q4f_kernel(Args a) {
     unsigned char* S = lds + OFF_SC + (lk % NRAW) * SC_BYTES + wave * 256;
     const size_t si = sc_row + ((kt * BK) >> gshift);
     const unsigned char* sp = sc_base + (FMT == 0 ? (si & ~(size_t)1) * 2 : si * 4);
-    if (BN == 256) {
+    if (T::RAW_ALL) {
       glds<16>(rsrc + (size_t)lk * (BK / 2), R + wave * 1024);
       glds<4>(sp, S);
     } else if (wave >= 4) {
@@ -641,13 +648,26 @@ bool q4f_fits(int M, int N, int K, int group, int fmt) {
   return group >= lga::pf::BK && (group & (group - 1)) == 0 && K % group == 0;
 }
 
+// the 4-wave 128 x 128 tile for M > 128: lab builds only (make lab-lib LABFLAGS=-DLGA_Q4F_W4_LAB), then LGA_Q4F_W4=1
+bool w4_tiles() {
+#ifdef LGA_Q4F_W4_LAB
+  static const bool on = [] {
+    const char* e = getenv("LGA_Q4F_W4");
+    return e && atoi(e) == 1;
+  }();
+  return on;
+#else
+  return false;
+#endif
+}
+
 // Launch plan: tile shape by M, then K-slices so the grid covers the CUs (>= 2 waves of tiles is left whole).
 struct Plan {
   int bm, bn, mt, tn, tiles, splits;
 };
 Plan q4f_plan(int M, int N, int K, bool dual) {
   Plan p;
-  p.bm = M <= 128 ? 64 : 256;
+  p.bm = M <= 128 ? 64 : (w4_tiles() ? 128 : 256);
   p.bn = p.bm == 64 ? (dual ? 256 : 128) : 128;
   if (p.bm == 256) {
     // 256 x 256 tiles (64 x 128 outputs per wave: a third less LDS fragment traffic per FLOP) where their rounds
@@ -671,17 +691,20 @@ Plan q4f_plan(int M, int N, int K, bool dual) {
   return p;
 }
 
-template <int FMT, bool DUAL, int BM, int BN>
+template <int FMT, bool DUAL, int BM, int BN, int NW = 8>
 int launch_tile(Args a, const Plan& p, hipStream_t stream) {
   a.mt = p.mt;
   a.splits = p.splits;
   const unsigned grid = (unsigned)(p.tiles * p.splits);
-  lga::pf::gemm_q4f_kernel<FMT, DUAL, BM, BN><<<grid, lga::pf::NT, 0, stream>>>(a);
+  lga::pf::gemm_q4f_kernel<FMT, DUAL, BM, BN, NW><<<grid, NW * 64, 0, stream>>>(a);
   LGA_LAUNCH_RETURN();
 }
 
 template <int FMT, bool DUAL>
 int launch_q4f(Args a, const Plan& p, hipStream_t stream) {
+#ifdef LGA_Q4F_W4_LAB
+  if (p.bm == 128) return launch_tile<FMT, DUAL, 128, 128, 4>(a, p, stream);
+#endif
   if (p.bm == 256 && p.bn == 256) return launch_tile<FMT, DUAL, 256, 256>(a, p, stream);
   if (p.bm == 256) return launch_tile<FMT, DUAL, 256, 128>(a, p, stream);
   if (DUAL || p.bn == 256) return launch_tile<FMT, DUAL, 64, 256>(a, p, stream);
@@ -697,7 +720,7 @@ size_t ws_need(const Plan& p, int M, int N, bool dual) {
 // two launches over column ranges of the same output (Llama-2-7B qkv at 2048 tokens: one big round over 8192 columns
 // + one small round over 4096, instead of three small rounds). Returns the big-tile column count (0: no split).
 int q4f_big_columns(int M, int N, int K) {
-  if (M <= 128 || getenv("LGA_Q4F_BN")) return 0;
+  if (M <= 128 || getenv("LGA_Q4F_BN") || w4_tiles()) return 0;
   const int mt = (M + 255) / 256;
   if (256 % mt || K / lga::pf::BK < 8) return 0;
   const int cols_per_round = 256 / mt * 256;
