@@ -50,7 +50,12 @@ __device__ __forceinline__ float butterfly(float* a, int lane) {
     const bool h = lane & D;
 #pragma unroll
     for (int i = 0; i < n; ++i) {
-      const float send = h ? a[i] : a[i + n], keep = h ? a[i + n] : a[i];
+      // the pair as register values first: on two loads of the array, LLVM folds the selects below into ONE load
+      // through a selected pointer, and the dynamically indexed array then lives in scratch (a store + load round
+      // trip per level in every wave's tail; round 6)
+      float lo = a[i], hi = a[i + n];
+      asm volatile("" : "+v"(lo), "+v"(hi));
+      const float send = h ? lo : hi, keep = h ? hi : lo;
       float recv;
       if (D == 8) recv = LGA_DPP(send, 0x128);  // row_ror:8 == xor 8 inside a 16-lane row
       else recv = __shfl_xor(send, D);

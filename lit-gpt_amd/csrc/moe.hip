@@ -192,7 +192,7 @@ static int dispatch_down_pair(const GemvArgs& a, const uint16_t* residual, uint1
     case 4: launch_down_pair<2, 4, FMT>(a, residual, y, scratch, counters, stream); break;
     case 5:
     case 6: launch_down_pair<2, 6, FMT>(a, residual, y, scratch, counters, stream); break;
-    case 7:
+    case 7: launch_down_pair<4, 7, FMT>(a, residual, y, scratch, counters, stream); break;  // as gemv.hip's case 7
     case 8: launch_down_pair<2, 8, FMT>(a, residual, y, scratch, counters, stream); break;
     default: launch_down_pair<2, 16, FMT>(a, residual, y, scratch, counters, stream); break;
   }
@@ -407,5 +407,5 @@ extern "C" int lga_moe_group(const int32_t* expert_ids, int T, int k, int n_expe
 int lga::preload_moe() {  // the sparse-MoE prefill's routing, grouping and combine kernels
   return lga::preload(lga::moe_route_kernel) + lga::preload(lga::moe_combine_kernel) +
          lga::preload(lga::moe_group_kernel) + lga::preload(lga::moe_gate_route_kernel<2, 0, true>) +
-         lga::preload(lga::moe_gate_route_kernel<2, 1, true>) + lga::preload(lga::moe_down_pair_kernel<2, 8, 0>);
+         lga::preload(lga::moe_gate_route_kernel<2, 1, true>) + lga::preload(lga::moe_down_pair_kernel<4, 7, 0>) + lga::preload(lga::moe_down_pair_kernel<2, 8, 0>);
 }
