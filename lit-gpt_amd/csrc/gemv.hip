@@ -133,6 +133,13 @@ static int dispatch(const GemvArgs& a, int variant, hipStream_t stream) {
     // the out-projection shape (residual epilogue, 2048..4096 rows, K <= 6144): 2 rows per wave, twice the
     // workgroups — attn.proj 4096 x 4096 3.81 vs 4.18 us (tools/gemv_variants.py, round 5); qkv / down unchanged
     if (!DUAL && !a.eidx && a.residual && a.N >= 2048 && a.N <= 4096 && cpt <= 3) variant |= 8;
+    // and for the router gate (N <= 64: 4 rows per wave left half the rows as repeats) and the mid-size qkv
+    // projections with the RMSNorm fused (N 4096..8192: Mixtral's 6,144 rows) — gate 3.14 -> 2.70 us, Mixtral qkv
+    // 5.71 -> 5.48 (tools/gemv_variants.py GEMV_SHAPES=mixtral, round 6). Not for row-parallel projections (no norm):
+    // their fused all-reduce form (gemv_ar.hip) keeps the 4-row grouping bit for bit. moe_gate_route_kernel uses the
+    // same 2-row body as the gate GEMV.
+    if (!DUAL && !a.eidx && !a.residual && cpt <= 3 && (a.N <= 64 || (a.norm_w && a.N >= 4096 && a.N <= 8192)))
+      variant |= 8;
   }
   // A persistent, double-buffered streaming form of this kernel (few workgroups per CU walking row tiles) measured
   // 10-70 % slower on every decode shape (tools/gemv_sweep.py, round 1) and was dropped.

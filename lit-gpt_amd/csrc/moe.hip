@@ -103,15 +103,15 @@ __global__ void __launch_bounds__(64) moe_route_kernel(const uint16_t* __restric
 }
 
 // Decode (one token): the router gate GEMV and the routing in ONE single-workgroup launch. The E <= 8 gate rows are
-// the decode GEMV body's (lga_q4_gemv's arithmetic, fused RMSNorm included: 4 waves x 4 rows, rows past E repeat
-// row E-1), left in LDS as the bf16 logits lga_q4_gemv would store; thread 0 then routes them exactly as
+// the decode GEMV body's (lga_q4_gemv's arithmetic for N <= 64, fused RMSNorm included: 4 waves x 2 rows, rows past E
+// repeat row E-1), left in LDS as the bf16 logits lga_q4_gemv would store; thread 0 then routes them exactly as
 // moe_route_kernel does — the pair lga_q4_gemv + lga_moe_route bit for bit, one launch ramp instead of two.
 template <int CPT, int FMT, bool NORM>
 __global__ void __launch_bounds__(256) moe_gate_route_kernel(GemvArgs a, int k, int32_t* __restrict__ ids,
                                                              uint16_t* __restrict__ probs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ KV sq[8];
-  gemv_q4_body<4, CPT, FMT, false, NORM, false, 4, true>(a, 0, smem);
+  gemv_q4_body<2, CPT, FMT, false, NORM, false, 4, true>(a, 0, smem);
   __syncthreads();
   if (threadIdx.x == 0) route_row(gemv_out_lds(smem, a.K), a.N, k, ids, probs, sq);
 }

@@ -5,6 +5,7 @@ usage: python tools/gemv_variants.py lib1.so [lib2.so ...]   (graph of back-to-b
        GEMV_VARIANTS=-1,4,6 ... times each launch variant (gemv.hip: bit 2 streaming form, bit 1 one row per tile,
        bits 4..7 workgroups per CU) of every library
 """
+import os
 import sys
 from pathlib import Path
 
@@ -17,6 +18,9 @@ from lit_gpt import ops  # noqa: E402
 SHAPES = {"qkv": (12288, 4096, False, "norm"), "o_proj": (4096, 4096, False, "res"),
           "gate_up": (11008, 4096, True, "norm"), "down": (4096, 11008, False, "res"),
           "lm_head": (32000, 4096, False, "norm")}
+if os.environ.get("GEMV_SHAPES") == "mixtral":  # Mixtral-8x7B decode shapes (qkv with 8 kv heads, attn.proj)
+    SHAPES = {"mix_qkv": (6144, 4096, False, "norm"), "mix_proj": (4096, 4096, False, "res"),
+              "gate": (8, 4096, False, "norm")}
 dev = torch.device("cuda")
 data = {}
 for name, (N, K, dual, kind) in SHAPES.items():
