@@ -12,6 +12,7 @@ consumers computing nothing (transport + hand-off floor).
 """
 
 import argparse
+import os
 import ctypes
 import math
 import sys
@@ -360,6 +361,14 @@ def _check(run, w, kc0, vc0, x0, act, offs, stride, Nq, Kp, C, Ir, Hr, Gr, hs, p
         for k, fn in cand.items():
             print(f"  attn vs '{k}': median per-head rel err {variant(fn):.3f}", flush=True)
         print(f"  reference per-head rel err median {d.median().item():.3f}", flush=True)
+        dump_path = os.environ.get("E3_ATTN_DUMP")
+        if dump_path:  # the first two groups' inputs and the engine's outputs, for offline analysis
+            nsp_ = ews.numel() // (L_ * Hr * (hs + 4))
+            np.savez(dump_path, q=t[:2].cpu().numpy(), kc=kc[:2, :pos + 1].cpu().numpy(),
+                     vc=vc[:2, :pos + 1].cpu().numpy(), y=ey[:2].cpu().numpy(),
+                     part=ews[:2 * nsp_ * (hs + 4)].view(2, nsp_, hs + 4).cpu().numpy(),
+                     scale=np.float32(scale), pos=np.int64(pos))
+            print(f"  dumped {dump_path}", flush=True)
         # per split: the engine's published (m, l, o) of layer 0 against the split's own attention
         nsp = ews.numel() // (L_ * Hr * (hs + 4))
         part = ews[:Hr * nsp * (hs + 4)].view(Hr, nsp, hs + 4)
