@@ -78,3 +78,49 @@ def test_missing_library_fails_loudly(tmp_path):
 
     with pytest.raises(ops.NativeLibraryError, match="no CPU fallback"):
         ops.load_library(tmp_path / "nope.so")
+
+
+def _kernel_scratch(lib_path):
+    """{kernel symbol: private segment bytes per lane} of every gfx950 kernel in the library: the clang offload
+    bundles embedded in the .so (one per translation unit), each kernel's `.private_segment_fixed_size` from the code
+    object's metadata note (llvm-readelf --notes)."""
+    import os
+    import struct
+    import tempfile
+
+    readelf = Path("/opt/rocm/lib/llvm/bin/llvm-readelf")
+    if not readelf.is_file():
+        pytest.skip("llvm-readelf not found")
+    data = Path(lib_path).read_bytes()
+    out, pos = {}, 0
+    while (i := data.find(b"__CLANG_OFFLOAD_BUNDLE__", pos)) >= 0:
+        n, off = struct.unpack_from("<Q", data, i + 24)[0], i + 32
+        for _ in range(n):
+            o, sz, ts = struct.unpack_from("<QQQ", data, off)
+            triple = data[off + 24:off + 24 + ts].decode()
+            off += 24 + ts
+            if "gfx950" not in triple or not sz:
+                continue
+            with tempfile.NamedTemporaryFile(suffix=".co", delete=False) as f:
+                f.write(data[i + o:i + o + sz])
+            notes = subprocess.run([str(readelf), "--notes", f.name], capture_output=True, text=True).stdout
+            os.unlink(f.name)
+            for blk in notes.split("  - .")[1:]:
+                name = re.search(r"\.name:\s+(\S+)", blk)
+                scratch = re.search(r"\.private_segment_fixed_size:\s+(\d+)", blk)
+                if name and scratch:
+                    out[name.group(1)] = int(scratch.group(1))
+        pos = i + 1
+    return out
+
+
+def test_decode_kernels_use_no_scratch(lib_path):
+    """Round 6 found every decode GEMV kernel spilling its butterfly partials to scratch (a select of two array loads
+    folded into one load through a selected pointer: a scratch round trip per butterfly level in each wave's tail).
+    Guard: no decode-path kernel (GEMV, streaming GEMV, MoE, attention, all-reduce, sampling) has a private segment.
+    The prefill fallback GEMM (gemm.hip, shapes the fused kernel declines) is the one known exception."""
+    scratch = _kernel_scratch(lib_path)
+    assert len(scratch) > 100, len(scratch)
+    decode = re.compile(r"gemv|attn_kernel|moe_|allreduce|comm|sample|argmax|rope|rmsnorm")
+    bad = {k: v for k, v in scratch.items() if v and decode.search(k)}
+    assert not bad, bad
