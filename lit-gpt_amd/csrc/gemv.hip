@@ -158,8 +158,8 @@ static int dispatch(const GemvArgs& a, int variant, hipStream_t stream) {
     case 4: LGA_L(2, 4, 4); break;
     case 5:
     case 6: LGA_L(2, 4, 6); break;
-    case 7: LGA_L(4, 4, 7); break;  // K 12,320..14,336 (Mixtral experts' proj, Llama-2-13B mlp.proj): 4 rows per wave,
-                                    // exactly 7 chunks per lane (round 6: the routed pair 17.0 -> 15.5-16.2 us)
+    case 7: LGA_L(2, 4, 7); break;  // K 12,320..14,336 (Mixtral experts' proj, Llama-2-13B mlp.proj): exactly 7 chunks
+                                    // per lane, 2 rows per wave as moe.hip's paired down-projection (bit-identical)
     case 8: LGA_L(2, 4, 8); break;
     default:
       if (cpt <= 16) {

@@ -123,13 +123,13 @@ __global__ void __launch_bounds__(256) moe_gate_route_kernel(GemvArgs a, int k, 
 // add); the second reads them with sc1 loads, adds both experts in ascending id order with lga_moe_combine's rounding
 // points and the residual, and re-arms the block's counter. Bit-identical to lga_q4_gemv_experts + lga_moe_combine.
 constexpr int kPairStride = 64;  // per-row-block counters 256 B apart
-template <int RPR, int CPT, int FMT>
-__global__ void __launch_bounds__(256) moe_down_pair_kernel(GemvArgs a, const uint16_t* __restrict__ residual,
+template <int RPR, int CPT, int FMT, int NW = 4>
+__global__ void __launch_bounds__(NW * 64) moe_down_pair_kernel(GemvArgs a, const uint16_t* __restrict__ residual,
                                                             uint16_t* __restrict__ y, uint16_t* __restrict__ scratch,
                                                             unsigned* __restrict__ counters) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ unsigned s_ticket;
-  constexpr int ROWS = 4 * RPR, PIECES = ROWS / 8;  // the workgroup's rows, their 16-B pieces
+  constexpr int ROWS = NW * RPR, PIECES = ROWS / 8;  // the workgroup's rows, their 16-B pieces
   const int b = blockIdx.x, slot = blockIdx.y, t = threadIdx.x;
   const int row0 = b * ROWS;
   // everything the combine needs, read up front: both ids (order), both probabilities, this block's residual rows
@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(256) moe_down_pair_kernel(GemvArgs a, const ui
   const float p0 = bf2f(a.probs[0]), p1 = bf2f(a.probs[1]);
   uint4 rv = make_uint4(0, 0, 0, 0);
   if (t < PIECES) rv = ((const uint4*)(residual + row0))[t];
-  gemv_q4_body<RPR, CPT, FMT, false, false, false, 4, true>(a, b, smem);
+  gemv_q4_body<RPR, CPT, FMT, false, false, false, NW, true>(a, b, smem);
   __syncthreads();
   const uint4* mine = (const uint4*)gemv_out_lds(smem, a.K);
   const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc((void*)scratch, (short)0, 2 * a.N * 2, 0x00020000);
@@ -174,11 +174,12 @@ __global__ void __launch_bounds__(256) moe_down_pair_kernel(GemvArgs a, const ui
   if (t == 0) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // both arrived: re-arm
 }
 
-template <int RPR, int CPT, int FMT>
+template <int RPR, int CPT, int FMT, int NW = 4>
 static void launch_down_pair(const GemvArgs& a, const uint16_t* residual, uint16_t* y, uint16_t* scratch,
                              unsigned* counters, hipStream_t stream) {
-  const dim3 grid(a.N / (4 * RPR), 2);
-  moe_down_pair_kernel<RPR, CPT, FMT><<<grid, 256, gemv_lds_bytes(a.K), stream>>>(a, residual, y, scratch, counters);
+  const dim3 grid(a.N / (NW * RPR), 2);
+  moe_down_pair_kernel<RPR, CPT, FMT, NW><<<grid, NW * 64, gemv_lds_bytes(a.K), stream>>>(a, residual, y, scratch,
+                                                                                           counters);
 }
 
 // gemv.hip dispatch's one-shot tile for an expert GEMV of this K (variant 0)
@@ -192,7 +193,9 @@ static int dispatch_down_pair(const GemvArgs& a, const uint16_t* residual, uint1
     case 4: launch_down_pair<2, 4, FMT>(a, residual, y, scratch, counters, stream); break;
     case 5:
     case 6: launch_down_pair<2, 6, FMT>(a, residual, y, scratch, counters, stream); break;
-    case 7: launch_down_pair<4, 7, FMT>(a, residual, y, scratch, counters, stream); break;  // as gemv.hip's case 7
+    // K 14,336 (Mixtral): 8 waves x 2 rows, exactly 7 chunks per lane — 15.5 vs 16.1 us for 4 waves x 4 rows
+    // (tools/moe_down_ab.py, round 6); the per-row arithmetic is gemv.hip's case 7 (2 rows per wave), bit for bit
+    case 7: launch_down_pair<2, 7, FMT, 8>(a, residual, y, scratch, counters, stream); break;
     case 8: launch_down_pair<2, 8, FMT>(a, residual, y, scratch, counters, stream); break;
     default: launch_down_pair<2, 16, FMT>(a, residual, y, scratch, counters, stream); break;
   }
@@ -407,5 +410,5 @@ extern "C" int lga_moe_group(const int32_t* expert_ids, int T, int k, int n_expe
 int lga::preload_moe() {  // the sparse-MoE prefill's routing, grouping and combine kernels
   return lga::preload(lga::moe_route_kernel) + lga::preload(lga::moe_combine_kernel) +
          lga::preload(lga::moe_group_kernel) + lga::preload(lga::moe_gate_route_kernel<2, 0, true>) +
-         lga::preload(lga::moe_gate_route_kernel<2, 1, true>) + lga::preload(lga::moe_down_pair_kernel<4, 7, 0>) + lga::preload(lga::moe_down_pair_kernel<2, 8, 0>);
+         lga::preload(lga::moe_gate_route_kernel<2, 1, true>) + lga::preload(lga::moe_down_pair_kernel<2, 7, 0, 8>) + lga::preload(lga::moe_down_pair_kernel<2, 8, 0>);
 }
